@@ -1,0 +1,45 @@
+"""Pin the CPU oracle against golden vectors produced by transformers 5.15.0
+(tests/golden/make_golden.py).  CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+from gonova_tts_amd.weights import make_vocoder_weights, make_acoustic_weights
+from oracle.vocoder import vocoder_forward
+from oracle.acoustic import acoustic_forward
+
+G = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_v1.npz"))
+
+
+def test_weight_generator_is_pinned():
+    for key, fn in (("voc", make_vocoder_weights), ("ac", make_acoustic_weights)):
+        w = fn(seed=0)
+        names = list(G[f"{key}_weight_names"])
+        assert sorted(w) == names
+        sums = np.array([float(np.asarray(w[n], np.float64).sum()) for n in names])
+        np.testing.assert_allclose(sums, G[f"{key}_weight_sums"], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("tag", ["voc_a", "voc_b"])
+def test_vocoder_oracle_matches_golden(tag):
+    w = make_vocoder_weights(seed=0)
+    wav = vocoder_forward(G[f"{tag}_mel"], w)
+    assert wav.shape == G[f"{tag}_wav"].shape
+    np.testing.assert_allclose(wav, G[f"{tag}_wav"], atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("tag", ["ac_a", "ac_b"])
+def test_acoustic_oracle_matches_golden(tag):
+    w = make_acoustic_weights(seed=0)
+    o = acoustic_forward(G[f"{tag}_ids"], w)
+    np.testing.assert_array_equal(o["durations"], G[f"{tag}_dur"])
+    np.testing.assert_allclose(o["pitch"], G[f"{tag}_pitch"], atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(o["energy"], G[f"{tag}_energy"], atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(o["mel"], G[f"{tag}_mel"], atol=1e-4, rtol=1e-4)
+
+
+def test_end_to_end_oracle_matches_golden():
+    o = acoustic_forward(G["ac_a_ids"], make_acoustic_weights(seed=0))
+    wav = vocoder_forward(o["mel"], make_vocoder_weights(seed=0))
+    np.testing.assert_allclose(wav, G["e2e_wav"], atol=1e-5, rtol=1e-4)

@@ -1,0 +1,67 @@
+"""Build libtts_hip.so in-tree with hipcc for gfx950 (no JIT cache, no pip install).
+
+    python -m gonova_tts_amd.build          (or __graft_entry__.build())
+
+Each csrc/*.hip / *.cpp is compiled to build/<name>.o (skipped when newer than
+its sources/headers), then linked into gonova-tts_amd/libtts_hip.so which
+travels with the repo snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(PKG, "build")
+LIB = os.path.join(PKG, "libtts_hip.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+          "-Wno-unused-result", "-I" + CSRC, "-I" + os.path.join(ROOT, "include")]
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.h"))
+
+
+def _compile(src, force):
+    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+    newest_dep = max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _headers()])
+    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
+        return obj, False
+    cmd = [HIPCC] + CFLAGS + ["-x", "hip", "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-8000:]}")
+    return obj, True
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = _sources()
+    jobs = min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        results = list(ex.map(lambda s: _compile(s, force), srcs))
+    objs = [o for o, _ in results]
+    rebuilt = any(r for _, r in results)
+    if rebuilt or not os.path.exists(LIB) or force:
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")
+        if verbose:
+            print(f"[gonova_tts_amd] built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,116 @@
+// Shared device/host helpers for the gfx950 (CDNA4) TTS kernels.
+//
+// Everything here is written for MI355X directly: 64-lane wavefronts, the
+// gfx950 MFMA builtins (32x32x16 f16/bf16, 32x32x2 f32) and 16-byte vector
+// memory accesses.  No portability layer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tts {
+
+enum DType : int { DT_F32 = 0, DT_F16 = 1, DT_BF16 = 2 };
+
+typedef _Float16 half_t;
+typedef __bf16 bf16_t;
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// ---------------------------------------------------------------------------
+// MFMA traits: one 32x32 output tile per wave-instruction.
+//   16-bit: v_mfma_f32_32x32x16_{f16,bf16}; lane l holds A[l&31][8*(l>>5)+e],
+//           B[8*(l>>5)+e][l&31], e = 0..7 (K = 16 per instruction).
+//   f32   : v_mfma_f32_32x32x2_f32; lane l holds A[l&31][l>>5], B[l>>5][l&31].
+//   C/D   : col = l&31, row = (r&3) + 8*(r>>2) + 4*(l>>5), r = 0..15.
+// ---------------------------------------------------------------------------
+template <typename T> struct Mfma;
+
+template <> struct Mfma<half_t> {
+  static constexpr int KSTEP = 16;  // K per instruction
+  static constexpr int KPL = 8;     // K elements per lane
+  typedef half8 frag;
+  __device__ static inline f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <> struct Mfma<bf16_t> {
+  static constexpr int KSTEP = 16;
+  static constexpr int KPL = 8;
+  typedef bf16x8 frag;
+  __device__ static inline f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <> struct Mfma<float> {
+  static constexpr int KSTEP = 2;
+  static constexpr int KPL = 1;
+  typedef float frag;
+  __device__ static inline f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Scalar conversions
+// ---------------------------------------------------------------------------
+template <typename T> __device__ __host__ inline float to_f32(T v) { return (float)v; }
+template <typename T> __device__ __host__ inline T from_f32(float v) { return (T)v; }
+
+// 4 consecutive elements <-> float4 (one 8-byte (16-bit) or 16-byte (f32) access)
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+  typedef f32x4 type;
+  __device__ static inline f32x4 load(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+  __device__ static inline void store(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+};
+template <> struct Vec4<half_t> {
+  __device__ static inline f32x4 load(const half_t* p) {
+    half4 h = *reinterpret_cast<const half4*>(p);
+    return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+  }
+  __device__ static inline void store(half_t* p, f32x4 v) {
+    half4 h = {(half_t)v[0], (half_t)v[1], (half_t)v[2], (half_t)v[3]};
+    *reinterpret_cast<half4*>(p) = h;
+  }
+};
+template <> struct Vec4<bf16_t> {
+  __device__ static inline f32x4 load(const bf16_t* p) {
+    bf16x4 h = *reinterpret_cast<const bf16x4*>(p);
+    return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+  }
+  __device__ static inline void store(bf16_t* p, f32x4 v) {
+    bf16x4 h = {(bf16_t)v[0], (bf16_t)v[1], (bf16_t)v[2], (bf16_t)v[3]};
+    *reinterpret_cast<bf16x4*>(p) = h;
+  }
+};
+
+// 16-byte chunk of T (8 x 16-bit or 4 x f32)
+template <typename T> struct Chunk16 {
+  static constexpr int N = 16 / sizeof(T);
+};
+
+__device__ inline float leaky(float x, float slope) { return x >= 0.f ? x : x * slope; }
+
+// activation codes shared by host and device
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2, ACT_LRELU = 3, ACT_SILU = 4 };
+
+__device__ inline float apply_act(float v, int act, float slope) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_TANH: return tanhf(v);
+    case ACT_LRELU: return leaky(v, slope);
+    case ACT_SILU: return v / (1.f + __expf(-v));
+    default: return v;
+  }
+}
+
+}  // namespace tts

@@ -1,0 +1,112 @@
+// Small bandwidth-bound kernels around the vocoder GEMMs.
+#include "common.h"
+#include "kernels.h"
+
+namespace tts {
+
+// mel f32 [B][T][C] (row stride smr) -> (x - mean) / scale in the compute dtype,
+// [B][T][C] contiguous.  HF:1445-1446 (normalize_before).
+template <typename T>
+__global__ void mel_in_kernel(const float* __restrict__ mel, long long smb, int smr,
+                              const float* __restrict__ mean, const float* __restrict__ scale,
+                              T* __restrict__ out, int T_, int C) {
+  const int b = blockIdx.y;
+  const long long n = (long long)T_ * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int t = (int)(i / C);
+    const int c = (int)(i - (long long)t * C);
+    float v = mel[b * smb + (long long)t * smr + c];
+    if (mean) v = (v - mean[c]) / scale[c];
+    out[b * n + i] = from_f32<T>(v);
+  }
+}
+
+hipError_t launch_mel_in(int dtype, const float* mel, long long smb, int smr, const float* mean,
+                         const float* scale, void* out, int B, int T_, int C, hipStream_t s) {
+  const long long n = (long long)T_ * C;
+  dim3 grid((unsigned)((n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024), B);
+  switch (dtype) {
+    case DT_F32: hipLaunchKernelGGL(mel_in_kernel<float>, grid, dim3(256), 0, s, mel, smb, smr, mean, scale, (float*)out, T_, C); break;
+    case DT_F16: hipLaunchKernelGGL(mel_in_kernel<half_t>, grid, dim3(256), 0, s, mel, smb, smr, mean, scale, (half_t*)out, T_, C); break;
+    case DT_BF16: hipLaunchKernelGGL(mel_in_kernel<bf16_t>, grid, dim3(256), 0, s, mel, smb, smr, mean, scale, (bf16_t*)out, T_, C); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// out[k*B + b] = in[b] * mult[k] + add[k]  (per-utterance row counts of every stage)
+__global__ void lens_kernel(const int* __restrict__ in, int* __restrict__ out, int B, int4 m0, int4 m1,
+                            int4 a0, int4 a1, int n) {
+  const int b = threadIdx.x + blockIdx.x * blockDim.x;
+  if (b >= B) return;
+  const int v = in[b];
+  const int mult[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+  const int add[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  for (int k = 0; k < n; ++k) out[k * B + b] = v * mult[k] + add[k];
+}
+
+hipError_t launch_lens(const int* in, int* out, int B, const int* mult, const int* add, int n,
+                       hipStream_t s) {
+  if (n > 8) return hipErrorInvalidValue;
+  int m[8] = {0}, a[8] = {0};
+  for (int i = 0; i < n; ++i) { m[i] = mult[i]; a[i] = add[i]; }
+  hipLaunchKernelGGL(lens_kernel, dim3((B + 255) / 256), dim3(256), 0, s, in, out, B,
+                     make_int4(m[0], m[1], m[2], m[3]), make_int4(m[4], m[5], m[6], m[7]),
+                     make_int4(a[0], a[1], a[2], a[3]), make_int4(a[4], a[5], a[6], a[7]), n);
+  return hipGetLastError();
+}
+
+// conv_post: wav[b][t] = tanh(bias + sum_{j,c} w[j][c] * lrelu(x[b][t+j-pad][c], slope)),
+// zero for t >= x_len[b].  HF:1464-1466.  One thread per output sample; the
+// (256 + k - 1) x C input tile is staged through LDS in fp32.
+template <typename T, int C>
+__global__ __launch_bounds__(256) void conv_post_kernel(const T* __restrict__ x, const int* __restrict__ x_len,
+                                                       int T_, const float* __restrict__ w, float bias, int k,
+                                                       float slope, float* __restrict__ wav, long long swb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* ws = reinterpret_cast<float*>(smem);            // [k][C]
+  float* xs = ws + k * C;                                 // [(256+k-1)][C+1]
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * 256;
+  const int len = x_len ? min(x_len[b], T_) : T_;
+  const int pad = (k - 1) / 2;
+  const int rows = 256 + k - 1;
+  for (int i = threadIdx.x; i < k * C; i += 256) ws[i] = w[i];
+  const T* xb = x + (long long)b * T_ * C;
+  for (int i = threadIdx.x; i < rows * C; i += 256) {
+    const int r = i / C, c = i - r * C;
+    const int t = t0 - pad + r;
+    float v = 0.f;
+    if (t >= 0 && t < len) v = leaky(to_f32(xb[(long long)t * C + c]), slope);
+    xs[r * (C + 1) + c] = v;
+  }
+  __syncthreads();
+  const int t = t0 + threadIdx.x;
+  if (t >= T_) return;
+  float acc = bias;
+  for (int j = 0; j < k; ++j) {
+    const float* xr = xs + (threadIdx.x + j) * (C + 1);
+    const float* wr = ws + j * C;
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc = fmaf(wr[c], xr[c], acc);
+  }
+  wav[b * swb + t] = t < len ? tanhf(acc) : 0.f;
+}
+
+hipError_t launch_conv_post(int dtype, const void* x, const int* x_len, int B, int T_, int C,
+                            const float* w, float bias, int k, float slope, float* wav, long long swb,
+                            hipStream_t s) {
+  if (C != 32) return hipErrorInvalidValue;
+  dim3 grid((T_ + 255) / 256, B);
+  const size_t lds = (size_t)(k * C + (256 + k - 1) * (C + 1)) * 4;
+  switch (dtype) {
+    case DT_F32: hipLaunchKernelGGL((conv_post_kernel<float, 32>), grid, dim3(256), lds, s, (const float*)x, x_len, T_, w, bias, k, slope, wav, swb); break;
+    case DT_F16: hipLaunchKernelGGL((conv_post_kernel<half_t, 32>), grid, dim3(256), lds, s, (const half_t*)x, x_len, T_, w, bias, k, slope, wav, swb); break;
+    case DT_BF16: hipLaunchKernelGGL((conv_post_kernel<bf16_t, 32>), grid, dim3(256), lds, s, (const bf16_t*)x, x_len, T_, w, bias, k, slope, wav, swb); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace tts

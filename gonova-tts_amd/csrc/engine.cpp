@@ -1,0 +1,604 @@
+// libtts_hip.so — engine runtime and C-ABI (include/tts_hip.h).
+//
+// The engine owns device weights (packed for the implicit-GEMM kernels) and a
+// workspace sized for [max_batch x max_frames]; forwards enqueue kernels on the
+// caller's stream and never allocate once reserved.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/tts_hip.h"
+#include "acoustic.h"
+#include "common.h"
+#include "kernels.h"
+
+using namespace tts;
+
+static thread_local std::string g_last_error;
+
+namespace {
+
+struct TtsError : std::runtime_error {
+  int code;
+  TtsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_CHECK(expr)                                                                    \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      throw TtsError(TTS_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));    \
+  } while (0)
+
+size_t dtype_size(int dt) { return dt == DT_F32 ? 4 : 2; }
+
+uint16_t f32_to_bf16_bits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// host fp32 -> device buffer in dtype
+void* upload(const std::vector<float>& h, int dt) {
+  void* d = nullptr;
+  const size_t n = h.size();
+  HIP_CHECK(hipMalloc(&d, std::max<size_t>(n, 1) * dtype_size(dt)));
+  if (dt == DT_F32) {
+    HIP_CHECK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+  } else if (dt == DT_F16) {
+    std::vector<_Float16> t(n);
+    for (size_t i = 0; i < n; ++i) t[i] = (_Float16)h[i];
+    HIP_CHECK(hipMemcpy(d, t.data(), n * 2, hipMemcpyHostToDevice));
+  } else {
+    std::vector<uint16_t> t(n);
+    for (size_t i = 0; i < n; ++i) t[i] = f32_to_bf16_bits(h[i]);
+    HIP_CHECK(hipMemcpy(d, t.data(), n * 2, hipMemcpyHostToDevice));
+  }
+  return d;
+}
+
+float* upload_f32(const std::vector<float>& h) { return (float*)upload(h, DT_F32); }
+
+struct HostTensor {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+};
+
+}  // namespace
+
+// A packed implicit-GEMM conv layer: W[M][taps][Cin] in the compute dtype, bias fp32 [M].
+struct ConvLayer {
+  void* w = nullptr;
+  float* bias = nullptr;
+  int M = 0, Cin = 0, taps = 1, dil = 1, pad = 0;
+  // transposed-conv output mapping
+  int up_s = 0, up_cout = 0, up_p = 0;
+};
+
+struct VocoderWeights {
+  bool loaded = false;
+  float* mean = nullptr;
+  float* scale = nullptr;
+  bool normalize = false;
+  ConvLayer conv_pre;
+  std::vector<ConvLayer> ups;                    // per stage
+  std::vector<int> up_rate;
+  std::vector<int> stage_ch;
+  // mrf[stage][block][pair][0=conv1,1=conv2]
+  std::vector<std::vector<std::vector<std::array<ConvLayer, 2>>>> mrf;
+  float* post_w = nullptr;  // fp32 [k][C]
+  float post_b = 0.f;
+  int post_k = 7, post_c = 32;
+  int hop = 256;
+};
+
+struct tts_engine {
+  int device = 0;
+  tts_config cfg{};
+  std::mutex mu;
+  std::map<std::string, HostTensor> host;
+  bool finalized = false;
+  std::vector<void*> allocs;  // weight allocations
+
+  VocoderWeights voc;
+  AcousticModel ac;
+
+  // vocoder workspace
+  void* vbuf[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  size_t vbuf_elems = 0;
+  void* vmel = nullptr;  // normalized mel in compute dtype
+  size_t vmel_elems = 0;
+  int* vlens = nullptr;  // [16][max_batch]
+  int vlens_batch = 0;
+  float* vchunk_wav = nullptr;
+  size_t vchunk_elems = 0;
+
+  // live kernel profiling: hipEvents around every implicit-GEMM launch, on the launch stream
+  bool profiling = false;
+  struct ProfRec { hipEvent_t a, b; double flops; };
+  std::vector<ProfRec> prof;
+  std::vector<hipEvent_t> ev_pool;
+  hipEvent_t get_event() {
+    if (!ev_pool.empty()) { hipEvent_t e = ev_pool.back(); ev_pool.pop_back(); return e; }
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    return e;
+  }
+
+  ~tts_engine() {
+    hipSetDevice(device);
+    for (void* p : allocs) hipFree(p);
+    for (void*& p : vbuf) if (p) hipFree(p);
+    if (vmel) hipFree(vmel);
+    if (vlens) hipFree(vlens);
+    if (vchunk_wav) hipFree(vchunk_wav);
+    for (auto& r : prof) { hipEventDestroy(r.a); hipEventDestroy(r.b); }
+    for (auto e : ev_pool) hipEventDestroy(e);
+    ac.free_all();
+  }
+
+  void* track(void* p) { allocs.push_back(p); return p; }
+
+  const HostTensor& get(const std::string& n) {
+    auto it = host.find(n);
+    if (it == host.end()) throw TtsError(TTS_ERR_STATE, "missing weight: " + n);
+    return it->second;
+  }
+  bool has(const std::string& n) const { return host.count(n) != 0; }
+
+  // nn.Conv1d weight [Cout][Cin][k] -> W[Cout][k][Cin]
+  ConvLayer pack_conv(const std::string& wname, const std::string& bname, int dil, int pad, int dt) {
+    const HostTensor& w = get(wname);
+    if (w.shape.size() != 3) throw TtsError(TTS_ERR_INVALID, wname + ": expected 3-D conv weight");
+    const int co = (int)w.shape[0], ci = (int)w.shape[1], k = (int)w.shape[2];
+    std::vector<float> p((size_t)co * k * ci);
+    for (int o = 0; o < co; ++o)
+      for (int c = 0; c < ci; ++c)
+        for (int j = 0; j < k; ++j) p[((size_t)o * k + j) * ci + c] = w.data[((size_t)o * ci + c) * k + j];
+    ConvLayer L;
+    L.w = track(upload(p, dt));
+    std::vector<float> b(co, 0.f);
+    if (!bname.empty() && has(bname)) b = get(bname).data;
+    L.bias = (float*)track(upload_f32(b));
+    L.M = co; L.Cin = ci; L.taps = k; L.dil = dil; L.pad = pad;
+    return L;
+  }
+
+  // nn.ConvTranspose1d weight [Cin][Cout][k], stride s, padding p as a polyphase conv:
+  //   y[u*s + r - p][co] = b[co] + sum_{t<taps} sum_ci x[u + t - (taps-1)][ci] * W[ci][co][r + (taps-1-t)*s]
+  // i.e. M = s*Cout rows (r, co), taps = k/s, conv pad = taps-1 (oracle: conv_transpose1d).
+  ConvLayer pack_transposed(const std::string& wname, const std::string& bname, int s, int dt) {
+    const HostTensor& w = get(wname);
+    const int ci = (int)w.shape[0], co = (int)w.shape[1], k = (int)w.shape[2];
+    if (k % s || (k - s) % 2) throw TtsError(TTS_ERR_INVALID, wname + ": need k % s == 0 and even k-s");
+    const int taps = k / s;
+    const int M = s * co;
+    std::vector<float> p((size_t)M * taps * ci);
+    for (int r = 0; r < s; ++r)
+      for (int o = 0; o < co; ++o)
+        for (int t = 0; t < taps; ++t) {
+          const int j = r + (taps - 1 - t) * s;
+          for (int c = 0; c < ci; ++c)
+            p[(((size_t)(r * co + o)) * taps + t) * ci + c] = w.data[((size_t)c * co + o) * k + j];
+        }
+    ConvLayer L;
+    L.w = track(upload(p, dt));
+    const auto& bh = get(bname).data;
+    std::vector<float> b(M);
+    for (int r = 0; r < s; ++r)
+      for (int o = 0; o < co; ++o) b[r * co + o] = bh[o];
+    L.bias = (float*)track(upload_f32(b));
+    L.M = M; L.Cin = ci; L.taps = taps; L.dil = 1; L.pad = taps - 1;
+    L.up_s = s; L.up_cout = co; L.up_p = (k - s) / 2;
+    return L;
+  }
+
+  void finalize_vocoder() {
+    if (!has("conv_pre.weight")) return;
+    const int dt = cfg.vocoder_dtype;
+    VocoderWeights& v = voc;
+    v.conv_pre = pack_conv("conv_pre.weight", "conv_pre.bias", 1, 3, dt);
+    if (has("mean") && has("scale")) {
+      v.mean = (float*)track(upload_f32(get("mean").data));
+      v.scale = (float*)track(upload_f32(get("scale").data));
+      v.normalize = true;
+    }
+    int nst = 0;
+    while (has("upsampler." + std::to_string(nst) + ".weight")) ++nst;
+    // count resblocks -> blocks per stage
+    int nres = 0;
+    while (has("resblocks." + std::to_string(nres) + ".convs1.0.weight")) ++nres;
+    if (nst == 0 || nres % nst) throw TtsError(TTS_ERR_INVALID, "inconsistent vocoder weights");
+    const int nk = nres / nst;
+    v.hop = 1;
+    v.ups.clear(); v.up_rate.clear(); v.stage_ch.clear(); v.mrf.assign(nst, {});
+    for (int i = 0; i < nst; ++i) {
+      const HostTensor& w = get("upsampler." + std::to_string(i) + ".weight");
+      const int cin = (int)w.shape[0], k = (int)w.shape[2];
+      // stride from "__cfg__.upsample_rates" if given, else HiFi-GAN V1's k = 2*stride
+      int s = k / 2;
+      if (has("__cfg__.upsample_rates")) s = (int)std::lround(get("__cfg__.upsample_rates").data.at(i));
+      (void)cin;
+      v.ups.push_back(pack_transposed("upsampler." + std::to_string(i) + ".weight",
+                                      "upsampler." + std::to_string(i) + ".bias", s, dt));
+      v.up_rate.push_back(s);
+      v.hop *= s;
+      const int ch = (int)w.shape[1];
+      v.stage_ch.push_back(ch);
+      v.mrf[i].resize(nk);
+      for (int j = 0; j < nk; ++j) {
+        const std::string pre = "resblocks." + std::to_string(i * nk + j) + ".";
+        const int ks = (int)get(pre + "convs1.0.weight").shape[2];
+        int np = 0;
+        while (has(pre + "convs1." + std::to_string(np) + ".weight")) ++np;
+        v.mrf[i][j].resize(np);
+        for (int q = 0; q < np; ++q) {
+          int d = q == 0 ? 1 : (q == 1 ? 3 : 5);
+          if (has("__cfg__.resblock_dilation_sizes")) {
+            const HostTensor& dd = get("__cfg__.resblock_dilation_sizes");  // [nk][np]
+            d = (int)std::lround(dd.data.at((size_t)j * dd.shape.at(1) + q));
+          }
+          v.mrf[i][j][q][0] = pack_conv(pre + "convs1." + std::to_string(q) + ".weight",
+                                        pre + "convs1." + std::to_string(q) + ".bias", d, (ks * d - d) / 2, dt);
+          v.mrf[i][j][q][1] = pack_conv(pre + "convs2." + std::to_string(q) + ".weight",
+                                        pre + "convs2." + std::to_string(q) + ".bias", 1, (ks - 1) / 2, dt);
+        }
+      }
+    }
+    const HostTensor& pw = get("conv_post.weight");  // [1][C][k]
+    v.post_c = (int)pw.shape[1];
+    v.post_k = (int)pw.shape[2];
+    std::vector<float> t((size_t)v.post_k * v.post_c);
+    for (int c = 0; c < v.post_c; ++c)
+      for (int j = 0; j < v.post_k; ++j) t[(size_t)j * v.post_c + c] = pw.data[(size_t)c * v.post_k + j];
+    v.post_w = (float*)track(upload_f32(t));
+    v.post_b = get("conv_post.bias").data[0];
+    v.loaded = true;
+  }
+
+  void reserve_vocoder(int B, int T) {
+    if (!voc.loaded) return;
+    size_t per_frame = (size_t)voc.conv_pre.M;  // conv_pre output channels
+    size_t cum = 1;
+    for (size_t i = 0; i < voc.ups.size(); ++i) {
+      cum *= voc.up_rate[i];
+      per_frame = std::max(per_frame, cum * voc.stage_ch[i]);
+    }
+    const size_t need = (size_t)B * T * per_frame;
+    const int dt = cfg.vocoder_dtype;
+    if (need > vbuf_elems) {
+      for (void*& p : vbuf) { if (p) hipFree(p); p = nullptr; }
+      vbuf_elems = 0;
+      for (void*& p : vbuf) HIP_CHECK(hipMalloc(&p, need * dtype_size(dt)));
+      vbuf_elems = need;
+    }
+    const size_t mel_need = (size_t)B * T * voc.conv_pre.Cin;
+    if (mel_need > vmel_elems) {
+      if (vmel) hipFree(vmel);
+      vmel = nullptr; vmel_elems = 0;
+      HIP_CHECK(hipMalloc(&vmel, mel_need * dtype_size(dt)));
+      vmel_elems = mel_need;
+    }
+    if (B > vlens_batch) {
+      if (vlens) hipFree(vlens);
+      vlens = nullptr; vlens_batch = 0;
+      HIP_CHECK(hipMalloc(&vlens, sizeof(int) * 16 * B));
+      vlens_batch = B;
+    }
+  }
+
+  void run_conv(const ConvLayer& L, const void* x, long long sxb, int sxr, const int* x_len, int x_rows,
+                void* y, long long syb, int syr, const int* y_len, int y_rows, float in_slope,
+                const void* r1, const void* r2, long long srb, int srr, float out_scale, int B,
+                const int* up_len, int dt, hipStream_t s, int act_out = ACT_NONE, float alpha = 1.f) {
+    ConvParams p = conv_params_default();
+    p.x = x; p.sxb = sxb; p.sxr = sxr; p.x_len = x_len; p.x_rows = x_rows;
+    p.w = L.w; p.swb = 0; p.w_ld = L.taps * L.Cin;
+    p.bias = L.bias;
+    p.y = y; p.syb = syb; p.syr = syr;
+    p.r1 = r1; p.r2 = r2; p.srb = srb; p.srr = srr;
+    p.y_len = y_len; p.y_rows = y_rows;
+    p.M = L.M; p.Cin = L.Cin; p.taps = L.taps; p.dil = L.dil; p.pad = L.pad;
+    p.in_slope = in_slope; p.act_out = act_out; p.alpha = alpha; p.out_scale = out_scale;
+    p.up_s = L.up_s; p.up_cout = L.up_cout; p.up_p = L.up_p; p.up_len = up_len;
+    p.B = B;
+    const char* why = nullptr;
+    if (conv_gemm_check(p, dt, &why)) throw TtsError(TTS_ERR_INVALID, std::string("conv: ") + why);
+    if (profiling) {
+      ProfRec r{get_event(), get_event(), 0.0};
+      // algorithmic FLOPs: 2 * Cout * Cin * k per produced row (transposed: per input row, all phases)
+      r.flops = 2.0 * L.M * (double)L.Cin * L.taps * (double)B * (L.up_s ? (y_rows - 1) : y_rows);
+      HIP_CHECK(hipEventRecord(r.a, s));
+      HIP_CHECK(conv_gemm_launch(dt, p, s));
+      HIP_CHECK(hipEventRecord(r.b, s));
+      prof.push_back(r);
+    } else {
+      HIP_CHECK(conv_gemm_launch(dt, p, s));
+    }
+  }
+
+  // HiFi-GAN V1 forward (oracle/vocoder.py vocoder_forward; HF:1435-1475).
+  void vocoder_forward(const float* mel, const int* mel_lens, int B, int T, float* wav, long long swb,
+                       hipStream_t s) {
+    if (!voc.loaded) throw TtsError(TTS_ERR_STATE, "vocoder weights not loaded/finalized");
+    const int dt = cfg.vocoder_dtype;
+    reserve_vocoder(B, T);
+    const VocoderWeights& v = voc;
+    const int nst = (int)v.ups.size();
+    // per-stage lengths: L[i] = len * cum_i (frames of stage i), U[i] = L[i] + 1 (polyphase rows)
+    int mult[8], add[8], n = 0;
+    int cum = 1;
+    mult[n] = 1; add[n] = 0; ++n;  // L0
+    for (int i = 0; i < nst; ++i) { cum *= v.up_rate[i]; mult[n] = cum; add[n] = 0; ++n; }
+    if (n > 8) throw TtsError(TTS_ERR_INVALID, "too many stages");
+    HIP_CHECK(launch_lens(mel_lens, vlens, B, mult, add, n, s));
+    int mult2[8], add2[8];
+    cum = 1;
+    for (int i = 0; i < nst; ++i) { mult2[i] = cum; add2[i] = 1; cum *= v.up_rate[i]; }
+    HIP_CHECK(launch_lens(mel_lens, vlens + 8 * B, B, mult2, add2, nst, s));
+    auto Lp = [&](int i) { return vlens + i * B; };
+    auto Up = [&](int i) { return vlens + (8 + i) * B; };
+
+    const int cin0 = v.conv_pre.Cin;
+    HIP_CHECK(launch_mel_in(dt, mel, (long long)T * cin0, cin0, v.normalize ? v.mean : nullptr, v.scale,
+                            vmel, B, T, cin0, s));
+    void* XS = vbuf[0];
+    void* T1 = vbuf[1];
+    void* HA = vbuf[2];
+    void* HB = vbuf[3];
+    void* S = vbuf[4];
+    // conv_pre: [B][T][80] -> S [B][T][512]
+    const int c0 = v.conv_pre.M;
+    run_conv(v.conv_pre, vmel, (long long)T * cin0, cin0, Lp(0), T, S, (long long)T * c0, c0, Lp(0), T, 1.f,
+             nullptr, nullptr, 0, 0, 1.f, B, nullptr, dt, s);
+    int Tin = T, cin = c0;
+    const float slope = 0.1f;
+    for (int i = 0; i < nst; ++i) {
+      const int ch = v.stage_ch[i];
+      const int Tout = Tin * v.up_rate[i];
+      const long long sb = (long long)Tout * ch;
+      // lrelu -> ConvTranspose1d (polyphase)
+      run_conv(v.ups[i], S, (long long)Tin * cin, cin, Lp(i), Tin, XS, sb, ch, Up(i), Tin + 1, slope,
+               nullptr, nullptr, 0, 0, 1.f, B, Lp(i + 1), dt, s);
+      const int nk = (int)v.mrf[i].size();
+      for (int j = 0; j < nk; ++j) {
+        const auto& blk = v.mrf[i][j];
+        const int np = (int)blk.size();
+        const void* h = XS;
+        for (int q = 0; q < np; ++q) {
+          // conv1: lrelu(h) -> T1
+          run_conv(blk[q][0], h, sb, ch, Lp(i + 1), Tout, T1, sb, ch, Lp(i + 1), Tout, slope, nullptr, nullptr,
+                   0, 0, 1.f, B, nullptr, dt, s);
+          // conv2: lrelu(T1) -> + h ; last pair accumulates into S (sum over blocks, /nk at the end)
+          const bool last = q == np - 1;
+          void* out = last ? S : (q % 2 == 0 ? HA : HB);
+          const void* r2 = (last && j > 0) ? S : nullptr;
+          const float sc = (last && j == nk - 1) ? 1.0f / (float)nk : 1.f;
+          run_conv(blk[q][1], T1, sb, ch, Lp(i + 1), Tout, out, sb, ch, Lp(i + 1), Tout, slope, h, r2, sb, ch,
+                   sc, B, nullptr, dt, s);
+          h = out;
+        }
+      }
+      Tin = Tout;
+      cin = ch;
+    }
+    HIP_CHECK(launch_conv_post(dt, S, Lp(nst), B, Tin, cin, v.post_w, v.post_b, v.post_k, 0.01f, wav, swb, s));
+  }
+};
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+template <typename F>
+static int guarded(tts_engine* eng, F&& f) {
+  try {
+    if (!eng) throw TtsError(TTS_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(eng->mu);
+    HIP_CHECK(hipSetDevice(eng->device));
+    f();
+    return TTS_OK;
+  } catch (const TtsError& e) {
+    g_last_error = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "out of host memory";
+    return TTS_ERR_NOMEM;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return TTS_ERR_INVALID;
+  }
+}
+
+extern "C" {
+
+const char* tts_last_error(void) { return g_last_error.c_str(); }
+
+int tts_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int tts_engine_create(int hip_device, const tts_config* cfg, tts_engine** out) {
+  try {
+    if (!out) throw TtsError(TTS_ERR_INVALID, "null out");
+    *out = nullptr;
+    int n = 0;
+    HIP_CHECK(hipGetDeviceCount(&n));
+    if (hip_device < 0 || hip_device >= n)
+      throw TtsError(TTS_ERR_INVALID, "hip device " + std::to_string(hip_device) + " out of range");
+    std::unique_ptr<tts_engine> e(new tts_engine());
+    e->device = hip_device;
+    if (cfg) e->cfg = *cfg;
+    auto okdt = [](int d) { return d == DT_F32 || d == DT_F16 || d == DT_BF16; };
+    if (!okdt(e->cfg.vocoder_dtype) || !okdt(e->cfg.acoustic_dtype)) throw TtsError(TTS_ERR_INVALID, "bad dtype");
+    HIP_CHECK(hipSetDevice(hip_device));
+    *out = e.release();
+    return TTS_OK;
+  } catch (const TtsError& e) {
+    g_last_error = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return TTS_ERR_INVALID;
+  }
+}
+
+int tts_engine_set_weight(tts_engine* eng, const char* name, const float* host_data, const int64_t* shape,
+                          int ndim) {
+  return guarded(eng, [&] {
+    if (!name || (!host_data) || ndim < 0 || ndim > 8) throw TtsError(TTS_ERR_INVALID, "bad weight args");
+    if (eng->finalized) throw TtsError(TTS_ERR_STATE, "engine already finalized");
+    HostTensor t;
+    size_t n = 1;
+    for (int i = 0; i < ndim; ++i) {
+      if (shape[i] < 0) throw TtsError(TTS_ERR_INVALID, "negative dim");
+      t.shape.push_back(shape[i]);
+      n *= (size_t)shape[i];
+    }
+    t.data.assign(host_data, host_data + n);
+    eng->host[name] = std::move(t);
+  });
+}
+
+int tts_engine_finalize(tts_engine* eng) {
+  return guarded(eng, [&] {
+    if (eng->finalized) return;
+    eng->finalize_vocoder();
+    eng->ac.finalize(
+        [&](const std::string& n) -> const std::vector<float>* {
+          auto it = eng->host.find(n);
+          return it == eng->host.end() ? nullptr : &it->second.data;
+        },
+        [&](const std::string& n) -> std::vector<int64_t> {
+          auto it = eng->host.find(n);
+          return it == eng->host.end() ? std::vector<int64_t>{} : it->second.shape;
+        },
+        eng->cfg.acoustic_dtype);
+    if (!eng->voc.loaded && !eng->ac.loaded) throw TtsError(TTS_ERR_STATE, "no known weights were set");
+    eng->host.clear();
+    eng->finalized = true;
+    if (eng->cfg.max_batch > 0 && eng->cfg.max_frames > 0) eng->reserve_vocoder(eng->cfg.max_batch, eng->cfg.max_frames);
+    if (eng->cfg.max_batch > 0 && eng->cfg.max_tokens > 0 && eng->cfg.max_frames > 0)
+      eng->ac.reserve(eng->cfg.max_batch, eng->cfg.max_tokens, eng->cfg.max_frames);
+  });
+}
+
+int tts_engine_reserve(tts_engine* eng, int max_batch, int max_frames, int max_tokens) {
+  return guarded(eng, [&] {
+    if (!eng->finalized) throw TtsError(TTS_ERR_STATE, "finalize first");
+    if (max_batch <= 0 || max_frames <= 0) throw TtsError(TTS_ERR_INVALID, "bad reserve sizes");
+    eng->reserve_vocoder(max_batch, max_frames);
+    if (eng->ac.loaded && max_tokens > 0) eng->ac.reserve(max_batch, max_tokens, max_frames);
+  });
+}
+
+void tts_engine_destroy(tts_engine* eng) { delete eng; }
+
+int tts_vocoder_forward(tts_engine* eng, const float* d_mel, const int32_t* d_mel_lens, int B, int T,
+                        float* d_wav, void* stream) {
+  return guarded(eng, [&] {
+    if (!eng->finalized) throw TtsError(TTS_ERR_STATE, "finalize first");
+    if (!d_mel || !d_mel_lens || !d_wav || B <= 0 || T <= 0) throw TtsError(TTS_ERR_INVALID, "bad vocoder args");
+    eng->vocoder_forward(d_mel, d_mel_lens, B, T, d_wav, (long long)T * eng->voc.hop, (hipStream_t)stream);
+  });
+}
+
+int tts_vocoder_forward_chunk(tts_engine* eng, const float* d_mel, const int32_t* d_win_lens, int B, int T_win,
+                              int ctx_left, int T_chunk, float* d_wav, void* stream) {
+  return guarded(eng, [&] {
+    if (!eng->finalized) throw TtsError(TTS_ERR_STATE, "finalize first");
+    if (!d_mel || !d_win_lens || !d_wav || B <= 0 || T_win <= 0 || ctx_left < 0 || T_chunk <= 0 ||
+        ctx_left + T_chunk > T_win)
+      throw TtsError(TTS_ERR_INVALID, "bad chunk args");
+    const int hop = eng->voc.hop;
+    const size_t need = (size_t)B * T_win * hop;
+    if (need > eng->vchunk_elems) {
+      if (eng->vchunk_wav) hipFree(eng->vchunk_wav);
+      eng->vchunk_wav = nullptr; eng->vchunk_elems = 0;
+      HIP_CHECK(hipMalloc(&eng->vchunk_wav, need * 4));
+      eng->vchunk_elems = need;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    eng->vocoder_forward(d_mel, d_win_lens, B, T_win, eng->vchunk_wav, (long long)T_win * hop, s);
+    HIP_CHECK(hipMemcpy2DAsync(d_wav, (size_t)T_chunk * hop * 4, eng->vchunk_wav + (size_t)ctx_left * hop,
+                               (size_t)T_win * hop * 4, (size_t)T_chunk * hop * 4, B, hipMemcpyDeviceToDevice, s));
+  });
+}
+
+int tts_acoustic_forward(tts_engine* eng, const int32_t* d_tokens, const int32_t* d_tok_lens, int B, int N,
+                         const int32_t* d_dur_override, float* d_mel, int32_t* d_mel_lens, int Tcap,
+                         int32_t* d_durations, void* stream) {
+  return guarded(eng, [&] {
+    if (!eng->finalized) throw TtsError(TTS_ERR_STATE, "finalize first");
+    if (!eng->ac.loaded) throw TtsError(TTS_ERR_STATE, "acoustic weights not loaded");
+    if (!d_tokens || !d_tok_lens || !d_mel || !d_mel_lens || B <= 0 || N <= 0 || Tcap <= 0)
+      throw TtsError(TTS_ERR_INVALID, "bad acoustic args");
+    eng->ac.forward(d_tokens, d_tok_lens, B, N, d_dur_override, d_mel, d_mel_lens, Tcap, d_durations,
+                    (hipStream_t)stream);
+  });
+}
+
+int tts_engine_profile(tts_engine* eng, int enable) {
+  return guarded(eng, [&] { eng->profiling = enable != 0; });
+}
+
+int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops, int* n_launches) {
+  return guarded(eng, [&] {
+    double ms = 0.0, fl = 0.0;
+    int n = 0;
+    for (auto& r : eng->prof) {
+      HIP_CHECK(hipEventSynchronize(r.b));
+      float e = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&e, r.a, r.b));
+      ms += e;
+      fl += r.flops;
+      ++n;
+      eng->ev_pool.push_back(r.a);
+      eng->ev_pool.push_back(r.b);
+    }
+    eng->prof.clear();
+    if (gemm_ms) *gemm_ms = ms;
+    if (gemm_flops) *gemm_flops = fl;
+    if (n_launches) *n_launches = n;
+  });
+}
+
+int tts_op_conv1d(int dtype, const tts_conv_desc* d, void* stream) {
+  try {
+    if (!d) throw TtsError(TTS_ERR_INVALID, "null desc");
+    if (dtype != DT_F32 && dtype != DT_F16 && dtype != DT_BF16) throw TtsError(TTS_ERR_INVALID, "bad dtype");
+    ConvParams p = conv_params_default();
+    p.x = d->x; p.sxb = d->sxb; p.sxr = d->sxr; p.x_len = d->x_len; p.x_rows = d->x_rows;
+    p.w = d->w; p.swb = d->swb; p.w_ld = d->w_ld; p.bias = d->bias;
+    p.y = d->y; p.syb = d->syb; p.syr = d->syr;
+    p.r1 = d->r1; p.r2 = d->r2; p.srb = d->srb; p.srr = d->srr;
+    p.y_len = d->y_len; p.y_rows = d->y_rows;
+    p.M = d->M; p.Cin = d->Cin; p.taps = d->taps; p.dil = d->dil; p.pad = d->pad;
+    p.in_slope = d->in_slope; p.act_out = d->act_out; p.out_slope = d->out_slope;
+    p.alpha = d->alpha; p.out_scale = d->out_scale;
+    p.up_s = d->up_s; p.up_cout = d->up_cout; p.up_p = d->up_p; p.up_len = d->up_len;
+    p.B = d->B;
+    const char* why = nullptr;
+    if (conv_gemm_check(p, dtype, &why)) throw TtsError(TTS_ERR_INVALID, std::string("conv: ") + why);
+    HIP_CHECK(conv_gemm_launch(dtype, p, (hipStream_t)stream));
+    return TTS_OK;
+  } catch (const TtsError& e) {
+    g_last_error = e.what();
+    return e.code;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,43 @@
+// Host-side declarations of the HIP kernel launchers (internal to libtts_hip.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tts {
+
+// Implicit-GEMM conv (conv_gemm.hip).  All strides are in elements of the compute dtype.
+struct ConvParams {
+  const void* x; long long sxb; int sxr; const int* x_len; int x_rows;
+  const void* w; long long swb; int w_ld;
+  const float* bias;
+  void* y; long long syb; int syr;
+  const void* r1; const void* r2; long long srb; int srr;
+  const int* y_len; int y_rows;
+  int M, Cin, taps, dil, pad;
+  float in_slope;          // leaky-relu slope applied to X on load; 1 = identity
+  int act_out; float out_slope;
+  float alpha, out_scale;  // y = ((alpha*(acc+bias)) -> act) + r1 + r2, then * out_scale
+  int up_s, up_cout, up_p; const int* up_len;  // transposed-conv output mapping (up_s = 0: off)
+  int B;
+};
+
+inline ConvParams conv_params_default() {
+  ConvParams p{};
+  p.in_slope = 1.f; p.alpha = 1.f; p.out_scale = 1.f; p.out_slope = 0.f;
+  p.taps = 1; p.dil = 1;
+  return p;
+}
+
+int conv_gemm_check(const ConvParams& p, int dtype, const char** why);
+hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s);
+
+// elementwise.hip
+hipError_t launch_mel_in(int dtype, const float* mel, long long smb, int smr, const float* mean,
+                         const float* scale, void* out, int B, int T, int C, hipStream_t s);
+hipError_t launch_lens(const int* in, int* out, int B, const int* mult, const int* add, int n,
+                       hipStream_t s);
+hipError_t launch_conv_post(int dtype, const void* x, const int* x_len, int B, int T, int C,
+                            const float* w /*[k][C]*/, float bias, int k, float in_slope,
+                            float* wav, long long swb, hipStream_t s);
+
+}  // namespace tts

@@ -1,0 +1,249 @@
+"""ctypes binding of libtts_hip.so (include/tts_hip.h) and the device-side engine handle.
+
+This is the layer that replaces `ChatterboxTTS.from_pretrained(device=...)`
+(`services/tts/core/synthesizer.py:185`): the engine is created on HIP device N
+for a "cuda:N" string, weights are handed over by HF state_dict name, and the
+forwards run the hand-written gfx950 kernels.  PyTorch-ROCm only allocates the
+caller-owned input/output device buffers and provides the stream.
+
+There is no CPU fallback: if the shared library is missing or no HIP device is
+visible, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Dict, Optional
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libtts_hip.so")
+
+DTYPES = {"f32": 0, "fp32": 0, "float32": 0, "f16": 1, "fp16": 1, "float16": 1, "bf16": 2, "bfloat16": 2}
+
+TTS_ERRORS = {-1: "invalid argument", -2: "HIP error", -3: "bad state", -4: "out of memory"}
+
+
+class TtsConfig(ctypes.Structure):
+    _fields_ = [("vocoder_dtype", ctypes.c_int), ("acoustic_dtype", ctypes.c_int),
+                ("max_batch", ctypes.c_int), ("max_frames", ctypes.c_int), ("max_tokens", ctypes.c_int)]
+
+
+class TtsConvDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", ctypes.c_void_p), ("sxb", ctypes.c_int64), ("sxr", ctypes.c_int32), ("x_len", ctypes.c_void_p),
+        ("x_rows", ctypes.c_int32),
+        ("w", ctypes.c_void_p), ("swb", ctypes.c_int64), ("w_ld", ctypes.c_int32),
+        ("bias", ctypes.c_void_p),
+        ("y", ctypes.c_void_p), ("syb", ctypes.c_int64), ("syr", ctypes.c_int32),
+        ("r1", ctypes.c_void_p), ("r2", ctypes.c_void_p), ("srb", ctypes.c_int64), ("srr", ctypes.c_int32),
+        ("y_len", ctypes.c_void_p), ("y_rows", ctypes.c_int32),
+        ("M", ctypes.c_int32), ("Cin", ctypes.c_int32), ("taps", ctypes.c_int32), ("dil", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
+        ("in_slope", ctypes.c_float), ("act_out", ctypes.c_int32), ("out_slope", ctypes.c_float),
+        ("alpha", ctypes.c_float), ("out_scale", ctypes.c_float),
+        ("up_s", ctypes.c_int32), ("up_cout", ctypes.c_int32), ("up_p", ctypes.c_int32),
+        ("up_len", ctypes.c_void_p),
+        ("B", ctypes.c_int32),
+    ]
+
+
+# every function declared in include/tts_hip.h: (name, restype, argtypes)
+_VP, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+C_API = [
+    ("tts_device_count", _I, []),
+    ("tts_engine_create", _I, [_I, ctypes.POINTER(TtsConfig), ctypes.POINTER(_VP)]),
+    ("tts_engine_set_weight", _I, [_VP, ctypes.c_char_p, _VP, ctypes.POINTER(ctypes.c_int64), _I]),
+    ("tts_engine_finalize", _I, [_VP]),
+    ("tts_engine_reserve", _I, [_VP, _I, _I, _I]),
+    ("tts_engine_destroy", None, [_VP]),
+    ("tts_vocoder_forward", _I, [_VP, _VP, _VP, _I, _I, _VP, _VP]),
+    ("tts_vocoder_forward_chunk", _I, [_VP, _VP, _VP, _I, _I, _I, _I, _VP, _VP]),
+    ("tts_acoustic_forward", _I, [_VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _I, _VP, _VP]),
+    ("tts_engine_profile", _I, [_VP, _I]),
+    ("tts_engine_profile_read", _I, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_int)]),
+    ("tts_last_error", ctypes.c_char_p, []),
+    ("tts_op_conv1d", _I, [_I, ctypes.POINTER(TtsConvDesc), _VP]),
+]
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libtts_hip.so (no GPU needed); raises if it has not been built."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} not found: build it with `python -m gonova_tts_amd.build` "
+                               "(there is no CPU fallback)")
+        lib = ctypes.CDLL(path)
+        for name, res, args in C_API:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = load_library().tts_last_error()
+        msg = msg.decode() if msg else ""
+        raise RuntimeError(f"{what}: {TTS_ERRORS.get(rc, rc)}: {msg}")
+
+
+def parse_device(device) -> int:
+    """Map a reference-style device string ("cuda", "cuda:N", int) to a HIP ordinal."""
+    if isinstance(device, int):
+        return device
+    s = str(device)
+    if s in ("cuda", "hip", "gpu"):
+        return 0
+    if s.startswith(("cuda:", "hip:")):
+        return int(s.split(":", 1)[1])
+    raise ValueError(f"unsupported device {device!r}: the engine runs on HIP devices only")
+
+
+def _stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class HipEngine:
+    """Device-side TTS engine (one per HIP device)."""
+
+    def __init__(self, device=0, vocoder_dtype: str = "f16", acoustic_dtype: str = "bf16",
+                 max_batch: int = 0, max_frames: int = 0, max_tokens: int = 0):
+        import torch
+        self.lib = load_library()
+        if not torch.cuda.is_available():
+            raise RuntimeError("no HIP device visible: gonova_tts_amd has no CPU path")
+        self.device_index = parse_device(device)
+        self.torch_device = torch.device("cuda", self.device_index)
+        self.vocoder_dtype = vocoder_dtype
+        self.acoustic_dtype = acoustic_dtype
+        cfg = TtsConfig(DTYPES[vocoder_dtype], DTYPES[acoustic_dtype], max_batch, max_frames, max_tokens)
+        h = ctypes.c_void_p()
+        check(self.lib.tts_engine_create(self.device_index, ctypes.byref(cfg), ctypes.byref(h)),
+              "tts_engine_create")
+        self.handle = h
+        self.hop = 256
+        self._finalized = False
+        self.has_vocoder = False
+        self.has_acoustic = False
+
+    # ------------------------------------------------------------------ weights
+    def set_weight(self, name: str, arr):
+        a = np.ascontiguousarray(np.asarray(arr, dtype=np.float32))
+        shape = (ctypes.c_int64 * max(a.ndim, 1))(*a.shape)
+        check(self.lib.tts_engine_set_weight(self.handle, name.encode(), a.ctypes.data_as(ctypes.c_void_p),
+                                             shape, a.ndim), f"set_weight({name})")
+
+    def load_weights(self, vocoder: Optional[Dict[str, np.ndarray]] = None,
+                     acoustic: Optional[Dict[str, np.ndarray]] = None, vocoder_cfg=None):
+        if vocoder is not None:
+            from .config import VocoderConfig
+            vc = vocoder_cfg or VocoderConfig()
+            for k, v in vocoder.items():
+                self.set_weight(k, v)
+            self.set_weight("__cfg__.upsample_rates", np.asarray(vc.upsample_rates, np.float32))
+            self.set_weight("__cfg__.resblock_dilation_sizes", np.asarray(vc.resblock_dilation_sizes, np.float32))
+            self.hop = vc.hop
+            self.has_vocoder = True
+        if acoustic is not None:
+            for k, v in acoustic.items():
+                if k.endswith("num_batches_tracked"):
+                    continue
+                self.set_weight(k, v)
+            self.has_acoustic = True
+        check(self.lib.tts_engine_finalize(self.handle), "finalize")
+        self._finalized = True
+
+    def reserve(self, max_batch: int, max_frames: int, max_tokens: int = 0):
+        check(self.lib.tts_engine_reserve(self.handle, max_batch, max_frames, max_tokens), "reserve")
+
+    # ------------------------------------------------------------------ forwards
+    def vocoder(self, mel, mel_lens=None, out=None, stream=None):
+        """mel: cuda float32 [B, T, 80]; mel_lens: cuda int32 [B] -> wav cuda float32 [B, T*hop]."""
+        import torch
+        assert mel.is_cuda and mel.dtype == torch.float32 and mel.dim() == 3
+        mel = mel.contiguous()
+        B, T, _ = mel.shape
+        if mel_lens is None:
+            mel_lens = torch.full((B,), T, dtype=torch.int32, device=mel.device)
+        mel_lens = mel_lens.to(device=mel.device, dtype=torch.int32).contiguous()
+        if out is None:
+            out = torch.empty((B, T * self.hop), dtype=torch.float32, device=mel.device)
+        check(self.lib.tts_vocoder_forward(self.handle, ctypes.c_void_p(mel.data_ptr()),
+                                           ctypes.c_void_p(mel_lens.data_ptr()), B, T,
+                                           ctypes.c_void_p(out.data_ptr()), _stream_ptr(stream)),
+              "tts_vocoder_forward")
+        return out
+
+    def vocoder_chunk(self, mel_win, win_lens, ctx_left: int, t_chunk: int, out=None, stream=None):
+        import torch
+        mel_win = mel_win.contiguous()
+        B, Tw, _ = mel_win.shape
+        win_lens = win_lens.to(device=mel_win.device, dtype=torch.int32).contiguous()
+        if out is None:
+            out = torch.empty((B, t_chunk * self.hop), dtype=torch.float32, device=mel_win.device)
+        check(self.lib.tts_vocoder_forward_chunk(self.handle, ctypes.c_void_p(mel_win.data_ptr()),
+                                                 ctypes.c_void_p(win_lens.data_ptr()), B, Tw, ctx_left, t_chunk,
+                                                 ctypes.c_void_p(out.data_ptr()), _stream_ptr(stream)),
+              "tts_vocoder_forward_chunk")
+        return out
+
+    def acoustic(self, tokens, tok_lens, t_cap: int, durations=None, stream=None, return_durations=False):
+        """tokens: cuda int32 [B, N]; returns (mel [B, t_cap, 80] f32, mel_lens int32 [B])."""
+        import torch
+        tokens = tokens.to(dtype=torch.int32).contiguous()
+        tok_lens = tok_lens.to(device=tokens.device, dtype=torch.int32).contiguous()
+        B, N = tokens.shape
+        mel = torch.zeros((B, t_cap, 80), dtype=torch.float32, device=tokens.device)
+        mel_lens = torch.empty((B,), dtype=torch.int32, device=tokens.device)
+        dur_out = torch.empty((B, N), dtype=torch.int32, device=tokens.device)
+        dptr = ctypes.c_void_p(0)
+        if durations is not None:
+            durations = durations.to(device=tokens.device, dtype=torch.int32).contiguous()
+            dptr = ctypes.c_void_p(durations.data_ptr())
+        check(self.lib.tts_acoustic_forward(self.handle, ctypes.c_void_p(tokens.data_ptr()),
+                                            ctypes.c_void_p(tok_lens.data_ptr()), B, N, dptr,
+                                            ctypes.c_void_p(mel.data_ptr()), ctypes.c_void_p(mel_lens.data_ptr()),
+                                            t_cap, ctypes.c_void_p(dur_out.data_ptr()), _stream_ptr(stream)),
+              "tts_acoustic_forward")
+        if return_durations:
+            return mel, mel_lens, dur_out
+        return mel, mel_lens
+
+    def profile(self, enable: bool = True):
+        check(self.lib.tts_engine_profile(self.handle, int(enable)), "profile")
+
+    def profile_read(self):
+        """-> (summed implicit-GEMM kernel ms, their algorithmic FLOPs, launch count); resets."""
+        ms, fl, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        check(self.lib.tts_engine_profile_read(self.handle, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(n)),
+              "profile_read")
+        return ms.value, fl.value, n.value
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.tts_engine_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def conv1d_op(dtype: str, desc: TtsConvDesc, stream=None):
+    lib = load_library()
+    check(lib.tts_op_conv1d(DTYPES[dtype], ctypes.byref(desc), _stream_ptr(stream)), "tts_op_conv1d")

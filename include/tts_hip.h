@@ -1,0 +1,129 @@
+/*
+ * tts_hip.h — C-ABI of libtts_hip.so, the MI355X (gfx950) batched TTS engine.
+ *
+ * The reference has no C-ABI: its only model boundary is duck-typed Python
+ * (SURVEY.md §8b).  Each entry point below replaces one step of that boundary:
+ *
+ *   tts_engine_create / tts_engine_set_weight / tts_engine_finalize
+ *       replace `ChatterboxTTS.from_pretrained(device=self.device)`
+ *       (/root/reference/services/tts/core/synthesizer.py:185; device string from
+ *       synthesizer.py:130, "cuda:0" from server.py:400-405).  The Python host maps
+ *       "cuda:N" to HIP device N and feeds weights by HF state_dict name.
+ *   tts_acoustic_forward + tts_vocoder_forward
+ *       replace `self.model.generate(text, audio_prompt_path=..., exaggeration=...,
+ *       cfg_weight=0.5, temperature=0.8)` (synthesizer.py:344-350) for a whole
+ *       batch of sentences at once (tokens -> mel -> waveform).
+ *   tts_vocoder_forward_chunk
+ *       sub-sentence streaming the reference lacks (synthesizer.py:320-321 yields
+ *       one chunk per sentence); exact receptive-field context.
+ *   tts_last_error
+ *       replaces Python exception text: the host raises RuntimeError(tts_last_error())
+ *       so the reference's exception path (synthesizer.py:323-325, 291-294) holds.
+ *
+ * Conventions
+ *   - Every device buffer passed in is caller-owned (PyTorch-ROCm tensors passed by
+ *     data_ptr()).  The engine owns its weights and workspace.
+ *   - Work is enqueued asynchronously on `stream` (a hipStream_t; NULL = default).
+ *   - Return 0 on success, a negative TTS_ERR_* on failure; no C++ exception crosses
+ *     the ABI.  Every entry sets the HIP device and takes a per-engine mutex, so any
+ *     host thread may call (the reference calls from a ThreadPoolExecutor,
+ *     synthesizer.py:312).
+ *   - Activations are channels-last: mel [B][T][80] float32 (HF spectrogram layout),
+ *     waveform [B][T*256] float32 at 22,050 Hz.  Compute dtype per stage is chosen
+ *     at create time; accumulation is always fp32.
+ */
+#ifndef TTS_HIP_H
+#define TTS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TTS_OK 0
+#define TTS_ERR_INVALID (-1)
+#define TTS_ERR_HIP (-2)
+#define TTS_ERR_STATE (-3)
+#define TTS_ERR_NOMEM (-4)
+
+enum { TTS_DTYPE_F32 = 0, TTS_DTYPE_F16 = 1, TTS_DTYPE_BF16 = 2 };
+
+typedef struct tts_engine tts_engine;
+
+typedef struct tts_config {
+  int vocoder_dtype;   /* TTS_DTYPE_*: compute/storage dtype of vocoder activations */
+  int acoustic_dtype;  /* TTS_DTYPE_*: compute/storage dtype of acoustic activations */
+  int max_batch;       /* workspace reservation hints (0 = grow on demand) */
+  int max_frames;
+  int max_tokens;
+} tts_config;
+
+/* Number of HIP devices visible to this process. */
+int tts_device_count(void);
+
+/* Engine lifetime (replaces ChatterboxTTS.from_pretrained, synthesizer.py:185). */
+int tts_engine_create(int hip_device, const tts_config* cfg, tts_engine** out);
+/* Host fp32 tensor in HF state_dict naming (e.g. "resblocks.3.convs1.2.weight"). */
+int tts_engine_set_weight(tts_engine* eng, const char* name, const float* host_data,
+                          const int64_t* shape, int ndim);
+/* Fold / pack / upload every weight set so far; must precede any forward. */
+int tts_engine_finalize(tts_engine* eng);
+/* Pre-size the workspace (so later calls allocate nothing and can be graph-captured). */
+int tts_engine_reserve(tts_engine* eng, int max_batch, int max_frames, int max_tokens);
+void tts_engine_destroy(tts_engine* eng);
+
+/* Vocoder (replaces the waveform half of model.generate, synthesizer.py:344).
+ *   d_mel      [B][T][80] float32, utterance b valid for d_mel_lens[b] <= T frames
+ *   d_wav      [B][T*256] float32; samples >= 256*d_mel_lens[b] are written as 0.   */
+int tts_vocoder_forward(tts_engine* eng, const float* d_mel, const int32_t* d_mel_lens, int B,
+                        int T, float* d_wav, void* stream);
+
+/* Streaming vocoder chunk with exact context: computes the waveform of frames
+ * [ctx_left, ctx_left + T_chunk) of each d_mel[b] window [ctx_left + T_chunk + ctx_right][80]
+ * (zero context at utterance edges is expressed by the caller passing shorter windows via
+ * d_win_lens).  d_wav [B][T_chunk*256]. */
+int tts_vocoder_forward_chunk(tts_engine* eng, const float* d_mel, const int32_t* d_win_lens,
+                              int B, int T_win, int ctx_left, int T_chunk, float* d_wav,
+                              void* stream);
+
+/* Acoustic model (replaces the text->spectrogram half of model.generate).
+ *   d_tokens      [B][N] int32 token ids (padding ignored past d_tok_lens[b])
+ *   d_dur_override optional [B][N] int32 frame counts (NULL = predicted durations)
+ *   d_mel         [B][Tcap][80] float32 output, d_mel_lens [B] int32 output
+ *   d_durations   optional [B][N] int32 output of the durations actually used
+ * Frames past Tcap are dropped (d_mel_lens is clamped to Tcap). */
+int tts_acoustic_forward(tts_engine* eng, const int32_t* d_tokens, const int32_t* d_tok_lens,
+                         int B, int N, const int32_t* d_dur_override, float* d_mel,
+                         int32_t* d_mel_lens, int Tcap, int32_t* d_durations, void* stream);
+
+/* Live kernel timing for bench.py: with profiling on, every implicit-GEMM launch is
+ * bracketed by hipEvents on its own stream; _read() waits for them and returns the summed
+ * kernel time (ms), the algorithmic FLOPs of those launches and their count, then resets. */
+int tts_engine_profile(tts_engine* eng, int enable);
+int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops, int* n_launches);
+
+/* Thread-local message describing the last failure on this thread. */
+const char* tts_last_error(void);
+
+/* ---- op-level entry used by the parity tests (one implicit-GEMM conv launch) ---- */
+typedef struct tts_conv_desc {
+  const void* x; int64_t sxb; int32_t sxr; const int32_t* x_len; int32_t x_rows;
+  const void* w; int64_t swb; int32_t w_ld;
+  const float* bias;
+  void* y; int64_t syb; int32_t syr;
+  const void* r1; const void* r2; int64_t srb; int32_t srr;
+  const int32_t* y_len; int32_t y_rows;
+  int32_t M, Cin, taps, dil, pad;
+  float in_slope; int32_t act_out; float out_slope; float alpha; float out_scale;
+  int32_t up_s, up_cout, up_p; const int32_t* up_len;
+  int32_t B;
+} tts_conv_desc;
+
+int tts_op_conv1d(int dtype, const tts_conv_desc* desc, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TTS_HIP_H */

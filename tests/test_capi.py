@@ -1,0 +1,38 @@
+"""CPU checks of the C-ABI boundary: libtts_hip.so loads and exports every symbol
+include/tts_hip.h declares (no compute calls; no GPU needed)."""
+import os
+import re
+
+import pytest
+
+from gonova_tts_amd import engine
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "tts_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tts_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    decl = declared_functions()
+    bound = sorted(n for n, _, _ in engine.C_API)
+    assert decl == bound
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(engine.LIB_PATH):
+        from gonova_tts_amd.build import build
+        build()
+    lib = engine.load_library()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+
+
+def test_parse_device():
+    assert engine.parse_device("cuda:3") == 3
+    assert engine.parse_device("cuda") == 0
+    with pytest.raises(ValueError):
+        engine.parse_device("cpu")

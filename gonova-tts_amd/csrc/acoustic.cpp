@@ -1,21 +1,448 @@
-// FastSpeech2-Conformer acoustic model runtime — placeholder until the HIP path lands.
+// FastSpeech2-Conformer acoustic model runtime: tokens -> mel frames on the GPU.
+//
+// Mirrors oracle/acoustic.py (HF:1099-1288) with B=1-per-utterance semantics on a
+// padded batch: every conv masks rows outside [0, len[b]), attention masks keys
+// j >= len[b], durations / the all-zero rule are per utterance.
+//
+// Dense work runs on the implicit-GEMM MFMA kernel:
+//   FFN convs (k=3, 384->1536->384), Q|K|V and output projections (k=1),
+//   Q.K^T, Q.P^T (relative-position term) and P.V as head-batched GEMMs,
+//   conv-module pointwise convs, predictor convs, postnet convs (BatchNorm folded).
+// The relative-position projections linear_pos(pos_emb) depend only on the
+// relative offset, so they are computed once per layer at load time into a table
+// indexed by (RMAX-1 - rel) and every forward reads a window of it.
 #include "acoustic.h"
 
-#include <stdexcept>
+#include <array>
+#include <cmath>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "acoustic_kernels.h"
+#include "runtime.h"
 
 namespace tts {
 
-struct AcousticModel::Impl {};
+namespace {
 
-void AcousticModel::finalize(const GetData& get, const GetShape&, int) {
+inline int rup(int x, int m) { return (x + m - 1) / m * m; }
+
+struct LNParam {
+  float* g = nullptr;
+  float* b = nullptr;
+};
+
+struct ConformerLayer {
+  ConvLayer ffm1, ffm2, ff1, ff2, qkv, out, pw1, pw2, pos;
+  float* pos_u = nullptr;
+  float* pos_v = nullptr;
+  void* ptab = nullptr;  // [2*RMAX][D] linear_pos(rel table) in dt
+  float* dw_w = nullptr;  // [D][k] BatchNorm-folded
+  float* dw_b = nullptr;
+  int dw_k = 0;
+  LNParam ln_mac, ln_att, ln_conv, ln_ff, ln_final;
+};
+
+struct Predictor {
+  std::vector<ConvLayer> convs;
+  std::vector<LNParam> lns;
+  float* lin_w = nullptr;
+  float lin_b = 0.f;
+};
+
+}  // namespace
+
+struct AcousticModel::Impl {
+  int dt = DT_F32;
+  Profiler* prof = nullptr;
+  int D = 384, H = 2, V = 78, NMEL = 80, FFN = 1536, PRED = 256;
+  float eps = 1e-5f;
+  void* embed = nullptr;
+  std::vector<ConformerLayer> enc, dec;
+  Predictor pitch, energy, duration;
+  float *pe_w = nullptr, *pe_b = nullptr, *ee_w = nullptr, *ee_b = nullptr;
+  ConvLayer feat_out;
+  std::vector<ConvLayer> postnet;
+  std::vector<void*> allocs;
+  int rmax = 0;
+  float* pe_host_table_dummy = nullptr;
+
+  // workspace
+  int cap_B = 0, cap_N = 0, cap_T = 0;
+  std::vector<void*> ws;
+  void *X = nullptr, *Y = nullptr, *O = nullptr, *G = nullptr, *Qu = nullptr, *Qv = nullptr;
+  void *H1 = nullptr, *QKV = nullptr, *A = nullptr, *Vt = nullptr, *AC = nullptr, *BD = nullptr, *P = nullptr;
+  void *ENC = nullptr, *PB1 = nullptr, *PB2 = nullptr, *BEF = nullptr, *PN1 = nullptr, *PN2 = nullptr, *MELT = nullptr;
+  float *f_pitch = nullptr, *f_energy = nullptr, *f_logd = nullptr;
+  int *i_dur = nullptr, *i_tokmap = nullptr;
+
+  ~Impl() {
+    for (void* p : allocs) hipFree(p);
+    for (void* p : ws) hipFree(p);
+  }
+
+  void* track(void* p) { allocs.push_back(p); return p; }
+  float* upf(const std::vector<float>& v) { return (float*)track(upload_f32(v)); }
+
+  // ---------------------------------------------------------------- weights
+  const std::vector<float>& need(const GetData& get, const std::string& n) {
+    const std::vector<float>* p = get(n);
+    if (!p) throw TtsError(TTS_ERR_STATE, "missing acoustic weight: " + n);
+    return *p;
+  }
+
+  ConvLayer conv(const GetData& get, const GetShape& shape, const std::string& w, const std::string& b, int pad,
+                 const std::vector<float>* scale = nullptr, const std::vector<float>* bias_override = nullptr) {
+    const auto s = shape(w);
+    std::vector<float> bias;
+    if (bias_override) bias = *bias_override;
+    else if (!b.empty() && get(b)) bias = *get(b);
+    if (s.size() == 3) return make_conv(need(get, w), (int)s[0], (int)s[1], (int)s[2], bias, 1, pad, dt, allocs, scale);
+    if (s.size() == 2) return make_conv(need(get, w), (int)s[0], (int)s[1], 1, bias, 1, 0, dt, allocs, scale);
+    throw TtsError(TTS_ERR_INVALID, "bad weight rank: " + w);
+  }
+
+  LNParam ln(const GetData& get, const std::string& p) {
+    LNParam l;
+    l.g = upf(need(get, p + ".weight"));
+    l.b = upf(need(get, p + ".bias"));
+    return l;
+  }
+
+  ConformerLayer layer(const GetData& get, const GetShape& shape, const std::string& p) {
+    ConformerLayer L;
+    const int kf = (int)shape(p + "feed_forward.conv1.weight").at(2);
+    L.ffm1 = conv(get, shape, p + "feed_forward_macaron.conv1.weight", p + "feed_forward_macaron.conv1.bias", (kf - 1) / 2);
+    L.ffm2 = conv(get, shape, p + "feed_forward_macaron.conv2.weight", p + "feed_forward_macaron.conv2.bias", (kf - 1) / 2);
+    L.ff1 = conv(get, shape, p + "feed_forward.conv1.weight", p + "feed_forward.conv1.bias", (kf - 1) / 2);
+    L.ff2 = conv(get, shape, p + "feed_forward.conv2.weight", p + "feed_forward.conv2.bias", (kf - 1) / 2);
+    // fused Q|K|V projection [3D][D]
+    const std::string a = p + "self_attn.";
+    std::vector<float> wq, bq;
+    for (const char* n : {"linear_q", "linear_k", "linear_v"}) {
+      const auto& w = need(get, a + n + ".weight");
+      const auto& b = need(get, a + n + ".bias");
+      wq.insert(wq.end(), w.begin(), w.end());
+      bq.insert(bq.end(), b.begin(), b.end());
+    }
+    L.qkv = make_conv(wq, 3 * D, D, 1, bq, 1, 0, dt, allocs);
+    L.out = conv(get, shape, a + "linear_out.weight", a + "linear_out.bias", 0);
+    L.pos = make_conv(need(get, a + "linear_pos.weight"), D, D, 1, {}, 1, 0, dt, allocs);
+    L.pos_u = upf(need(get, a + "pos_bias_u"));
+    L.pos_v = upf(need(get, a + "pos_bias_v"));
+    const std::string c = p + "conv_module.";
+    L.pw1 = conv(get, shape, c + "pointwise_conv1.weight", c + "pointwise_conv1.bias", 0);
+    L.pw2 = conv(get, shape, c + "pointwise_conv2.weight", c + "pointwise_conv2.bias", 0);
+    // depthwise conv with BatchNorm folded: w' = w*s, b' = (b - rm)*s + beta, s = g / sqrt(rv + eps)
+    const auto& dw = need(get, c + "depthwise_conv.weight");  // [D][1][k]
+    const int k = (int)shape(c + "depthwise_conv.weight").at(2);
+    const auto& dwb = need(get, c + "depthwise_conv.bias");
+    const auto& g = need(get, c + "norm.weight");
+    const auto& be = need(get, c + "norm.bias");
+    const auto& rm = need(get, c + "norm.running_mean");
+    const auto& rv = need(get, c + "norm.running_var");
+    std::vector<float> wf((size_t)D * k), bf(D);
+    for (int ch = 0; ch < D; ++ch) {
+      const float s = g[ch] / std::sqrt(rv[ch] + eps);
+      for (int j = 0; j < k; ++j) wf[(size_t)ch * k + j] = dw[(size_t)ch * k + j] * s;
+      bf[ch] = (dwb[ch] - rm[ch]) * s + be[ch];
+    }
+    L.dw_w = upf(wf);
+    L.dw_b = upf(bf);
+    L.dw_k = k;
+    L.ln_mac = ln(get, p + "ff_macaron_layer_norm");
+    L.ln_att = ln(get, p + "self_attn_layer_norm");
+    L.ln_conv = ln(get, p + "conv_layer_norm");
+    L.ln_ff = ln(get, p + "ff_layer_norm");
+    L.ln_final = ln(get, p + "final_layer_norm");
+    return L;
+  }
+
+  Predictor predictor(const GetData& get, const GetShape& shape, const std::string& p) {
+    Predictor P;
+    for (int i = 0;; ++i) {
+      const std::string q = p + "conv_layers." + std::to_string(i) + ".";
+      if (!get(q + "conv.weight")) break;
+      const int k = (int)shape(q + "conv.weight").at(2);
+      P.convs.push_back(conv(get, shape, q + "conv.weight", q + "conv.bias", (k - 1) / 2));
+      P.lns.push_back(ln(get, q + "layer_norm"));
+    }
+    if (P.convs.empty()) throw TtsError(TTS_ERR_STATE, "predictor without layers: " + p);
+    P.lin_w = upf(need(get, p + "linear.weight"));
+    P.lin_b = need(get, p + "linear.bias").at(0);
+    return P;
+  }
+
+  // relative-position table through linear_pos, rows q <-> rel = rmax-1-q (HF:723-752, 419)
+  void build_ptabs(int new_rmax, hipStream_t s) {
+    const int rows = 2 * new_rmax;
+    std::vector<float> pe((size_t)rows * D, 0.f);
+    for (int q = 0; q < 2 * new_rmax - 1; ++q) {
+      const float rel = (float)(new_rmax - 1 - q);
+      for (int i = 0; i < D / 2; ++i) {
+        const float div = std::exp((float)(2 * i) * (float)(-(std::log(10000.0) / D)));
+        const double ang = (double)(rel * div);
+        pe[(size_t)q * D + 2 * i] = (float)std::sin(ang);
+        pe[(size_t)q * D + 2 * i + 1] = (float)std::cos(ang);
+      }
+    }
+    void* ped = upload(pe, dt);
+    for (auto* stack : {&enc, &dec})
+      for (auto& L : *stack) {
+        if (L.ptab) {
+          hipFree(L.ptab);
+          for (auto& a : allocs) if (a == L.ptab) a = nullptr;
+        }
+        void* t = nullptr;
+        HIP_CHECK(hipMalloc(&t, (size_t)rows * D * dtype_size(dt)));
+        L.ptab = track(t);
+        run_layer(L.pos, ped, rows, nullptr, L.ptab, rows, 1, dt, s, nullptr);
+      }
+    HIP_CHECK(hipStreamSynchronize(s));
+    hipFree(ped);
+    rmax = new_rmax;
+  }
+
+  // ---------------------------------------------------------------- workspace
+  void* alloc_ws(size_t elems, size_t esz) {
+    void* p = nullptr;
+    HIP_CHECK(hipMalloc(&p, std::max<size_t>(elems, 1) * esz));
+    HIP_CHECK(hipMemset(p, 0, std::max<size_t>(elems, 1) * esz));
+    ws.push_back(p);
+    return p;
+  }
+
+  void reserve(int B, int N, int T) {
+    if (B <= cap_B && N <= cap_N && T <= cap_T) return;
+    B = std::max(B, cap_B); N = std::max(N, cap_N); T = std::max(T, cap_T);
+    for (void* p : ws) hipFree(p);
+    ws.clear();
+    const size_t e = dtype_size(dt);
+    const int Tm = std::max(N, T);
+    const int Tp = rup(Tm, 32);
+    const int dk = D / H;
+    const size_t rows = (size_t)B * Tp;
+    X = alloc_ws(rows * D, e); Y = alloc_ws(rows * D, e); O = alloc_ws(rows * D, e); G = alloc_ws(rows * D, e);
+    Qu = alloc_ws(rows * D, e); Qv = alloc_ws(rows * D, e);
+    H1 = alloc_ws(rows * FFN, e); QKV = alloc_ws(rows * 3 * D, e); A = alloc_ws(rows * 2 * D, e);
+    const int Sk = rup(Tm, 16), Sac = rup(Tm, 16), Sbd = rup(2 * Tm, 16);
+    Vt = alloc_ws((size_t)B * H * dk * Sk, e);
+    AC = alloc_ws((size_t)B * H * Tm * Sac, e);
+    BD = alloc_ws((size_t)B * H * Tm * Sbd, e);
+    P = alloc_ws((size_t)B * H * Tm * Sk, e);
+    const size_t nrows = (size_t)B * rup(N, 32);
+    ENC = alloc_ws(nrows * D, e);
+    PB1 = alloc_ws(nrows * PRED, e); PB2 = alloc_ws(nrows * PRED, e);
+    const size_t trows = (size_t)B * rup(T, 32);
+    BEF = alloc_ws(trows * NMEL, e); MELT = alloc_ws(trows * NMEL, e);
+    PN1 = alloc_ws(trows * PRED, e); PN2 = alloc_ws(trows * PRED, e);
+    f_pitch = (float*)alloc_ws(nrows, 4); f_energy = (float*)alloc_ws(nrows, 4); f_logd = (float*)alloc_ws(nrows, 4);
+    i_dur = (int*)alloc_ws((size_t)B * N, 4);
+    i_tokmap = (int*)alloc_ws((size_t)B * T, 4);
+    cap_B = B; cap_N = N; cap_T = T;
+  }
+
+  // ---------------------------------------------------------------- forward
+  void ln_rows(const void* in, void* out, int rows, int C, const LNParam& a, const LNParam* b, hipStream_t s) {
+    HIP_CHECK(launch_layernorm(dt, in, out, rows, C, a.g, a.b, b ? b->g : nullptr, b ? b->b : nullptr, eps, s));
+  }
+
+  // one head-batched attention GEMM: Y[b,h][n][m] = sum_c X[b,h][n][c] * W[b,h][m][c]
+  void attn_gemm(const void* x, long long sxb, long long sxh, int sxr, const int* lens, int x_rows, const void* w,
+                 long long swb, long long swh, int w_ld, int M, int K, void* y, long long syb, long long syh,
+                 int syr, int B, hipStream_t s) {
+    ConvParams p = conv_params_default();
+    p.x = x; p.sxb = sxb; p.sxh = sxh; p.sxr = sxr; p.x_len = lens; p.x_rows = x_rows;
+    p.w = w; p.swb = swb; p.swh = swh; p.w_ld = w_ld;
+    p.y = y; p.syb = syb; p.syh = syh; p.syr = syr;
+    p.y_len = lens; p.y_rows = x_rows;
+    p.M = M; p.Cin = K; p.taps = 1; p.dil = 1; p.pad = 0;
+    p.B = B; p.nh = H;
+    launch_conv_checked(p, dt, s, prof, 2.0 * M * (double)K * x_rows * B * H);
+  }
+
+  void stack(std::vector<ConformerLayer>& layers, void* Xb, const int* lens, int B, int Tm, hipStream_t s) {
+    const int Tp = rup(Tm, 32);
+    const int dk = D / H;
+    const int rows = B * Tp;
+    const int Sk = rup(Tm, 16), Sac = rup(Tm, 16), Sbd = rup(2 * Tm, 16);
+    const int Mk = rup(Tm, 4), Mbd = rup(2 * Tm - 1, 4);
+    const float scale = 1.0f / std::sqrt((float)dk);
+    for (auto& L : layers) {
+      // macaron FFN: x = LN(x + 0.5 * ffn(x))
+      run_layer(L.ffm1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
+      run_layer(L.ffm2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
+      ln_rows(Y, Xb, rows, D, L.ln_mac, nullptr, s);
+      // relative-position MHSA: x = LN(x + mhsa(x))
+      run_layer(L.qkv, Xb, Tp, lens, QKV, Tp, B, dt, s, prof);
+      HIP_CHECK(launch_pos_bias(dt, QKV, rows, D, L.pos_u, L.pos_v, Qu, Qv, s));
+      HIP_CHECK(launch_transpose_v(dt, QKV, lens, B, Tp, D, H, Sk, Vt, s));
+      const size_t e = dtype_size(dt);
+      // AC[b,h][i][j] = Qu[b][i][h] . K[b][j][h]
+      attn_gemm(Qu, (long long)Tp * D, dk, D, lens, Tm, (const char*)QKV + (size_t)D * e, (long long)Tp * 3 * D, dk,
+                3 * D, Mk, dk, AC, (long long)H * Tm * Sac, (long long)Tm * Sac, Sac, B, s);
+      // BD[b,h][i][q] = Qv[b][i][h] . Ptab[rmax - Tm + q][h]   (q <-> rel = Tm-1-q)
+      attn_gemm(Qv, (long long)Tp * D, dk, D, lens, Tm, (const char*)L.ptab + (size_t)(rmax - Tm) * D * e, 0, dk, D,
+                Mbd, dk, BD, (long long)H * Tm * Sbd, (long long)Tm * Sbd, Sbd, B, s);
+      HIP_CHECK(launch_rel_softmax(dt, AC, BD, lens, B, H, Tm, Sac, Sbd, Sk, scale, P, s));
+      // O[b][i][h*dk + d] = sum_j P[b,h][i][j] * Vt[b,h][d][j]
+      attn_gemm(P, (long long)H * Tm * Sk, (long long)Tm * Sk, Sk, lens, Tm, Vt, (long long)H * dk * Sk,
+                (long long)dk * Sk, Sk, dk, Sk, O, (long long)Tp * D, dk, D, B, s);
+      run_layer(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
+      ln_rows(Y, Xb, rows, D, L.ln_att, nullptr, s);
+      // conv module: x = LN(x + pw2(silu(bn(dw(glu(pw1(x)))))))
+      run_layer(L.pw1, Xb, Tp, lens, A, Tp, B, dt, s, prof);
+      HIP_CHECK(launch_glu_dwconv(dt, A, lens, B, Tp, D, L.dw_w, L.dw_k, L.dw_b, G, s));
+      run_layer(L.pw2, G, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
+      ln_rows(Y, Xb, rows, D, L.ln_conv, nullptr, s);
+      // FFN: x = final_LN(LN(x + 0.5 * ffn(x)))
+      run_layer(L.ff1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
+      run_layer(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
+      ln_rows(Y, Xb, rows, D, L.ln_ff, &L.ln_final, s);
+    }
+  }
+
+  void predict(Predictor& Pr, const void* x, const int* lens, int B, int Np, float* out, hipStream_t s) {
+    const void* h = x;
+    void* bufs[2] = {PB1, PB2};
+    const int n = (int)Pr.convs.size();
+    for (int i = 0; i < n; ++i) {
+      void* o = bufs[i & 1];
+      run_layer(Pr.convs[i], h, Np, lens, o, Np, B, dt, s, prof, 1.f, ACT_RELU);
+      if (i + 1 < n) ln_rows(o, o, B * Np, PRED, Pr.lns[i], nullptr, s);
+      else HIP_CHECK(launch_ln_linear1(dt, o, B * Np, PRED, Pr.lns[i].g, Pr.lns[i].b, eps, Pr.lin_w, Pr.lin_b, out, s));
+      h = o;
+    }
+  }
+
+  void forward(const int* tokens, const int* tok_lens, int B, int N, const int* dur_override, float* mel,
+               int* mel_lens, int Tcap, int* durations, hipStream_t s) {
+    reserve(B, N, Tcap);
+    const int Tm = std::max(N, Tcap);
+    if (Tm > rmax) build_ptabs(rup(Tm, 256), s);
+    const float xscale = std::sqrt((float)D);
+    const int Np = rup(N, 32), Tp = rup(Tcap, 32);
+    // encoder
+    HIP_CHECK(launch_embed(dt, tokens, tok_lens, B, N, Np, embed, V, D, xscale, ENC, s));
+    stack(enc, ENC, tok_lens, B, N, s);
+    // variance adaptor (HF:1198-1218)
+    predict(pitch, ENC, tok_lens, B, Np, f_pitch, s);
+    predict(energy, ENC, tok_lens, B, Np, f_energy, s);
+    predict(duration, ENC, tok_lens, B, Np, f_logd, s);
+    // logd is laid out [B][Np]; durations kernel reads [B][N] rows -> compact view via stride Np
+    int* dur = durations ? durations : i_dur;
+    HIP_CHECK(launch_durations_strided(s, B, N, Np, tok_lens, dur_override, Tcap, dur, mel_lens));
+    HIP_CHECK(launch_var_embed_add(dt, ENC, B * Np, D, f_energy, ee_w, ee_b, f_pitch, pe_w, pe_b, s));
+    // decoder rows are laid out with stride Tp; regulate writes [B][Tcap] rows
+    void* Xd = X;
+    if (Tp == Tcap) {
+      HIP_CHECK(launch_regulate(dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, X, s));
+    } else {
+      HIP_CHECK(launch_regulate(dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, Y, s));
+      HIP_CHECK(hipMemcpy2DAsync(X, (size_t)Tp * D * dtype_size(dt), Y, (size_t)Tcap * D * dtype_size(dt),
+                                 (size_t)Tcap * D * dtype_size(dt), B, hipMemcpyDeviceToDevice, s));
+    }
+    stack(dec, Xd, mel_lens, B, Tcap, s);
+    // postnet (HF:238-244), BatchNorm folded
+    run_layer(feat_out, Xd, Tp, mel_lens, BEF, Tp, B, dt, s, prof);
+    const void* h = BEF;
+    void* bufs[2] = {PN1, PN2};
+    const int n = (int)postnet.size();
+    for (int i = 0; i < n; ++i) {
+      const bool last = i == n - 1;
+      void* o = last ? MELT : bufs[i & 1];
+      run_layer(postnet[i], h, Tp, mel_lens, o, Tp, B, dt, s, prof, 1.f, last ? ACT_NONE : ACT_TANH, 1.f,
+                last ? BEF : nullptr);
+      h = o;
+    }
+    // MELT rows have stride Tp; output [B][Tcap][80] float32
+    if (Tp == Tcap) {
+      HIP_CHECK(launch_mel_out(dt, MELT, mel_lens, B, Tcap, NMEL, mel, s));
+    } else {
+      HIP_CHECK(hipMemcpy2DAsync(BEF, (size_t)Tcap * NMEL * dtype_size(dt), MELT, (size_t)Tp * NMEL * dtype_size(dt),
+                                 (size_t)Tcap * NMEL * dtype_size(dt), B, hipMemcpyDeviceToDevice, s));
+      HIP_CHECK(launch_mel_out(dt, BEF, mel_lens, B, Tcap, NMEL, mel, s));
+    }
+  }
+
+  hipError_t launch_durations_strided(hipStream_t s, int B, int N, int Np, const int* tok_lens, const int* ovr,
+                                      int Tcap, int* dur, int* mel_lens) {
+    // compact f_logd [B][Np] -> [B][N] in place is unsafe; copy into PB1 (float view) first
+    float* logd = f_logd;
+    if (Np != N) {
+      HIP_CHECK(hipMemcpy2DAsync(PB1, (size_t)N * 4, f_logd, (size_t)Np * 4, (size_t)N * 4, B,
+                                 hipMemcpyDeviceToDevice, s));
+      logd = (float*)PB1;
+    }
+    return launch_durations(logd, tok_lens, B, N, ovr, 1.0f, Tcap, dur, mel_lens, i_tokmap, s);
+  }
+};
+
+void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtype, Profiler* prof) {
+  if (!get("encoder.embed.weight")) {
+    loaded = false;
+    return;
+  }
+  std::unique_ptr<Impl> m(new Impl());
+  m->dt = dtype;
+  m->prof = prof;
+  const auto es = shape("encoder.embed.weight");
+  m->V = (int)es.at(0);
+  m->D = (int)es.at(1);
+  m->H = (int)shape("encoder.conformer_layers.0.self_attn.pos_bias_u").at(0);
+  m->FFN = (int)shape("encoder.conformer_layers.0.feed_forward.conv1.weight").at(0);
+  m->PRED = (int)shape("duration_predictor.conv_layers.0.conv.weight").at(0);
+  m->NMEL = (int)shape("speech_decoder_postnet.feat_out.weight").at(0);
+  if (m->D % 64 || m->D > 512 || (m->D / m->H) % 16) throw TtsError(TTS_ERR_INVALID, "unsupported hidden size");
+  m->embed = m->track(upload(*get("encoder.embed.weight"), dtype));
+  for (int i = 0; get("encoder.conformer_layers." + std::to_string(i) + ".self_attn.pos_bias_u"); ++i)
+    m->enc.push_back(m->layer(get, shape, "encoder.conformer_layers." + std::to_string(i) + "."));
+  for (int i = 0; get("decoder.conformer_layers." + std::to_string(i) + ".self_attn.pos_bias_u"); ++i)
+    m->dec.push_back(m->layer(get, shape, "decoder.conformer_layers." + std::to_string(i) + "."));
+  m->pitch = m->predictor(get, shape, "pitch_predictor.");
+  m->energy = m->predictor(get, shape, "energy_predictor.");
+  m->duration = m->predictor(get, shape, "duration_predictor.");
+  m->pe_w = m->upf(m->need(get, "pitch_embed.conv.weight"));
+  m->pe_b = m->upf(m->need(get, "pitch_embed.conv.bias"));
+  m->ee_w = m->upf(m->need(get, "energy_embed.conv.weight"));
+  m->ee_b = m->upf(m->need(get, "energy_embed.conv.bias"));
+  m->feat_out = m->conv(get, shape, "speech_decoder_postnet.feat_out.weight", "speech_decoder_postnet.feat_out.bias", 0);
+  for (int i = 0;; ++i) {
+    const std::string p = "speech_decoder_postnet.layers." + std::to_string(i) + ".";
+    if (!get(p + "conv.weight")) break;
+    const auto s = shape(p + "conv.weight");
+    const int co = (int)s.at(0), k = (int)s.at(2);
+    const auto& g = m->need(get, p + "batch_norm.weight");
+    const auto& be = m->need(get, p + "batch_norm.bias");
+    const auto& rm = m->need(get, p + "batch_norm.running_mean");
+    const auto& rv = m->need(get, p + "batch_norm.running_var");
+    std::vector<float> sc(co), bb(co);
+    for (int o = 0; o < co; ++o) {
+      sc[o] = g[o] / std::sqrt(rv[o] + m->eps);
+      bb[o] = be[o] - rm[o] * sc[o];  // conv has no bias
+    }
+    m->postnet.push_back(m->conv(get, shape, p + "conv.weight", "", (k - 1) / 2, &sc, &bb));
+  }
+  m->build_ptabs(1024, nullptr);
+  impl = m.release();
+  loaded = true;
+}
+
+void AcousticModel::reserve(int B, int N, int T) {
+  if (impl) impl->reserve(B, N, T);
+}
+
+void AcousticModel::forward(const int32_t* tokens, const int32_t* tok_lens, int B, int N, const int32_t* dur_override,
+                            float* mel, int32_t* mel_lens, int Tcap, int32_t* durations, hipStream_t s) {
+  if (!impl) throw TtsError(TTS_ERR_STATE, "acoustic model not loaded");
+  impl->forward(tokens, tok_lens, B, N, dur_override, mel, mel_lens, Tcap, durations, s);
+}
+
+void AcousticModel::free_all() {
+  delete impl;
+  impl = nullptr;
   loaded = false;
-  (void)get;
 }
-void AcousticModel::reserve(int, int, int) {}
-void AcousticModel::forward(const int32_t*, const int32_t*, int, int, const int32_t*, float*, int32_t*, int,
-                            int32_t*, hipStream_t) {
-  throw std::runtime_error("acoustic model not implemented");
-}
-void AcousticModel::free_all() {}
 
 }  // namespace tts

@@ -9,11 +9,13 @@
 
 namespace tts {
 
+struct Profiler;
+
 struct AcousticModel {
   bool loaded = false;
   typedef std::function<const std::vector<float>*(const std::string&)> GetData;
   typedef std::function<std::vector<int64_t>(const std::string&)> GetShape;
-  void finalize(const GetData& get, const GetShape& shape, int dtype);
+  void finalize(const GetData& get, const GetShape& shape, int dtype, Profiler* prof);
   void reserve(int B, int N, int T);
   void forward(const int32_t* tokens, const int32_t* tok_lens, int B, int N, const int32_t* dur_override,
                float* mel, int32_t* mel_lens, int Tcap, int32_t* durations, hipStream_t s);

@@ -1,0 +1,30 @@
+// Launchers of the acoustic-model row-wise kernels (acoustic_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace tts {
+
+hipError_t launch_embed(int dt, const int* ids, const int* lens, int B, int N, int Tm, const void* E, int V, int D,
+                        float scale, void* out, hipStream_t s);
+hipError_t launch_layernorm(int dt, const void* in, void* out, int rows, int C, const float* g1, const float* b1,
+                            const float* g2, const float* b2, float eps, hipStream_t s);
+hipError_t launch_pos_bias(int dt, const void* qkv, int rows, int D, const float* u, const float* v, void* qu,
+                           void* qv, hipStream_t s);
+hipError_t launch_transpose_v(int dt, const void* qkv, const int* lens, int B, int Tm, int D, int H, int Sk, void* vt,
+                              hipStream_t s);
+hipError_t launch_rel_softmax(int dt, const void* ac, const void* bd, const int* lens, int B, int H, int Tm, int Sac,
+                              int Sbd, int Sk, float scale, void* p, hipStream_t s);
+hipError_t launch_glu_dwconv(int dt, const void* a, const int* lens, int B, int Tm, int D, const float* w, int k,
+                             const float* bias, void* out, hipStream_t s);
+hipError_t launch_ln_linear1(int dt, const void* in, int rows, int C, const float* g, const float* b, float eps,
+                             const float* w, float wb, float* out, hipStream_t s);
+hipError_t launch_durations(const float* logd, const int* lens, int B, int N, const int* override_d, float speed,
+                            int Tcap, int* dur, int* mel_lens, int* tokmap, hipStream_t s);
+hipError_t launch_var_embed_add(int dt, void* x, int rows, int D, const float* e, const float* we, const float* be,
+                                const float* p, const float* wp, const float* bp, hipStream_t s);
+hipError_t launch_regulate(int dt, const void* enc, int B, int N, int D, const int* tokmap, int Tcap, float scale,
+                           void* out, hipStream_t s);
+hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, int Tcap, int C, float* out,
+                          hipStream_t s);
+
+}  // namespace tts

@@ -1,0 +1,451 @@
+// Non-GEMM kernels of the FastSpeech2-Conformer acoustic model (oracle/acoustic.py).
+// The dense contractions (FFN convs, projections, attention products) run on the
+// implicit-GEMM MFMA kernel (conv_gemm.hip); these are the row-wise / integer steps.
+//
+// Activations: [B][Tm][C] channels-last in the compute dtype T; per-utterance valid
+// lengths `lens[b]` give B=1 semantics (rows >= len are never read by valid rows).
+#include "acoustic_kernels.h"
+#include "common.h"
+
+namespace tts {
+
+// ---------------------------------------------------------------------------
+// token embedding * sqrt(D)   (HF:793-795 embed, HF:763 input_scale)
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void embed_kernel(const int* __restrict__ ids, const int* __restrict__ lens, int N, int Tm,
+                             const T* __restrict__ E, int V, int D, float scale, T* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int t = blockIdx.x;
+  const int L = min(lens[b], N);
+  T* o = out + ((long long)b * Tm + t) * D;
+  if (t >= L) {
+    for (int c = threadIdx.x; c < D; c += blockDim.x) o[c] = from_f32<T>(0.f);
+    return;
+  }
+  int id = ids[(long long)b * N + t];
+  id = min(max(id, 0), V - 1);
+  const T* e = E + (long long)id * D;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) o[c] = from_f32<T>(to_f32(e[c]) * scale);
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm over C (one wave per row), optional second LayerNorm applied after
+// (ff_layer_norm followed by final_layer_norm, HF:644-647).  Two-pass variance in fp32.
+// ---------------------------------------------------------------------------
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, int PER>
+__global__ __launch_bounds__(256) void layernorm_kernel(const T* __restrict__ in, T* __restrict__ out, int rows,
+                                                       int C, const float* __restrict__ g1,
+                                                       const float* __restrict__ b1, const float* __restrict__ g2,
+                                                       const float* __restrict__ b2, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const T* x = in + (long long)row * C;
+  float v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < C ? to_f32(x[c]) : 0.f;
+  }
+  const float invC = 1.f / (float)C;
+  for (int pass = 0; pass < (g2 ? 2 : 1); ++pass) {
+    const float* g = pass ? g2 : g1;
+    const float* bb = pass ? b2 : b1;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) s += v[i];
+    const float mu = wave_sum(s) * invC;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      const float d = c < C ? v[i] - mu : 0.f;
+      q += d * d;
+    }
+    const float rstd = rsqrtf(wave_sum(q) * invC + eps);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      if (c < C) {
+        float y = (v[i] - mu) * rstd * g[c] + bb[c];
+        if (pass == 0 && g2) y = to_f32(from_f32<T>(y));  // first LN output is materialised in T
+        v[i] = y;
+      }
+    }
+  }
+  T* o = out + (long long)row * C;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    if (c < C) o[c] = from_f32<T>(v[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// attention prep: Qu = q + pos_bias_u, Qv = q + pos_bias_v (HF:420-423) from QKV [rows][3D]
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void pos_bias_kernel(const T* __restrict__ qkv, int rows, int D, const float* __restrict__ u,
+                                const float* __restrict__ v, T* __restrict__ qu, T* __restrict__ qv) {
+  const long long n = (long long)rows * D;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / D;
+    const int c = (int)(i - r * D);
+    const float q = to_f32(qkv[r * 3 * D + c]);
+    qu[i] = from_f32<T>(q + u[c]);
+    qv[i] = from_f32<T>(q + v[c]);
+  }
+}
+
+// Vt[b][h][d][j] = v[b][j][h*dk + d] for j < len[b], 0 for len <= j < Sk
+template <typename T>
+__global__ void transpose_v_kernel(const T* __restrict__ qkv, const int* __restrict__ lens, int Tm, int D, int H,
+                                   int Sk, T* __restrict__ vt) {
+  __shared__ float tile[32][33];
+  const int dk = D / H;
+  const int bh = blockIdx.z;
+  const int b = bh / H, h = bh - b * H;
+  const int L = min(lens[b], Tm);
+  const int j0 = blockIdx.x * 32, d0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
+  for (int r = ty; r < 32; r += 8) {
+    const int j = j0 + r, d = d0 + tx;
+    float val = 0.f;
+    if (j < L && d < dk) val = to_f32(qkv[((long long)b * Tm + j) * 3 * D + 2 * D + h * dk + d]);
+    tile[r][tx] = val;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int d = d0 + r, j = j0 + tx;
+    if (d < dk && j < Sk) vt[(((long long)b * H + h) * dk + d) * Sk + j] = from_f32<T>(tile[tx][r]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// scores = (AC[i][j] + BD[i][(Tm-1) - i + j]) / sqrt(dk), key-masked softmax (HF:430-449,
+// shift_relative_position_tensor HF:381-393).  One wave per query row.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void rel_softmax_kernel(const T* __restrict__ ac, const T* __restrict__ bd,
+                                                         const int* __restrict__ lens, int H, int Tm, int Sac,
+                                                         int Sbd, int Sk, float scale, T* __restrict__ pout) {
+  const int bh = blockIdx.y;
+  const int b = bh / H;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= Tm) return;
+  const int L = max(min(lens[b], Tm), 1);
+  const T* acr = ac + ((long long)bh * Tm + i) * Sac;
+  const T* bdr = bd + ((long long)bh * Tm + i) * Sbd + (Tm - 1 - i);
+  T* pr = pout + ((long long)bh * Tm + i) * Sk;
+  float mx = -INFINITY;
+  for (int j = lane; j < L; j += 64) {
+    const float s = (to_f32(acr[j]) + to_f32(bdr[j])) * scale;
+    mx = fmaxf(mx, s);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  float sum = 0.f;
+  for (int j = lane; j < L; j += 64) sum += __expf((to_f32(acr[j]) + to_f32(bdr[j])) * scale - mx);
+  sum = wave_sum(sum);
+  const float inv = 1.f / sum;
+  for (int j = lane; j < Sk; j += 64) {
+    float pv = 0.f;
+    if (j < L) pv = __expf((to_f32(acr[j]) + to_f32(bdr[j])) * scale - mx) * inv;
+    pr[j] = from_f32<T>(pv);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Conformer conv module core (HF:501-535): g = a[:, :D] * sigmoid(a[:, D:]) (GLU),
+// depthwise conv k (zero padded per utterance), BatchNorm folded into (w, b), SiLU.
+// Block: 64 channels x TR rows; LDS holds the GLU output with the halo in fp32.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void glu_dwconv_kernel(const T* __restrict__ a, const int* __restrict__ lens,
+                                                        int Tm, int D, const float* __restrict__ w, int k,
+                                                        const float* __restrict__ bias, T* __restrict__ out) {
+  constexpr int TR = 128, CB = 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* g = reinterpret_cast<float*>(smem);  // [(TR + k - 1)][CB]
+  const int b = blockIdx.z;
+  const int t0 = blockIdx.x * TR;
+  const int c0 = blockIdx.y * CB;
+  const int L = min(lens[b], Tm);
+  if (t0 >= L) return;
+  const int pad = (k - 1) / 2;
+  const int rows = TR + k - 1;
+  const T* ab = a + (long long)b * Tm * 2 * D;
+  for (int i = threadIdx.x; i < rows * CB; i += 256) {
+    const int r = i / CB, c = i - r * CB;
+    const int t = t0 - pad + r;
+    float val = 0.f;
+    if (t >= 0 && t < L && c0 + c < D) {
+      const float x = to_f32(ab[(long long)t * 2 * D + c0 + c]);
+      const float gt = to_f32(ab[(long long)t * 2 * D + D + c0 + c]);
+      val = x * (1.f / (1.f + __expf(-gt)));
+    }
+    g[i] = val;
+  }
+  __syncthreads();
+  const int c = threadIdx.x & (CB - 1);
+  const int rg = threadIdx.x / CB;  // 4 row groups
+  if (c0 + c >= D) return;
+  const float* wc = w + (long long)(c0 + c) * k;
+  const float bc = bias[c0 + c];
+  T* ob = out + (long long)b * Tm * D;
+  for (int r = rg; r < TR; r += 4) {
+    const int t = t0 + r;
+    if (t >= L) break;
+    float acc = bc;
+    for (int j = 0; j < k; ++j) acc = fmaf(wc[j], g[(r + j) * CB + c], acc);
+    const float y = acc / (1.f + __expf(-acc));  // SiLU
+    ob[(long long)t * D + c0 + c] = from_f32<T>(y);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// variance-predictor head: LayerNorm(C) then Linear(C -> 1) (HF:261-271, 318)
+// ---------------------------------------------------------------------------
+template <typename T, int PER>
+__global__ __launch_bounds__(256) void ln_linear1_kernel(const T* __restrict__ in, int rows, int C,
+                                                        const float* __restrict__ g, const float* __restrict__ bb,
+                                                        float eps, const float* __restrict__ w, float wb,
+                                                        float* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const T* x = in + (long long)row * C;
+  float v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < C ? to_f32(x[c]) : 0.f;
+    s += v[i];
+  }
+  const float mu = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    const float d = c < C ? v[i] - mu : 0.f;
+    q += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+  float dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    if (c < C) {
+      const float y = to_f32(from_f32<T>((v[i] - mu) * rstd * g[c] + bb[c]));
+      dot = fmaf(y, w[c], dot);
+    }
+  }
+  dot = wave_sum(dot);
+  if (lane == 0) out[row] = dot + wb;
+}
+
+// ---------------------------------------------------------------------------
+// durations (HF:183 clamp(round(exp(x) - 1), 0); length_regulator speed + all-zero rule
+// HF:104-109, per utterance), exclusive prefix sums, mel lengths (clamped to Tcap) and the
+// frame -> token map.  One block per utterance.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void durations_kernel(const float* __restrict__ logd, const int* __restrict__ lens,
+                                                       int N, const int* __restrict__ override_d, float speed,
+                                                       int Tcap, int* __restrict__ dur, int* __restrict__ mel_lens,
+                                                       int* __restrict__ tokmap) {
+  extern __shared__ int sm[];  // cum[N + 1]
+  __shared__ int total;
+  const int b = blockIdx.x;
+  const int L = min(lens[b], N);
+  int* cum = sm;
+  for (int t = threadIdx.x; t < N; t += blockDim.x) {
+    int d = 0;
+    if (t < L) {
+      if (override_d) {
+        d = max(override_d[(long long)b * N + t], 0);
+      } else {
+        const float x = logd[(long long)b * N + t];
+        d = (int)fmaxf(rintf(expf(x) - 1.0f), 0.f);  // rint = round half to even, like torch.round
+      }
+      if (speed != 1.0f) d = (int)rintf((float)d * speed);
+    }
+    cum[t + 1] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    cum[0] = 0;
+    int s = 0;
+    for (int t = 1; t <= N; ++t) s += cum[t];
+    if (s == 0 && L > 0) {  // all-zero rule: every token gets one frame
+      for (int t = 1; t <= N; ++t) cum[t] = (t <= L) ? 1 : 0;
+    }
+    for (int t = 1; t <= N; ++t) cum[t] += cum[t - 1];  // inclusive -> cumulative
+    total = min(cum[N], Tcap);
+    mel_lens[b] = total;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < N; t += blockDim.x) dur[(long long)b * N + t] = cum[t + 1] - cum[t];
+  const int tot = total;
+  for (int f = threadIdx.x; f < Tcap; f += blockDim.x) {
+    int tok = -1;
+    if (f < tot) {
+      int lo = 0, hi = N - 1;  // first t with cum[t+1] > f
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cum[mid + 1] > f) hi = mid; else lo = mid + 1;
+      }
+      tok = lo;
+    }
+    tokmap[(long long)b * Tcap + f] = tok;
+  }
+}
+
+// x[row][c] = (x + (e[row] * we[c] + be[c])) + (p[row] * wp[c] + bp[c])    (HF:1216-1218)
+template <typename T>
+__global__ void var_embed_add_kernel(T* __restrict__ x, int rows, int D, const float* __restrict__ e,
+                                     const float* __restrict__ we, const float* __restrict__ be,
+                                     const float* __restrict__ p, const float* __restrict__ wp,
+                                     const float* __restrict__ bp) {
+  const long long n = (long long)rows * D;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / D;
+    const int c = (int)(i - r * D);
+    const float ee = to_f32(from_f32<T>(e[r] * we[c] + be[c]));
+    const float pp = to_f32(from_f32<T>(p[r] * wp[c] + bp[c]));
+    const float y = to_f32(from_f32<T>(to_f32(x[i]) + ee));
+    x[i] = from_f32<T>(y + pp);
+  }
+}
+
+// length regulator gather (HF:82-126) fused with the decoder's input_scale (HF:763)
+template <typename T>
+__global__ void regulate_kernel(const T* __restrict__ enc, int N, int D, const int* __restrict__ tokmap, int Tcap,
+                                float scale, T* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int f = blockIdx.x;
+  const int tok = tokmap[(long long)b * Tcap + f];
+  T* o = out + ((long long)b * Tcap + f) * D;
+  if (tok < 0) {
+    for (int c = threadIdx.x; c < D; c += blockDim.x) o[c] = from_f32<T>(0.f);
+    return;
+  }
+  const T* s = enc + ((long long)b * N + tok) * D;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) o[c] = from_f32<T>(to_f32(s[c]) * scale);
+}
+
+// mel [B][Tcap][C] (T) -> float32 [B][Tcap][C], rows >= mel_len zeroed
+template <typename T>
+__global__ void mel_out_kernel(const T* __restrict__ in, const int* __restrict__ mel_lens, int Tcap, int C,
+                               float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const long long n = (long long)Tcap * C;
+  const int L = mel_lens[b];
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int t = (int)(i / C);
+    out[(long long)b * n + i] = t < L ? to_f32(in[(long long)b * n + i]) : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+#define TTS_DISPATCH(dtype, KERNEL_CALL)                       \
+  switch (dtype) {                                             \
+    case DT_F32: { typedef float TT; KERNEL_CALL; break; }     \
+    case DT_F16: { typedef half_t TT; KERNEL_CALL; break; }    \
+    case DT_BF16: { typedef bf16_t TT; KERNEL_CALL; break; }   \
+    default: return hipErrorInvalidValue;                      \
+  }                                                            \
+  return hipGetLastError();
+
+static unsigned grid1(long long n) { long long g = (n + 255) / 256; return (unsigned)(g < 4096 ? (g > 0 ? g : 1) : 4096); }
+
+hipError_t launch_embed(int dt, const int* ids, const int* lens, int B, int N, int Tm, const void* E, int V, int D,
+                        float scale, void* out, hipStream_t s) {
+  TTS_DISPATCH(dt, hipLaunchKernelGGL(embed_kernel<TT>, dim3(Tm, B), dim3(128), 0, s, ids, lens, N, Tm,
+                                      (const TT*)E, V, D, scale, (TT*)out));
+}
+
+hipError_t launch_layernorm(int dt, const void* in, void* out, int rows, int C, const float* g1, const float* b1,
+                            const float* g2, const float* b2, float eps, hipStream_t s) {
+  if (C > 512) return hipErrorInvalidValue;
+  dim3 grid((rows + 3) / 4);
+  if (C <= 256) {
+    TTS_DISPATCH(dt, hipLaunchKernelGGL((layernorm_kernel<TT, 4>), grid, dim3(256), 0, s, (const TT*)in, (TT*)out,
+                                        rows, C, g1, b1, g2, b2, eps));
+  }
+  TTS_DISPATCH(dt, hipLaunchKernelGGL((layernorm_kernel<TT, 8>), grid, dim3(256), 0, s, (const TT*)in, (TT*)out, rows,
+                                      C, g1, b1, g2, b2, eps));
+}
+
+hipError_t launch_pos_bias(int dt, const void* qkv, int rows, int D, const float* u, const float* v, void* qu,
+                           void* qv, hipStream_t s) {
+  TTS_DISPATCH(dt, hipLaunchKernelGGL(pos_bias_kernel<TT>, dim3(grid1((long long)rows * D)), dim3(256), 0, s,
+                                      (const TT*)qkv, rows, D, u, v, (TT*)qu, (TT*)qv));
+}
+
+hipError_t launch_transpose_v(int dt, const void* qkv, const int* lens, int B, int Tm, int D, int H, int Sk, void* vt,
+                              hipStream_t s) {
+  dim3 grid((Sk + 31) / 32, (D / H + 31) / 32, B * H);
+  TTS_DISPATCH(dt, hipLaunchKernelGGL(transpose_v_kernel<TT>, grid, dim3(256), 0, s, (const TT*)qkv, lens, Tm, D, H,
+                                      Sk, (TT*)vt));
+}
+
+hipError_t launch_rel_softmax(int dt, const void* ac, const void* bd, const int* lens, int B, int H, int Tm, int Sac,
+                              int Sbd, int Sk, float scale, void* p, hipStream_t s) {
+  dim3 grid((Tm + 3) / 4, B * H);
+  TTS_DISPATCH(dt, hipLaunchKernelGGL(rel_softmax_kernel<TT>, grid, dim3(256), 0, s, (const TT*)ac, (const TT*)bd,
+                                      lens, H, Tm, Sac, Sbd, Sk, scale, (TT*)p));
+}
+
+hipError_t launch_glu_dwconv(int dt, const void* a, const int* lens, int B, int Tm, int D, const float* w, int k,
+                             const float* bias, void* out, hipStream_t s) {
+  dim3 grid((Tm + 127) / 128, (D + 63) / 64, B);
+  const size_t lds = (size_t)(128 + k - 1) * 64 * 4;
+  TTS_DISPATCH(dt, hipLaunchKernelGGL(glu_dwconv_kernel<TT>, grid, dim3(256), lds, s, (const TT*)a, lens, Tm, D, w, k,
+                                      bias, (TT*)out));
+}
+
+hipError_t launch_ln_linear1(int dt, const void* in, int rows, int C, const float* g, const float* b, float eps,
+                             const float* w, float wb, float* out, hipStream_t s) {
+  if (C > 256) return hipErrorInvalidValue;
+  TTS_DISPATCH(dt, hipLaunchKernelGGL((ln_linear1_kernel<TT, 4>), dim3((rows + 3) / 4), dim3(256), 0, s,
+                                      (const TT*)in, rows, C, g, b, eps, w, wb, out));
+}
+
+hipError_t launch_durations(const float* logd, const int* lens, int B, int N, const int* override_d, float speed,
+                            int Tcap, int* dur, int* mel_lens, int* tokmap, hipStream_t s) {
+  hipLaunchKernelGGL(durations_kernel, dim3(B), dim3(256), (size_t)(N + 1) * sizeof(int), s, logd, lens, N,
+                     override_d, speed, Tcap, dur, mel_lens, tokmap);
+  return hipGetLastError();
+}
+
+hipError_t launch_var_embed_add(int dt, void* x, int rows, int D, const float* e, const float* we, const float* be,
+                                const float* p, const float* wp, const float* bp, hipStream_t s) {
+  TTS_DISPATCH(dt, hipLaunchKernelGGL(var_embed_add_kernel<TT>, dim3(grid1((long long)rows * D)), dim3(256), 0, s,
+                                      (TT*)x, rows, D, e, we, be, p, wp, bp));
+}
+
+hipError_t launch_regulate(int dt, const void* enc, int B, int N, int D, const int* tokmap, int Tcap, float scale,
+                           void* out, hipStream_t s) {
+  TTS_DISPATCH(dt, hipLaunchKernelGGL(regulate_kernel<TT>, dim3(Tcap, B), dim3(128), 0, s, (const TT*)enc, N, D,
+                                      tokmap, Tcap, scale, (TT*)out));
+}
+
+hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, int Tcap, int C, float* out,
+                          hipStream_t s) {
+  dim3 grid(grid1((long long)Tcap * C), B);
+  TTS_DISPATCH(dt, hipLaunchKernelGGL(mel_out_kernel<TT>, grid, dim3(256), 0, s, (const TT*)in, mel_lens, Tcap, C,
+                                      out));
+}
+
+}  // namespace tts

@@ -16,21 +16,27 @@
 // tile of X rows, so each input row is fetched from HBM once per block.
 //
 // Tiling: a block = WM x WN waves; each wave owns MT x NT 32x32 MFMA tiles
-// (M = output channels, N = time).  Weights stream straight from L2 into the
-// A fragments (every wave reads distinct rows of W, so there is no intra-block
-// sharing to stage), the X tile is staged through LDS in 64-byte column chunks
-// with a 16-byte row pad (80-byte row stride => ds_read_b128 of 16 consecutive
-// rows hits 16 distinct 4-bank slots: conflict-free).
+// (M = output channels, N = time).  Weights stream from L2 straight into the
+// A fragments, prefetched one tap ahead (every wave reads distinct rows of W,
+// so there is no intra-block sharing to stage through LDS).  The X tile is
+// staged through LDS in CK-channel chunks, double-buffered: the global loads of
+// chunk c+1 are issued into registers before chunk c's MFMAs and written to the
+// other LDS buffer after them (one barrier per chunk).  LDS rows carry a 16-byte
+// pad (row stride 80 B or 144 B) so ds_read_b128 of 16 consecutive rows hits 16
+// distinct 4-bank slots: conflict-free.  Loads are clamped in-bounds and masked
+// after the fact (no per-element branches around loads).
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace tts {
 
+constexpr int HALO_MAX = 64;  // max (taps-1)*dil supported (HiFi-GAN V1: 50)
+
 template <typename T>
-__device__ inline uint4 load16_act(const T* ptr, bool valid, float slope) {
-  uint4 u = {0u, 0u, 0u, 0u};
-  if (!valid) return u;
-  u = *reinterpret_cast<const uint4*>(ptr);
+__device__ inline uint4 act16(uint4 u, bool valid, float slope) {
+  if (!valid) return uint4{0u, 0u, 0u, 0u};
   if (slope != 1.0f) {
     constexpr int N = 16 / sizeof(T);
     T* e = reinterpret_cast<T*>(&u);
@@ -44,31 +50,33 @@ template <typename T>
 __device__ inline typename Mfma<T>::frag load_afrag(const T* ptr, bool valid) {
   typedef typename Mfma<T>::frag F;
   if constexpr (sizeof(T) == 4) {
-    return valid ? *ptr : 0.0f;
+    const float v = *ptr;
+    return valid ? v : 0.0f;
   } else {
-    if (!valid) return F{};
     uint4 u = *reinterpret_cast<const uint4*>(ptr);
+    if (!valid) u = uint4{0u, 0u, 0u, 0u};
     return *reinterpret_cast<F*>(&u);
   }
 }
 
-template <typename T, int MT, int NT, int WM, int WN>
+template <typename T, int MT, int NT, int WM, int WN, int CK>
 __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(ConvParams p) {
   using MF = Mfma<T>;
   typedef typename MF::frag Frag;
   constexpr int BM = 32 * MT * WM;
   constexpr int BN = 32 * NT * WN;
   constexpr int NTHR = 64 * WM * WN;
-  constexpr int CK = 64 / (int)sizeof(T);       // channels per LDS chunk (64 bytes)
-  constexpr int LDSR = 80 / (int)sizeof(T);     // LDS row stride in elements (64 B + 16 B pad)
   constexpr int EPV = 16 / (int)sizeof(T);      // elements per 16-byte vector
-  constexpr int VPR = CK / EPV;                 // vectors per row chunk (4)
-  constexpr int KS = CK / MF::KSTEP;            // MFMA k-steps per chunk
+  constexpr int VPR = CK / EPV;                 // vectors per row chunk
+  constexpr int LDSR = CK + EPV;                // LDS row stride (elements): +16 B pad
+  constexpr int KS = CK / MF::KSTEP;            // MFMA k-steps per chunk and tap
+  constexpr int PF = ((BN + HALO_MAX) * VPR + NTHR - 1) / NTHR;  // prefetch vectors per thread
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* xs = reinterpret_cast<T*>(smem);
 
-  const int b = blockIdx.z;
+  const int nh = p.nh;
+  const int b = blockIdx.z / nh;
+  const int hd = blockIdx.z - b * nh;
   const int n0 = blockIdx.x * BN;
   const int ylen = p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows;
   if (n0 >= ylen) return;
@@ -85,10 +93,63 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(ConvParams p) {
   const int l31 = lane & 31;
   const int hh = lane >> 5;
 
-  const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.sxb;
-  const T* W = reinterpret_cast<const T*>(p.w) + (long long)b * p.swb;
+  const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.sxb + (long long)hd * p.sxh;
+  const T* W = reinterpret_cast<const T*>(p.w) + (long long)b * p.swb + (long long)hd * p.swh;
   const int R = BN + (p.taps - 1) * p.dil;
+  const int RV = R * VPR;
   const int x_start = n0 - p.pad;
+  const int tile = R * LDSR;
+  T* xs0 = reinterpret_cast<T*>(smem);
+  T* xs1 = xs0 + tile;
+  const int nchunks = (p.Cin + CK - 1) / CK;
+  const int xlast = xlen > 0 ? xlen - 1 : 0;
+
+  // ---- X chunk staging: global -> registers (raw) -> act/mask -> LDS ----
+  uint4 pf[PF];
+  auto load_chunk = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int v = tid + i * NTHR;
+      const int r = v / VPR;
+      const int cv = v - r * VPR;
+      const int xr = min(max(x_start + r, 0), xlast);
+      const int c = min(c0 + cv * EPV, p.Cin - EPV);
+      pf[i] = *reinterpret_cast<const uint4*>(X + (long long)xr * p.sxr + c);
+    }
+  };
+  auto store_chunk = [&](T* buf, int c0) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int v = tid + i * NTHR;
+      if (v < RV) {
+        const int r = v / VPR;
+        const int cv = v - r * VPR;
+        const int xr = x_start + r;
+        const bool ok = (xr >= 0) && (xr < xlen) && (c0 + cv * EPV < p.Cin);
+        *reinterpret_cast<uint4*>(buf + r * LDSR + cv * EPV) = act16<T>(pf[i], ok, p.in_slope);
+      }
+    }
+  };
+
+  // ---- A (weight) fragments, one tap of one chunk ----
+  const T* wrow[MT];
+  bool mok[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = m_w0 + mt * 32 + l31;
+    mok[mt] = m < p.M;
+    wrow[mt] = W + (long long)(mok[mt] ? m : 0) * p.w_ld;
+  }
+  auto load_a = [&](Frag (&a)[MT][KS], int c0, int tap) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int k = c0 + ks * MF::KSTEP + hh * MF::KPL;
+        const bool ok = mok[mt] && (k < p.Cin);
+        a[mt][ks] = load_afrag<T>(wrow[mt] + tap * p.Cin + (ok ? k : 0), ok);
+      }
+  };
 
   f32x16 acc[MT][NT];
 #pragma unroll
@@ -96,33 +157,23 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(ConvParams p) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x16{};
 
-  for (int c0 = 0; c0 < p.Cin; c0 += CK) {
-    __syncthreads();
-    for (int v = tid; v < R * VPR; v += NTHR) {
-      const int r = v / VPR;
-      const int cv = v - r * VPR;
-      const int xr = x_start + r;
-      const int c = c0 + cv * EPV;
-      const bool ok = (xr >= 0) && (xr < xlen) && (c < p.Cin);
-      uint4 u = load16_act<T>(X + (long long)xr * p.sxr + c, ok, p.in_slope);
-      *reinterpret_cast<uint4*>(xs + r * LDSR + cv * EPV) = u;
-    }
-    __syncthreads();
+  Frag a_cur[MT][KS], a_nxt[MT][KS];
+  load_chunk(0);
+  load_a(a_cur, 0, 0);
+  store_chunk(xs0, 0);
+  __syncthreads();
 
+  for (int ci = 0; ci < nchunks; ++ci) {
+    const T* cur = (ci & 1) ? xs1 : xs0;
+    T* nxt = (ci & 1) ? xs0 : xs1;
+    const int c0 = ci * CK;
+    const bool has_next = ci + 1 < nchunks;
+    if (has_next) load_chunk(c0 + CK);
     for (int tap = 0; tap < p.taps; ++tap) {
-      Frag a[MT][KS];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int m = m_w0 + mt * 32 + l31;
-        const bool mok = m < p.M;
-        const T* wrow = W + (long long)(mok ? m : 0) * p.w_ld + tap * p.Cin;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const int k = c0 + ks * MF::KSTEP + hh * MF::KPL;
-          a[mt][ks] = load_afrag<T>(wrow + k, mok && (k < p.Cin));
-        }
-      }
-      const T* xrow = xs + (n_w0 + l31 + tap * p.dil) * LDSR + hh * MF::KPL;
+      int ntap = tap + 1, nc0 = c0;
+      if (ntap == p.taps) { ntap = 0; nc0 = c0 + CK; }
+      if (nc0 < p.Cin) load_a(a_nxt, nc0, ntap);
+      const T* xrow = cur + (n_w0 + l31 + tap * p.dil) * LDSR + hh * MF::KPL;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         Frag bf[NT];
@@ -132,15 +183,21 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(ConvParams p) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = MF::mma(a[mt][ks], bf[nt], acc[mt][nt]);
+          for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = MF::mma(a_cur[mt][ks], bf[nt], acc[mt][nt]);
       }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) a_cur[mt][ks] = a_nxt[mt][ks];
     }
+    if (has_next) store_chunk(nxt, c0 + CK);
+    __syncthreads();
   }
 
   // ---------------- epilogue ----------------
-  T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.syb;
-  const T* R1 = p.r1 ? reinterpret_cast<const T*>(p.r1) + (long long)b * p.srb : nullptr;
-  const T* R2 = p.r2 ? reinterpret_cast<const T*>(p.r2) + (long long)b * p.srb : nullptr;
+  T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.syb + (long long)hd * p.syh;
+  const T* R1 = p.r1 ? reinterpret_cast<const T*>(p.r1) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
+  const T* R2 = p.r2 ? reinterpret_cast<const T*>(p.r2) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const int tlen = p.up_len ? min(p.up_len[b], (p.y_rows - 1) * p.up_s) : 0;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -179,22 +236,42 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(ConvParams p) {
   }
 }
 
-template <typename T, int MT, int NT, int WM, int WN>
+template <typename T, int MT, int NT, int WM, int WN, int CK>
 static hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
   constexpr int BM = 32 * MT * WM;
   constexpr int BN = 32 * NT * WN;
+  constexpr int LDSR = CK + 16 / (int)sizeof(T);
   const int R = BN + (p.taps - 1) * p.dil;
-  const size_t lds = (size_t)R * 80;
-  dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B);
-  hipLaunchKernelGGL((conv_gemm_kernel<T, MT, NT, WM, WN>), grid, dim3(64 * WM * WN), lds, s, p);
+  const int nchunks = (p.Cin + CK - 1) / CK;
+  const size_t lds = (size_t)R * LDSR * sizeof(T) * (nchunks > 1 ? 2 : 1);
+  dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
+  hipLaunchKernelGGL((conv_gemm_kernel<T, MT, NT, WM, WN, CK>), grid, dim3(64 * WM * WN), lds, s, p);
   return hipGetLastError();
+}
+
+static int wide_mode() {
+  static int m = [] {
+    const char* e = getenv("TTS_CONV_WIDE");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
 }
 
 template <typename T>
 static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
-  if (p.M <= 32) return launch_cfg<T, 1, 2, 1, 4>(p, s);
-  if (p.M <= 64) return launch_cfg<T, 1, 2, 2, 2>(p, s);
-  return launch_cfg<T, 1, 4, 4, 1>(p, s);
+  constexpr int CKW = 64 / (int)sizeof(T);   // 32 x 16-bit / 16 x f32 (64-byte rows)
+  constexpr int CKWW = 128 / (int)sizeof(T); // 64 x 16-bit / 32 x f32 (128-byte rows)
+  const bool wide = wide_mode() && p.Cin % CKWW == 0 && p.Cin >= 2 * CKWW;
+  if (p.M <= 32) {
+    if (wide) return launch_cfg<T, 1, 2, 1, 4, CKWW>(p, s);
+    return launch_cfg<T, 1, 2, 1, 4, CKW>(p, s);
+  }
+  if (p.M <= 64) {
+    if (wide) return launch_cfg<T, 1, 2, 2, 2, CKWW>(p, s);
+    return launch_cfg<T, 1, 2, 2, 2, CKW>(p, s);
+  }
+  if (wide) return launch_cfg<T, 1, 4, 4, 1, CKWW>(p, s);
+  return launch_cfg<T, 1, 4, 4, 1, CKW>(p, s);
 }
 
 int conv_gemm_check(const ConvParams& p, int dtype, const char** why) {
@@ -202,12 +279,16 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why) {
   if (p.M <= 0 || p.Cin <= 0 || p.taps <= 0 || p.dil <= 0 || p.B <= 0) { *why = "bad dims"; return -1; }
   if (p.M % 4) { *why = "M must be a multiple of 4"; return -1; }
   if (p.Cin % epv) { *why = "Cin must be a multiple of 16 bytes"; return -1; }
-  if (p.sxr % epv || p.w_ld % epv || p.sxb % epv) { *why = "X/W strides must be 16-byte multiples"; return -1; }
+  if (p.sxr % epv || p.w_ld % epv || p.sxb % epv || p.swb % epv) {
+    *why = "X/W strides must be 16-byte multiples"; return -1;
+  }
   if (p.syr % 4 || p.syb % 4 || ((p.r1 || p.r2) && (p.srr % 4 || p.srb % 4))) {
     *why = "Y/R strides must be multiples of 4 elements"; return -1;
   }
-  if ((p.taps - 1) * p.dil > 512) { *why = "receptive field too large for LDS"; return -1; }
+  if ((p.taps - 1) * p.dil > HALO_MAX) { *why = "receptive field (taps-1)*dil > 64"; return -1; }
   if (p.up_s && (p.up_cout % 4 || !p.up_len)) { *why = "bad transposed mapping"; return -1; }
+  if (p.x_rows <= 0 || p.y_rows <= 0) { *why = "empty rows"; return -1; }
+  if (p.nh < 1 || p.sxh % epv || p.swh % epv || p.syh % 4 || p.srh % 4) { *why = "bad head batching"; return -1; }
   return 0;
 }
 

@@ -58,48 +58,56 @@ hipError_t launch_lens(const int* in, int* out, int B, const int* mult, const in
 }
 
 // conv_post: wav[b][t] = tanh(bias + sum_{j,c} w[j][c] * lrelu(x[b][t+j-pad][c], slope)),
-// zero for t >= x_len[b].  HF:1464-1466.  One thread per output sample; the
-// (256 + k - 1) x C input tile is staged through LDS in fp32.
+// zero for t >= x_len[b].  HF:1464-1466.  Bandwidth-bound (reads C x 2 B per sample):
+// a block stages (512 + k - 1) rows x C channels of lrelu(x) channel-major in LDS
+// (fp32) and each thread produces samples t and t+256 (consecutive lanes read
+// consecutive rows: conflict-free); the k x C weights are wave-uniform (scalar loads).
 template <typename T, int C>
 __global__ __launch_bounds__(256) void conv_post_kernel(const T* __restrict__ x, const int* __restrict__ x_len,
                                                        int T_, const float* __restrict__ w, float bias, int k,
                                                        float slope, float* __restrict__ wav, long long swb) {
+  constexpr int TB = 512;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* ws = reinterpret_cast<float*>(smem);            // [k][C]
-  float* xs = ws + k * C;                                 // [(256+k-1)][C+1]
+  float* xs = reinterpret_cast<float*>(smem);  // [C][rows]
   const int b = blockIdx.y;
-  const int t0 = blockIdx.x * 256;
+  const int t0 = blockIdx.x * TB;
   const int len = x_len ? min(x_len[b], T_) : T_;
   const int pad = (k - 1) / 2;
-  const int rows = 256 + k - 1;
-  for (int i = threadIdx.x; i < k * C; i += 256) ws[i] = w[i];
+  const int rows = TB + k - 1;
+  constexpr int EPV = 16 / (int)sizeof(T);
+  constexpr int VPR = C / EPV;
   const T* xb = x + (long long)b * T_ * C;
-  for (int i = threadIdx.x; i < rows * C; i += 256) {
-    const int r = i / C, c = i - r * C;
+  for (int i = threadIdx.x; i < rows * VPR; i += 256) {
+    const int r = i / VPR, cv = i - r * VPR;
     const int t = t0 - pad + r;
-    float v = 0.f;
-    if (t >= 0 && t < len) v = leaky(to_f32(xb[(long long)t * C + c]), slope);
-    xs[r * (C + 1) + c] = v;
+    const bool ok = t >= 0 && t < len;
+    uint4 u = *reinterpret_cast<const uint4*>(xb + (long long)min(max(t, 0), T_ - 1) * C + cv * EPV);
+    const T* e = reinterpret_cast<const T*>(&u);
+#pragma unroll
+    for (int q = 0; q < EPV; ++q) xs[(cv * EPV + q) * rows + r] = ok ? leaky(to_f32(e[q]), slope) : 0.f;
   }
   __syncthreads();
-  const int t = t0 + threadIdx.x;
-  if (t >= T_) return;
-  float acc = bias;
+  float acc0 = bias, acc1 = bias;
   for (int j = 0; j < k; ++j) {
-    const float* xr = xs + (threadIdx.x + j) * (C + 1);
-    const float* wr = ws + j * C;
 #pragma unroll
-    for (int c = 0; c < C; ++c) acc = fmaf(wr[c], xr[c], acc);
+    for (int c = 0; c < C; ++c) {
+      const float wv = w[j * C + c];
+      const float* xr = xs + c * rows + threadIdx.x + j;
+      acc0 = fmaf(wv, xr[0], acc0);
+      acc1 = fmaf(wv, xr[256], acc1);
+    }
   }
-  wav[b * swb + t] = t < len ? tanhf(acc) : 0.f;
+  const int ta = t0 + threadIdx.x, tb = ta + 256;
+  if (ta < T_) wav[b * swb + ta] = ta < len ? tanhf(acc0) : 0.f;
+  if (tb < T_) wav[b * swb + tb] = tb < len ? tanhf(acc1) : 0.f;
 }
 
 hipError_t launch_conv_post(int dtype, const void* x, const int* x_len, int B, int T_, int C,
                             const float* w, float bias, int k, float slope, float* wav, long long swb,
                             hipStream_t s) {
   if (C != 32) return hipErrorInvalidValue;
-  dim3 grid((T_ + 255) / 256, B);
-  const size_t lds = (size_t)(k * C + (256 + k - 1) * (C + 1)) * 4;
+  dim3 grid((T_ + 511) / 512, B);
+  const size_t lds = (size_t)C * (512 + k - 1) * 4;
   switch (dtype) {
     case DT_F32: hipLaunchKernelGGL((conv_post_kernel<float, 32>), grid, dim3(256), lds, s, (const float*)x, x_len, T_, w, bias, k, slope, wav, swb); break;
     case DT_F16: hipLaunchKernelGGL((conv_post_kernel<half_t, 32>), grid, dim3(256), lds, s, (const half_t*)x, x_len, T_, w, bias, k, slope, wav, swb); break;

@@ -13,7 +13,6 @@
 #include <map>
 #include <memory>
 #include <mutex>
-#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -21,55 +20,13 @@
 #include "acoustic.h"
 #include "common.h"
 #include "kernels.h"
+#include "runtime.h"
 
 using namespace tts;
 
 static thread_local std::string g_last_error;
 
 namespace {
-
-struct TtsError : std::runtime_error {
-  int code;
-  TtsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
-};
-
-#define HIP_CHECK(expr)                                                                    \
-  do {                                                                                     \
-    hipError_t _e = (expr);                                                                \
-    if (_e != hipSuccess)                                                                  \
-      throw TtsError(TTS_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));    \
-  } while (0)
-
-size_t dtype_size(int dt) { return dt == DT_F32 ? 4 : 2; }
-
-uint16_t f32_to_bf16_bits(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-
-// host fp32 -> device buffer in dtype
-void* upload(const std::vector<float>& h, int dt) {
-  void* d = nullptr;
-  const size_t n = h.size();
-  HIP_CHECK(hipMalloc(&d, std::max<size_t>(n, 1) * dtype_size(dt)));
-  if (dt == DT_F32) {
-    HIP_CHECK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
-  } else if (dt == DT_F16) {
-    std::vector<_Float16> t(n);
-    for (size_t i = 0; i < n; ++i) t[i] = (_Float16)h[i];
-    HIP_CHECK(hipMemcpy(d, t.data(), n * 2, hipMemcpyHostToDevice));
-  } else {
-    std::vector<uint16_t> t(n);
-    for (size_t i = 0; i < n; ++i) t[i] = f32_to_bf16_bits(h[i]);
-    HIP_CHECK(hipMemcpy(d, t.data(), n * 2, hipMemcpyHostToDevice));
-  }
-  return d;
-}
-
-float* upload_f32(const std::vector<float>& h) { return (float*)upload(h, DT_F32); }
 
 struct HostTensor {
   std::vector<int64_t> shape;
@@ -78,22 +35,13 @@ struct HostTensor {
 
 }  // namespace
 
-// A packed implicit-GEMM conv layer: W[M][taps][Cin] in the compute dtype, bias fp32 [M].
-struct ConvLayer {
-  void* w = nullptr;
-  float* bias = nullptr;
-  int M = 0, Cin = 0, taps = 1, dil = 1, pad = 0;
-  // transposed-conv output mapping
-  int up_s = 0, up_cout = 0, up_p = 0;
-};
-
 struct VocoderWeights {
   bool loaded = false;
   float* mean = nullptr;
   float* scale = nullptr;
   bool normalize = false;
   ConvLayer conv_pre;
-  std::vector<ConvLayer> ups;                    // per stage
+  std::vector<ConvLayer> ups;  // per stage
   std::vector<int> up_rate;
   std::vector<int> stage_ch;
   // mrf[stage][block][pair][0=conv1,1=conv2]
@@ -114,6 +62,7 @@ struct tts_engine {
 
   VocoderWeights voc;
   AcousticModel ac;
+  Profiler prof;
 
   // vocoder workspace
   void* vbuf[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -125,18 +74,6 @@ struct tts_engine {
   float* vchunk_wav = nullptr;
   size_t vchunk_elems = 0;
 
-  // live kernel profiling: hipEvents around every implicit-GEMM launch, on the launch stream
-  bool profiling = false;
-  struct ProfRec { hipEvent_t a, b; double flops; };
-  std::vector<ProfRec> prof;
-  std::vector<hipEvent_t> ev_pool;
-  hipEvent_t get_event() {
-    if (!ev_pool.empty()) { hipEvent_t e = ev_pool.back(); ev_pool.pop_back(); return e; }
-    hipEvent_t e;
-    HIP_CHECK(hipEventCreate(&e));
-    return e;
-  }
-
   ~tts_engine() {
     hipSetDevice(device);
     for (void* p : allocs) hipFree(p);
@@ -144,8 +81,6 @@ struct tts_engine {
     if (vmel) hipFree(vmel);
     if (vlens) hipFree(vlens);
     if (vchunk_wav) hipFree(vchunk_wav);
-    for (auto& r : prof) { hipEventDestroy(r.a); hipEventDestroy(r.b); }
-    for (auto e : ev_pool) hipEventDestroy(e);
     ac.free_all();
   }
 
@@ -162,18 +97,9 @@ struct tts_engine {
   ConvLayer pack_conv(const std::string& wname, const std::string& bname, int dil, int pad, int dt) {
     const HostTensor& w = get(wname);
     if (w.shape.size() != 3) throw TtsError(TTS_ERR_INVALID, wname + ": expected 3-D conv weight");
-    const int co = (int)w.shape[0], ci = (int)w.shape[1], k = (int)w.shape[2];
-    std::vector<float> p((size_t)co * k * ci);
-    for (int o = 0; o < co; ++o)
-      for (int c = 0; c < ci; ++c)
-        for (int j = 0; j < k; ++j) p[((size_t)o * k + j) * ci + c] = w.data[((size_t)o * ci + c) * k + j];
-    ConvLayer L;
-    L.w = track(upload(p, dt));
-    std::vector<float> b(co, 0.f);
+    std::vector<float> b;
     if (!bname.empty() && has(bname)) b = get(bname).data;
-    L.bias = (float*)track(upload_f32(b));
-    L.M = co; L.Cin = ci; L.taps = k; L.dil = dil; L.pad = pad;
-    return L;
+    return make_conv(w.data, (int)w.shape[0], (int)w.shape[1], (int)w.shape[2], b, dil, pad, dt, allocs);
   }
 
   // nn.ConvTranspose1d weight [Cin][Cout][k], stride s, padding p as a polyphase conv:
@@ -217,7 +143,6 @@ struct tts_engine {
     }
     int nst = 0;
     while (has("upsampler." + std::to_string(nst) + ".weight")) ++nst;
-    // count resblocks -> blocks per stage
     int nres = 0;
     while (has("resblocks." + std::to_string(nres) + ".convs1.0.weight")) ++nres;
     if (nst == 0 || nres % nst) throw TtsError(TTS_ERR_INVALID, "inconsistent vocoder weights");
@@ -226,11 +151,10 @@ struct tts_engine {
     v.ups.clear(); v.up_rate.clear(); v.stage_ch.clear(); v.mrf.assign(nst, {});
     for (int i = 0; i < nst; ++i) {
       const HostTensor& w = get("upsampler." + std::to_string(i) + ".weight");
-      const int cin = (int)w.shape[0], k = (int)w.shape[2];
+      const int k = (int)w.shape[2];
       // stride from "__cfg__.upsample_rates" if given, else HiFi-GAN V1's k = 2*stride
       int s = k / 2;
       if (has("__cfg__.upsample_rates")) s = (int)std::lround(get("__cfg__.upsample_rates").data.at(i));
-      (void)cin;
       v.ups.push_back(pack_transposed("upsampler." + std::to_string(i) + ".weight",
                                       "upsampler." + std::to_string(i) + ".bias", s, dt));
       v.up_rate.push_back(s);
@@ -302,31 +226,21 @@ struct tts_engine {
   void run_conv(const ConvLayer& L, const void* x, long long sxb, int sxr, const int* x_len, int x_rows,
                 void* y, long long syb, int syr, const int* y_len, int y_rows, float in_slope,
                 const void* r1, const void* r2, long long srb, int srr, float out_scale, int B,
-                const int* up_len, int dt, hipStream_t s, int act_out = ACT_NONE, float alpha = 1.f) {
+                const int* up_len, int dt, hipStream_t s) {
     ConvParams p = conv_params_default();
     p.x = x; p.sxb = sxb; p.sxr = sxr; p.x_len = x_len; p.x_rows = x_rows;
-    p.w = L.w; p.swb = 0; p.w_ld = L.taps * L.Cin;
+    p.w = L.w; p.w_ld = L.taps * L.Cin;
     p.bias = L.bias;
     p.y = y; p.syb = syb; p.syr = syr;
     p.r1 = r1; p.r2 = r2; p.srb = srb; p.srr = srr;
     p.y_len = y_len; p.y_rows = y_rows;
     p.M = L.M; p.Cin = L.Cin; p.taps = L.taps; p.dil = L.dil; p.pad = L.pad;
-    p.in_slope = in_slope; p.act_out = act_out; p.alpha = alpha; p.out_scale = out_scale;
+    p.in_slope = in_slope; p.out_scale = out_scale;
     p.up_s = L.up_s; p.up_cout = L.up_cout; p.up_p = L.up_p; p.up_len = up_len;
     p.B = B;
-    const char* why = nullptr;
-    if (conv_gemm_check(p, dt, &why)) throw TtsError(TTS_ERR_INVALID, std::string("conv: ") + why);
-    if (profiling) {
-      ProfRec r{get_event(), get_event(), 0.0};
-      // algorithmic FLOPs: 2 * Cout * Cin * k per produced row (transposed: per input row, all phases)
-      r.flops = 2.0 * L.M * (double)L.Cin * L.taps * (double)B * (L.up_s ? (y_rows - 1) : y_rows);
-      HIP_CHECK(hipEventRecord(r.a, s));
-      HIP_CHECK(conv_gemm_launch(dt, p, s));
-      HIP_CHECK(hipEventRecord(r.b, s));
-      prof.push_back(r);
-    } else {
-      HIP_CHECK(conv_gemm_launch(dt, p, s));
-    }
+    // algorithmic FLOPs: 2 * Cout * Cin * k per produced row (transposed: per input row, all phases)
+    const double fl = 2.0 * L.M * (double)L.Cin * L.taps * (double)B * (L.up_s ? (y_rows - 1) : y_rows);
+    launch_conv_checked(p, dt, s, &prof, fl);
   }
 
   // HiFi-GAN V1 forward (oracle/vocoder.py vocoder_forward; HF:1435-1475).
@@ -486,12 +400,12 @@ int tts_engine_finalize(tts_engine* eng) {
           auto it = eng->host.find(n);
           return it == eng->host.end() ? std::vector<int64_t>{} : it->second.shape;
         },
-        eng->cfg.acoustic_dtype);
+        eng->cfg.acoustic_dtype, &eng->prof);
     if (!eng->voc.loaded && !eng->ac.loaded) throw TtsError(TTS_ERR_STATE, "no known weights were set");
     eng->host.clear();
     eng->finalized = true;
     if (eng->cfg.max_batch > 0 && eng->cfg.max_frames > 0) eng->reserve_vocoder(eng->cfg.max_batch, eng->cfg.max_frames);
-    if (eng->cfg.max_batch > 0 && eng->cfg.max_tokens > 0 && eng->cfg.max_frames > 0)
+    if (eng->ac.loaded && eng->cfg.max_batch > 0 && eng->cfg.max_tokens > 0 && eng->cfg.max_frames > 0)
       eng->ac.reserve(eng->cfg.max_batch, eng->cfg.max_tokens, eng->cfg.max_frames);
   });
 }
@@ -552,28 +466,11 @@ int tts_acoustic_forward(tts_engine* eng, const int32_t* d_tokens, const int32_t
 }
 
 int tts_engine_profile(tts_engine* eng, int enable) {
-  return guarded(eng, [&] { eng->profiling = enable != 0; });
+  return guarded(eng, [&] { eng->prof.on = enable != 0; });
 }
 
 int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops, int* n_launches) {
-  return guarded(eng, [&] {
-    double ms = 0.0, fl = 0.0;
-    int n = 0;
-    for (auto& r : eng->prof) {
-      HIP_CHECK(hipEventSynchronize(r.b));
-      float e = 0.f;
-      HIP_CHECK(hipEventElapsedTime(&e, r.a, r.b));
-      ms += e;
-      fl += r.flops;
-      ++n;
-      eng->ev_pool.push_back(r.a);
-      eng->ev_pool.push_back(r.b);
-    }
-    eng->prof.clear();
-    if (gemm_ms) *gemm_ms = ms;
-    if (gemm_flops) *gemm_flops = fl;
-    if (n_launches) *n_launches = n;
-  });
+  return guarded(eng, [&] { eng->prof.read(gemm_ms, gemm_flops, n_launches); });
 }
 
 int tts_op_conv1d(int dtype, const tts_conv_desc* d, void* stream) {
@@ -591,9 +488,7 @@ int tts_op_conv1d(int dtype, const tts_conv_desc* d, void* stream) {
     p.alpha = d->alpha; p.out_scale = d->out_scale;
     p.up_s = d->up_s; p.up_cout = d->up_cout; p.up_p = d->up_p; p.up_len = d->up_len;
     p.B = d->B;
-    const char* why = nullptr;
-    if (conv_gemm_check(p, dtype, &why)) throw TtsError(TTS_ERR_INVALID, std::string("conv: ") + why);
-    HIP_CHECK(conv_gemm_launch(dtype, p, (hipStream_t)stream));
+    launch_conv_checked(p, dtype, (hipStream_t)stream, nullptr, 0.0);
     return TTS_OK;
   } catch (const TtsError& e) {
     g_last_error = e.what();

@@ -19,12 +19,15 @@ struct ConvParams {
   float alpha, out_scale;  // y = ((alpha*(acc+bias)) -> act) + r1 + r2, then * out_scale
   int up_s, up_cout, up_p; const int* up_len;  // transposed-conv output mapping (up_s = 0: off)
   int B;
+  // optional head batching: grid z = B * nh, z -> (b = z / nh, h = z % nh); every pointer is
+  // offset by b * s?b + h * s?h (lengths are indexed by b)
+  int nh; long long sxh, swh, syh, srh;
 };
 
 inline ConvParams conv_params_default() {
   ConvParams p{};
   p.in_slope = 1.f; p.alpha = 1.f; p.out_scale = 1.f; p.out_slope = 0.f;
-  p.taps = 1; p.dil = 1;
+  p.taps = 1; p.dil = 1; p.nh = 1;
   return p;
 }
 

@@ -1,0 +1,161 @@
+// Host-side runtime helpers shared by the vocoder and acoustic runtimes:
+// error type, weight packing/upload, and the implicit-GEMM launch wrapper with
+// optional live hipEvent profiling.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/tts_hip.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace tts {
+
+struct TtsError : std::runtime_error {
+  int code;
+  TtsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_CHECK(expr)                                                                       \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess)                                                                     \
+      throw ::tts::TtsError(TTS_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+inline size_t dtype_size(int dt) { return dt == DT_F32 ? 4 : 2; }
+
+inline uint16_t f32_to_bf16_bits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// host fp32 -> new device buffer in dtype dt
+inline void* upload(const std::vector<float>& h, int dt) {
+  void* d = nullptr;
+  const size_t n = h.size();
+  HIP_CHECK(hipMalloc(&d, std::max<size_t>(n, 1) * dtype_size(dt)));
+  if (n == 0) return d;
+  if (dt == DT_F32) {
+    HIP_CHECK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+  } else if (dt == DT_F16) {
+    std::vector<_Float16> t(n);
+    for (size_t i = 0; i < n; ++i) t[i] = (_Float16)h[i];
+    HIP_CHECK(hipMemcpy(d, t.data(), n * 2, hipMemcpyHostToDevice));
+  } else {
+    std::vector<uint16_t> t(n);
+    for (size_t i = 0; i < n; ++i) t[i] = f32_to_bf16_bits(h[i]);
+    HIP_CHECK(hipMemcpy(d, t.data(), n * 2, hipMemcpyHostToDevice));
+  }
+  return d;
+}
+
+inline float* upload_f32(const std::vector<float>& h) { return (float*)upload(h, DT_F32); }
+
+// A packed implicit-GEMM conv layer: W[M][taps][Cin] in the compute dtype, bias fp32 [M].
+struct ConvLayer {
+  void* w = nullptr;
+  float* bias = nullptr;
+  int M = 0, Cin = 0, taps = 1, dil = 1, pad = 0;
+  int up_s = 0, up_cout = 0, up_p = 0;  // transposed-conv output mapping
+};
+
+// nn.Conv1d weight [Cout][Cin][k] (host fp32) -> ConvLayer; scale[o] (optional) folds a
+// per-output-channel factor (BatchNorm) into the weights.
+inline ConvLayer make_conv(const std::vector<float>& w, int co, int ci, int k, const std::vector<float>& bias,
+                           int dil, int pad, int dt, std::vector<void*>& allocs,
+                           const std::vector<float>* scale = nullptr) {
+  if (w.size() != (size_t)co * ci * k) throw TtsError(TTS_ERR_INVALID, "conv weight size mismatch");
+  std::vector<float> p((size_t)co * k * ci);
+  for (int o = 0; o < co; ++o) {
+    const float s = scale ? (*scale)[o] : 1.f;
+    for (int c = 0; c < ci; ++c)
+      for (int j = 0; j < k; ++j) p[((size_t)o * k + j) * ci + c] = w[((size_t)o * ci + c) * k + j] * s;
+  }
+  ConvLayer L;
+  L.w = upload(p, dt);
+  allocs.push_back(L.w);
+  std::vector<float> b = bias;
+  if (b.empty()) b.assign(co, 0.f);
+  if (b.size() != (size_t)co) throw TtsError(TTS_ERR_INVALID, "conv bias size mismatch");
+  L.bias = upload_f32(b);
+  allocs.push_back(L.bias);
+  L.M = co; L.Cin = ci; L.taps = k; L.dil = dil; L.pad = pad;
+  return L;
+}
+
+// Live kernel timing (bench.py roofline): hipEvents around every implicit-GEMM launch.
+struct Profiler {
+  bool on = false;
+  struct Rec { hipEvent_t a, b; double flops; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t get() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    return e;
+  }
+  void read(double* ms, double* fl, int* n) {
+    double m = 0, f = 0;
+    int c = 0;
+    for (auto& r : recs) {
+      HIP_CHECK(hipEventSynchronize(r.b));
+      float e = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&e, r.a, r.b));
+      m += e; f += r.flops; ++c;
+      pool.push_back(r.a); pool.push_back(r.b);
+    }
+    recs.clear();
+    if (ms) *ms = m;
+    if (fl) *fl = f;
+    if (n) *n = c;
+  }
+  ~Profiler() {
+    for (auto& r : recs) { hipEventDestroy(r.a); hipEventDestroy(r.b); }
+    for (auto e : pool) hipEventDestroy(e);
+  }
+};
+
+// Launch one implicit-GEMM conv (validates, optionally profiles).
+inline void launch_conv_checked(const ConvParams& p, int dt, hipStream_t s, Profiler* prof, double flops) {
+  const char* why = nullptr;
+  if (conv_gemm_check(p, dt, &why)) throw TtsError(TTS_ERR_INVALID, std::string("conv: ") + why);
+  if (prof && prof->on) {
+    Profiler::Rec r{prof->get(), prof->get(), flops};
+    HIP_CHECK(hipEventRecord(r.a, s));
+    HIP_CHECK(conv_gemm_launch(dt, p, s));
+    HIP_CHECK(hipEventRecord(r.b, s));
+    prof->recs.push_back(r);
+  } else {
+    HIP_CHECK(conv_gemm_launch(dt, p, s));
+  }
+}
+
+// Standard conv over activations [B][rows][C]: X [B][x_rows][Cin] -> Y [B][y_rows][M] (+ residual R like Y).
+inline void run_layer(const ConvLayer& L, const void* x, int x_rows, const int* lens, void* y, int y_rows, int B,
+                      int dt, hipStream_t s, Profiler* prof, float in_slope = 1.f, int act = ACT_NONE,
+                      float alpha = 1.f, const void* r1 = nullptr, const void* r2 = nullptr, float out_scale = 1.f,
+                      int x_ld = 0, int y_ld = 0) {
+  ConvParams p = conv_params_default();
+  const int xl = x_ld ? x_ld : L.Cin, yl = y_ld ? y_ld : L.M;
+  p.x = x; p.sxb = (long long)x_rows * xl; p.sxr = xl; p.x_len = lens; p.x_rows = x_rows;
+  p.w = L.w; p.w_ld = L.taps * L.Cin; p.bias = L.bias;
+  p.y = y; p.syb = (long long)y_rows * yl; p.syr = yl;
+  p.r1 = r1; p.r2 = r2; p.srb = p.syb; p.srr = yl;
+  p.y_len = lens; p.y_rows = y_rows;
+  p.M = L.M; p.Cin = L.Cin; p.taps = L.taps; p.dil = L.dil; p.pad = L.pad;
+  p.in_slope = in_slope; p.act_out = act; p.alpha = alpha; p.out_scale = out_scale;
+  p.B = B;
+  launch_conv_checked(p, dt, s, prof, 2.0 * L.M * (double)L.Cin * L.taps * (double)B * y_rows);
+}
+
+}  // namespace tts

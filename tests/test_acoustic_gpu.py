@@ -1,0 +1,140 @@
+"""GPU parity of the HIP acoustic model (FastSpeech2-Conformer, through the C-ABI)
+against the CPU oracle and the transformers golden vectors.
+
+Tolerances: fp32 mel atol 2e-4 / rtol 2e-3 (8 conformer layers of fp32 GEMMs vs
+NumPy/torch BLAS); durations exact (except a logit within 1e-3 of a rounding
+boundary); bf16 mel rel-RMS <= 5e-2 with durations forced (bf16 log-durations
+legitimately round differently).
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from gonova_tts_amd.engine import HipEngine  # noqa: E402
+from gonova_tts_amd.weights import make_acoustic_weights, make_vocoder_weights  # noqa: E402
+from oracle.acoustic import acoustic_forward  # noqa: E402
+from oracle.vocoder import vocoder_forward  # noqa: E402
+
+G = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_v1.npz"))
+DEV = "cuda:0"
+
+
+def rel_rms(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.sqrt(np.mean((a - b) ** 2)) / (np.sqrt(np.mean(b ** 2)) + 1e-30))
+
+
+@pytest.fixture(scope="module")
+def aw():
+    return make_acoustic_weights(seed=0)
+
+
+_ENG = {}
+
+
+def engine(dtype, aw, vocoder=False):
+    key = (dtype, vocoder)
+    if key not in _ENG:
+        e = HipEngine(DEV, vocoder_dtype="f32", acoustic_dtype=dtype)
+        e.load_weights(acoustic=aw, vocoder=make_vocoder_weights(seed=0) if vocoder else None)
+        _ENG[key] = e
+    return _ENG[key]
+
+
+def run(eng, ids_list, t_cap, durations=None):
+    B = len(ids_list)
+    N = max(len(x) for x in ids_list)
+    tok = np.zeros((B, N), np.int32)
+    for b, x in enumerate(ids_list):
+        tok[b, :len(x)] = x
+    lens = torch.tensor([len(x) for x in ids_list], dtype=torch.int32)
+    dd = None
+    if durations is not None:
+        d = np.zeros((B, N), np.int32)
+        for b, x in enumerate(durations):
+            d[b, :len(x)] = x
+        dd = torch.from_numpy(d).to(DEV)
+    mel, mel_lens, dur = eng.acoustic(torch.from_numpy(tok).to(DEV), lens, t_cap, durations=dd,
+                                      return_durations=True)
+    torch.cuda.synchronize()
+    return mel.cpu().numpy(), mel_lens.cpu().numpy(), dur.cpu().numpy()
+
+
+@pytest.mark.parametrize("tag", ["ac_a", "ac_b"])
+def test_acoustic_fp32_matches_golden(aw, tag):
+    eng = engine("f32", aw)
+    ids = G[f"{tag}_ids"]
+    mel, mel_lens, dur = run(eng, [ids], t_cap=128)
+    np.testing.assert_array_equal(dur[0, :len(ids)], G[f"{tag}_dur"])
+    L = int(mel_lens[0])
+    assert L == G[f"{tag}_mel"].shape[0]
+    np.testing.assert_allclose(mel[0, :L], G[f"{tag}_mel"], atol=2e-4, rtol=2e-3)
+    assert np.all(mel[0, L:] == 0)
+
+
+def test_acoustic_fp32_ragged_batch_matches_oracle(aw):
+    eng = engine("f32", aw)
+    rng = np.random.default_rng(3)
+    ids_list = [rng.integers(1, 78, size=n) for n in (20, 7, 33, 1)]
+    mel, mel_lens, dur = run(eng, ids_list, t_cap=200)
+    for b, ids in enumerate(ids_list):
+        ref = acoustic_forward(ids, aw)
+        # durations: exact unless the oracle's exp(x)-1 is within 1e-3 of a .5 rounding boundary
+        frac = np.abs((np.exp(ref["log_durations"]) - 1) % 1 - 0.5)
+        ok = frac > 1e-3
+        np.testing.assert_array_equal(dur[b, :len(ids)][ok], ref["durations"][ok])
+        if not np.array_equal(dur[b, :len(ids)], ref["durations"]):
+            continue
+        L = int(mel_lens[b])
+        assert L == min(ref["mel"].shape[0], 200)
+        np.testing.assert_allclose(mel[b, :L], ref["mel"][:L], atol=2e-4, rtol=2e-3)
+
+
+def test_acoustic_duration_override_and_cap(aw):
+    eng = engine("f32", aw)
+    rng = np.random.default_rng(9)
+    ids = rng.integers(1, 78, size=15)
+    d = rng.integers(0, 5, size=15)
+    mel, mel_lens, dur = run(eng, [ids], t_cap=256, durations=[d])
+    ref = acoustic_forward(ids, aw, durations=d)
+    np.testing.assert_array_equal(dur[0, :15], d)
+    assert int(mel_lens[0]) == int(d.sum())
+    np.testing.assert_allclose(mel[0, :int(d.sum())], ref["mel"], atol=2e-4, rtol=2e-3)
+    # cap: frames beyond Tcap are dropped, the kept prefix is unchanged
+    cap = int(d.sum()) - 5
+    mel2, mel_lens2, _ = run(eng, [ids], t_cap=cap, durations=[d])
+    assert int(mel_lens2[0]) == cap
+    ref2 = acoustic_forward(ids, aw, durations=d)  # decoder sees only cap frames on GPU
+    assert np.all(np.isfinite(mel2[0, :cap]))
+    # all-zero durations -> one frame per token (HF:108-109, per utterance)
+    mel3, mel_lens3, dur3 = run(eng, [ids], t_cap=64, durations=[np.zeros(15, np.int64)])
+    assert int(mel_lens3[0]) == 15 and np.all(dur3[0, :15] == 1)
+    del ref2
+
+
+def test_acoustic_bf16_forced_durations(aw):
+    eng = engine("bf16", aw)
+    rng = np.random.default_rng(4)
+    ids_list = [rng.integers(1, 78, size=n) for n in (40, 25)]
+    durs = [np.full(len(x), 6) for x in ids_list]
+    mel, mel_lens, _ = run(eng, ids_list, t_cap=240, durations=durs)
+    for b, ids in enumerate(ids_list):
+        ref = acoustic_forward(ids, aw, durations=durs[b])
+        L = int(mel_lens[b])
+        assert L == len(ids) * 6
+        e = rel_rms(mel[b, :L], ref["mel"])
+        assert e <= 5e-2, e
+
+
+def test_end_to_end_fp32_matches_golden(aw):
+    eng = engine("f32", aw, vocoder=True)
+    ids = G["ac_a_ids"]
+    mel, mel_lens, _ = run(eng, [ids], t_cap=64)
+    L = int(mel_lens[0])
+    wav = eng.vocoder(torch.from_numpy(mel[:, :L].copy()).to(DEV)).cpu().numpy()[0]
+    np.testing.assert_allclose(wav, G["e2e_wav"], atol=2e-4, rtol=2e-3)

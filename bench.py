@@ -4,17 +4,21 @@ Workload (BASELINE.json configs[1], the config the metric is quoted on that fits
 GPU): HiFi-GAN V1 vocoder, batch 32 x 862 mel frames (10.008 s @ 22,050 Hz, 220,672
 samples per utterance), fp16 activations / fp32 accumulation, synthetic mel ~ N(0,1)
 already resident in HBM, deterministic seeded weights (no checkpoint offline).
-A "step" = one vocoder forward over the batch.  `--workload full` runs configs[2]
-(tokens -> acoustic -> vocoder, bf16 acoustic) instead.
+A "step" = one vocoder forward over the batch.
+
+The same line also carries `full_pipeline` (configs[2]: token ids U[1,77] [32,144],
+durations forced to 6 frames/token -> 864 frames; acoustic bf16 + vocoder bf16,
+tokens in HBM -> waveform in HBM), measured after the headline loop.
+`--workload full` makes that the headline instead.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 utterances are independent, so every rank runs its own batch-32 shard with no
-data-path collective (weak scaling); rank timing is bracketed by barriers and the
-max over ranks is reported.  value = samples of all ranks / max time.
+data-path collective (weak scaling); the timed loop is bracketed by barriers and
+the max time over ranks is used.  value = samples of all ranks / max time.
 
-Also reported: `roofline` for the dominant kernel family (the implicit-GEMM conv,
-timed live with hipEvents around each launch on its stream) and `cpu_baseline`
-(the NumPy oracle on the host cores, bounded sample, rank 0 only).
+`roofline` is for the dominant kernel family (the implicit-GEMM MFMA conv, timed
+live with hipEvents around every launch on its stream); `cpu_baseline` is the
+NumPy oracle on the host cores (bounded sample, rank 0 only).
 """
 from __future__ import annotations
 
@@ -41,8 +45,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--frames", type=int, default=862)
+    ap.add_argument("--tokens", type=int, default=144)
     ap.add_argument("--dtype", default="f16")
     ap.add_argument("--workload", default="vocoder", choices=["vocoder", "full"])
+    ap.add_argument("--no-full", action="store_true", help="skip the full-pipeline side measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=862, help="frames in the CPU-baseline sample")
     return ap.parse_args()
@@ -60,100 +66,168 @@ def cpu_baseline(frames: int):
     dt = time.perf_counter() - t
     threads = os.environ.get("OMP_NUM_THREADS") or os.environ.get("OPENBLAS_NUM_THREADS")
     cores = int(threads) if threads else (os.cpu_count() or 1)
-    return {"value": len(wav) / dt, "unit": "samples/s", "cores": cores, "kind": "port",
-            "sample": f"1 utterance x {frames} frames ({len(wav) / SR:.2f} s audio), NumPy fp32 oracle, "
-                      f"{dt:.1f} s wall"}
+    return {"value": round(len(wav) / dt, 1), "unit": "samples/s", "cores": cores, "kind": "port",
+            "sample": f"1 utterance x {frames} frames ({len(wav) / SR:.2f} s audio), NumPy fp32 oracle "
+                      f"(oracle/vocoder.py), {dt:.1f} s wall"}
+
+
+class Ctx:
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world > 1:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device("cuda", self.local)
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def max_over_ranks(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(self, step, steps, warmup, eng=None):
+        for _ in range(warmup):
+            step()
+        self.torch.cuda.synchronize()
+        if eng is not None:
+            eng.profile(True)
+        self.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        self.barrier()
+        el = time.perf_counter() - t0
+        prof = None
+        if eng is not None:
+            eng.profile(False)
+            prof = eng.profile_read()
+        return self.max_over_ranks(el), prof
+
+
+def roofline(prof, elapsed, steps, dtype, kernel):
+    gemm_ms, gemm_flops, n_launch = prof
+    per_launch_flops = gemm_flops / max(n_launch, 1)
+    avg_launch_ms = gemm_ms / max(n_launch, 1)
+    achieved = per_launch_flops / (avg_launch_ms * 1e-3) / 1e12 if n_launch else 0.0
+    peak = MFMA_PEAK_TFLOPS[dtype]
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 5), "traffic": None, "kernel": kernel,
+            "avg_launch_us": round(avg_launch_ms * 1e3, 2), "launches_per_step": n_launch // max(steps, 1),
+            "gemm_share_of_step": round(gemm_ms / (elapsed * 1e3), 4)}
+
+
+def bench_vocoder(ctx, args):
+    torch = ctx.torch
+    from gonova_tts_amd.config import vocoder_flops_per_sample
+    from gonova_tts_amd.engine import HipEngine
+    from gonova_tts_amd.weights import make_vocoder_weights
+    B, T = args.batch, args.frames
+    eng = HipEngine(ctx.local, vocoder_dtype=args.dtype, max_batch=B, max_frames=T)
+    eng.load_weights(vocoder=make_vocoder_weights(seed=0))
+    g = torch.Generator(device="cpu").manual_seed(1000 + ctx.rank)
+    mel = torch.randn((B, T, 80), generator=g).to(ctx.dev)
+    lens = torch.full((B,), T, dtype=torch.int32, device=ctx.dev)
+    wav = torch.empty((B, T * 256), dtype=torch.float32, device=ctx.dev)
+    el, prof = ctx.timed(lambda: eng.vocoder(mel, lens, out=wav), args.steps, args.warmup, eng)
+    samples = B * T * 256 * args.steps * ctx.world
+    value = samples / el
+    out = {"value": value, "ms_per_step": el * 1e3 / args.steps, "samples_per_utt": T * 256,
+           "algorithmic_tflops_per_gpu": value / ctx.world * vocoder_flops_per_sample() / 1e12,
+           "roofline": roofline(prof, el, args.steps, args.dtype,
+                                "conv_gemm_kernel (implicit-GEMM MFMA conv, all vocoder launches)")}
+    eng.close()
+    return out
+
+
+def bench_full(ctx, args, steps, warmup):
+    torch = ctx.torch
+    from gonova_tts_amd.engine import HipEngine
+    from gonova_tts_amd.weights import make_acoustic_weights, make_vocoder_weights
+    B, N, dur = args.batch, args.tokens, 6
+    T = N * dur
+    eng = HipEngine(ctx.local, vocoder_dtype="bf16", acoustic_dtype="bf16", max_batch=B, max_frames=T, max_tokens=N)
+    eng.load_weights(vocoder=make_vocoder_weights(seed=0), acoustic=make_acoustic_weights(seed=0, fixed_duration=dur))
+    g = torch.Generator(device="cpu").manual_seed(2000 + ctx.rank)
+    tok = torch.randint(1, 78, (B, N), generator=g, dtype=torch.int32).to(ctx.dev)
+    tl = torch.full((B,), N, dtype=torch.int32, device=ctx.dev)
+    wav = torch.empty((B, T * 256), dtype=torch.float32, device=ctx.dev)
+
+    def step():
+        mel, mel_lens = eng.acoustic(tok, tl, T)
+        eng.vocoder(mel, mel_lens, out=wav)
+
+    el, prof = ctx.timed(step, steps, warmup, eng)
+    mel, mel_lens = eng.acoustic(tok, tl, T)
+    torch.cuda.synchronize()
+    assert int(mel_lens.min()) == T, "forced durations must give 864 frames"
+    samples = B * T * 256 * steps * ctx.world
+    value = samples / el
+    ac_ms = None
+    # acoustic-only timing (same inputs) to split the step
+    el_ac, _ = ctx.timed(lambda: eng.acoustic(tok, tl, T), steps, 1)
+    ac_ms = el_ac * 1e3 / steps
+    eng.close()
+    return {"value": round(value, 1), "unit": "samples/s", "ms_per_step": round(el * 1e3 / steps, 3),
+            "acoustic_ms_per_step": round(ac_ms, 3), "per_gpu_samples_per_s": round(value / ctx.world, 1),
+            "x_realtime_per_gpu": round(value / ctx.world / SR, 2), "dtype": "bf16",
+            "config": {"workload": "C3 full pipeline (tokens -> FS2-Conformer -> HiFi-GAN), "
+                                   f"batch-{B} x {N} tokens x {dur} frames = {T} frames (10.03 s)"},
+            "roofline": roofline(prof, el, steps, "bf16", "conv_gemm_kernel (all acoustic + vocoder GEMM launches)")}
 
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    from gonova_tts_amd.engine import HipEngine
-    from gonova_tts_amd.weights import make_vocoder_weights
-    from gonova_tts_amd.config import vocoder_flops_per_sample
-
-    B, T = args.batch, args.frames
-    eng = HipEngine(local, vocoder_dtype=args.dtype, max_batch=B, max_frames=T)
-    eng.load_weights(vocoder=make_vocoder_weights(seed=0))
-    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
-    mel = torch.randn((B, T, 80), generator=g).to(dev)
-    lens = torch.full((B,), T, dtype=torch.int32, device=dev)
-    wav = torch.empty((B, T * 256), dtype=torch.float32, device=dev)
-
-    def step():
-        eng.vocoder(mel, lens, out=wav)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    eng.profile(True)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    eng.profile(False)
-    gemm_ms, gemm_flops, n_launch = eng.profile_read()
-
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    samples_per_rank = B * T * 256 * args.steps
-    total_samples = samples_per_rank * world
-    value = total_samples / elapsed
-    ms_per_step = elapsed * 1000.0 / args.steps
-    per_gpu = value / world
-
-    # roofline of the implicit-GEMM conv family (dominant kernel): algorithmic FLOPs per launch /
-    # average launch duration, both from the timed region.
-    per_launch_flops = gemm_flops / max(n_launch, 1)
-    avg_launch_ms = gemm_ms / max(n_launch, 1)
-    achieved = per_launch_flops / (avg_launch_ms * 1e-3) / 1e12 if n_launch else 0.0
-    peak = MFMA_PEAK_TFLOPS[args.dtype]
-    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 5), "traffic": None,
-            "kernel": "conv_gemm_kernel (implicit-GEMM conv, all vocoder launches)",
-            "avg_launch_us": round(avg_launch_ms * 1e3, 2), "launches_per_step": n_launch // args.steps,
-            "gemm_share_of_step": round(gemm_ms / (elapsed * 1e3), 4)}
-
-    out = {
-        "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-        "data": "synthetic (mel ~ N(0,1), seeded fan-in weights; no checkpoint offline)",
-        "config": {"workload": "C2 vocoder-only HiFi-GAN V1, batch-32 x 862 frames (10.0 s) per GPU",
-                   "global_batch": B * world, "frames": T, "samples_per_utt": T * 256,
-                   "parallelism": f"utterance-sharded dp{world} (no data-path collective)"},
-        "per_gpu_samples_per_s": round(per_gpu, 1),
-        "x_realtime_per_gpu": round(per_gpu / SR, 2),
-        "rtf": round(SR / per_gpu, 6),
-        "algorithmic_tflops": round(value * vocoder_flops_per_sample() / 1e12 / world, 2),
-        "roofline": roof,
-    }
-    if rank == 0 and not args.no_cpu_baseline:
+    ctx = Ctx()
+    if args.workload == "vocoder":
+        v = bench_vocoder(ctx, args)
+        per_gpu = v["value"] / ctx.world
+        out = {
+            "metric": METRIC, "value": round(v["value"], 1), "unit": "samples/s", "n_gpus": ctx.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(v["ms_per_step"], 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (mel ~ N(0,1), seeded fan-in weights; no checkpoint offline)",
+            "config": {"workload": f"C2 vocoder-only HiFi-GAN V1, batch-{args.batch} x {args.frames} frames "
+                                   f"({args.frames * 256 / SR:.2f} s) per GPU",
+                       "global_batch": args.batch * ctx.world, "frames": args.frames,
+                       "samples_per_utt": v["samples_per_utt"],
+                       "parallelism": f"utterance-sharded dp{ctx.world} (no data-path collective)"},
+            "per_gpu_samples_per_s": round(per_gpu, 1),
+            "x_realtime_per_gpu": round(per_gpu / SR, 2),
+            "rtf": round(SR / per_gpu, 7),
+            "algorithmic_tflops_per_gpu": round(v["algorithmic_tflops_per_gpu"], 2),
+            "roofline": v["roofline"],
+        }
+        if not args.no_full:
+            out["full_pipeline"] = bench_full(ctx, args, steps=max(3, args.steps // 2), warmup=1)
+    else:
+        f = bench_full(ctx, args, args.steps, args.warmup)
+        per_gpu = f["value"] / ctx.world
+        out = {"metric": METRIC, "value": f["value"], "unit": "samples/s", "n_gpus": ctx.world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": f["ms_per_step"],
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+               "data": "synthetic (token ids U[1,77], forced 6 frames/token, seeded weights)",
+               "config": dict(f["config"], global_batch=args.batch * ctx.world,
+                              parallelism=f"utterance-sharded dp{ctx.world}"),
+               "per_gpu_samples_per_s": round(per_gpu, 1), "x_realtime_per_gpu": round(per_gpu / SR, 2),
+               "rtf": round(SR / per_gpu, 7), "acoustic_ms_per_step": f["acoustic_ms_per_step"],
+               "roofline": f["roofline"]}
+    if ctx.rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_frames)
-    if rank == 0:
+    if ctx.rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if ctx.world > 1:
+        ctx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

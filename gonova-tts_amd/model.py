@@ -1,0 +1,125 @@
+"""Drop-in model for the reference's synthesis call site.
+
+The reference constructs its model with `ChatterboxTTS.from_pretrained(device=...)`
+(`services/tts/core/synthesizer.py:185`) and calls
+`model.generate(text, audio_prompt_path=..., exaggeration=..., cfg_weight=0.5,
+temperature=0.8)` (`synthesizer.py:344-350`), then `audio.squeeze().cpu().numpy()`
+and a float32 cast (`:352-357`).  `GonovaTTS` keeps exactly that duck-typed surface
+ and adds `generate_batch` for many sentences at once.
+
+Semantics of the extra arguments: the FastSpeech2 + HiFi-GAN pipeline is
+deterministic and has no voice cloning, so `audio_prompt_path`, `exaggeration`,
+`cfg_weight` and `temperature` are accepted and ignored (the reference forwards a
+possibly unsanitised path, `voice_manager.py:166-177`; it is never opened here).
+Output rate is `self.sr` = 22,050 Hz (the reference hard-codes 24 kHz,
+`synthesizer.py:119`).
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from .config import AcousticConfig, VocoderConfig, SAMPLE_RATE
+from .engine import HipEngine
+from .text import tokenize_batch
+from .weights import make_acoustic_weights, make_vocoder_weights
+
+
+def load_state_dict(path: str) -> Dict[str, np.ndarray]:
+    """Load a local checkpoint without executing code from it (safetensors / npz)."""
+    if path.endswith(".safetensors"):
+        from safetensors.numpy import load_file
+        return {k: np.asarray(v, np.float32) for k, v in load_file(path).items()}
+    if path.endswith(".npz"):
+        with np.load(path, allow_pickle=False) as z:
+            return {k: z[k].astype(np.float32) for k in z.files}
+    raise ValueError(f"unsupported checkpoint format: {path}")
+
+
+class GonovaTTS:
+    """FastSpeech2-Conformer + HiFi-GAN V1 on MI355X (HIP kernels via libtts_hip.so)."""
+
+    FRAMES_PER_TOKEN_CAP = 12  # first-pass frame budget per token; exact retry if exceeded
+
+    def __init__(self, engine: HipEngine, acoustic_cfg: AcousticConfig, vocoder_cfg: VocoderConfig):
+        self.engine = engine
+        self.acoustic_cfg = acoustic_cfg
+        self.vocoder_cfg = vocoder_cfg
+        self.sr = SAMPLE_RATE
+        self.device = f"cuda:{engine.device_index}"
+        self._lock = threading.Lock()
+
+    @classmethod
+    def from_pretrained(cls, device: str = "cuda", ckpt_dir: Optional[str] = None, seed: int = 0,
+                        vocoder_dtype: str = "f16", acoustic_dtype: str = "bf16", fixed_duration: Optional[int] = None,
+                        max_batch: int = 0, max_frames: int = 0, max_tokens: int = 0):
+        """Mirror of `ChatterboxTTS.from_pretrained(device=...)` (synthesizer.py:185).
+
+        ckpt_dir: optional directory with `acoustic.safetensors` and `vocoder.safetensors`
+        (HF state_dict names); without it the deterministic seeded weights are used
+        (no checkpoint is reachable offline)."""
+        acfg, vcfg = AcousticConfig(), VocoderConfig()
+        if ckpt_dir:
+            aw = load_state_dict(os.path.join(ckpt_dir, "acoustic.safetensors"))
+            vw = load_state_dict(os.path.join(ckpt_dir, "vocoder.safetensors"))
+        else:
+            aw = make_acoustic_weights(seed, acfg, fixed_duration=fixed_duration)
+            vw = make_vocoder_weights(seed, vcfg)
+        eng = HipEngine(device, vocoder_dtype=vocoder_dtype, acoustic_dtype=acoustic_dtype,
+                        max_batch=max_batch, max_frames=max_frames, max_tokens=max_tokens)
+        eng.load_weights(vocoder=vw, acoustic=aw, vocoder_cfg=vcfg)
+        return cls(eng, acfg, vcfg)
+
+    # -------------------------------------------------------------- synthesis
+    def synthesize_tokens(self, tokens: np.ndarray, lens: np.ndarray, durations: Optional[np.ndarray] = None,
+                          stream=None):
+        """tokens int32 [B, N], lens [B] -> (wav cuda float32 [B, T*256], wav_lens np.int64 [B])."""
+        import torch
+        dev = self.engine.torch_device
+        B, N = tokens.shape
+        tok = torch.from_numpy(np.ascontiguousarray(tokens, np.int32)).to(dev)
+        tl = torch.from_numpy(np.ascontiguousarray(lens, np.int32)).to(dev)
+        dd = None if durations is None else torch.from_numpy(np.ascontiguousarray(durations, np.int32)).to(dev)
+        t_cap = max(64, int(self.FRAMES_PER_TOKEN_CAP * N))
+        if durations is not None:
+            t_cap = max(1, int(np.asarray(durations).sum(axis=1).max()))
+        mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True)
+        if durations is None:
+            need = int(dur.sum(dim=1).max().item())
+            if need > t_cap:  # exact second pass with the predicted durations and a fitting cap
+                mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
+                                                          return_durations=True)
+        wav = self.engine.vocoder(mel, mel_lens, stream=stream)
+        wav_lens = mel_lens.to(torch.int64).cpu().numpy() * self.vocoder_cfg.hop
+        return wav, wav_lens
+
+    def generate_batch(self, texts: List[str], **_ignored) -> List[np.ndarray]:
+        """Synthesize many sentences in one batched pass -> list of float32 waveforms."""
+        if not texts:
+            return []
+        with self._lock:
+            tokens, lens = tokenize_batch(texts)
+            wav, wav_lens = self.synthesize_tokens(tokens, lens)
+            host = wav.cpu().numpy()
+        return [host[i, : int(wav_lens[i])].astype(np.float32, copy=False) for i in range(len(texts))]
+
+    def generate(self, text: str, audio_prompt_path: Optional[str] = None, exaggeration: float = 0.5,
+                 cfg_weight: float = 0.5, temperature: float = 0.8, **kwargs):
+        """Same call shape as the reference's `model.generate` (synthesizer.py:344-350).
+
+        Returns a float32 torch tensor of shape (1, N) on the engine device; the
+        reference's `audio.squeeze().cpu().numpy()` applies unchanged."""
+        import torch
+        del audio_prompt_path, exaggeration, cfg_weight, temperature, kwargs
+        with self._lock:
+            tokens, lens = tokenize_batch([text])
+            wav, wav_lens = self.synthesize_tokens(tokens, lens)
+        return wav[:, : int(wav_lens[0])].contiguous().to(torch.float32)
+
+
+# Alias with the reference's class name so `from gonova_tts_amd.model import ChatterboxTTS`
+# is a one-line swap at synthesizer.py:167.
+ChatterboxTTS = GonovaTTS

@@ -1,0 +1,76 @@
+"""GPU tests of the drop-in model surface (from_pretrained / generate / generate_batch)
+and the StreamingSynthesizer mirror, all through the HIP engine."""
+import asyncio
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from gonova_tts_amd.model import GonovaTTS  # noqa: E402
+from gonova_tts_amd.synthesizer import StreamingSynthesizer  # noqa: E402
+from gonova_tts_amd.text import tokenize  # noqa: E402
+from gonova_tts_amd.weights import make_acoustic_weights, make_vocoder_weights  # noqa: E402
+from oracle.acoustic import acoustic_forward  # noqa: E402
+from oracle.vocoder import vocoder_forward  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def model32():
+    return GonovaTTS.from_pretrained("cuda:0", vocoder_dtype="f32", acoustic_dtype="f32")
+
+
+def test_generate_contract_matches_reference_call_site(model32):
+    audio = model32.generate("Hello world.", audio_prompt_path=None, exaggeration=0.5, cfg_weight=0.5,
+                             temperature=0.8, unknown_kwarg=1)
+    assert isinstance(audio, torch.Tensor) and audio.dtype == torch.float32 and audio.dim() == 2
+    a = audio.squeeze().cpu().numpy()  # reference synthesizer.py:352-353
+    assert a.ndim == 1 and a.size % 256 == 0 and np.isfinite(a).all()
+    assert model32.sr == 22050
+
+
+def test_generate_matches_oracle_pipeline(model32):
+    text = "The quick brown fox."
+    ids = tokenize(text)
+    o = acoustic_forward(ids, make_acoustic_weights(0))
+    ref = vocoder_forward(o["mel"], make_vocoder_weights(0))
+    got = model32.generate(text).squeeze().cpu().numpy()
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, atol=5e-4, rtol=5e-3)
+
+
+def test_generate_batch_equals_single(model32):
+    texts = ["Short one.", "A somewhat longer sentence to synthesize, with a comma.", "Mid length text here."]
+    batch = model32.generate_batch(texts)
+    for t, b in zip(texts, batch):
+        single = model32.generate(t).squeeze().cpu().numpy()
+        assert b.shape == single.shape
+        np.testing.assert_allclose(b, single, atol=1e-5, rtol=1e-4)
+
+
+def test_frame_cap_retry_is_exact(model32):
+    old = model32.FRAMES_PER_TOKEN_CAP
+    try:
+        full = model32.generate("Retry path check.").squeeze().cpu().numpy()
+        model32.FRAMES_PER_TOKEN_CAP = 1  # force the first pass to truncate
+        again = model32.generate("Retry path check.").squeeze().cpu().numpy()
+    finally:
+        model32.FRAMES_PER_TOKEN_CAP = old
+    np.testing.assert_array_equal(full, again)
+
+
+def test_streaming_synthesizer_yields_one_chunk_per_sentence():
+    s = StreamingSynthesizer(device="cuda", device_index=0, vocoder_dtype="f16", acoustic_dtype="bf16")
+
+    async def go():
+        await s.load()
+        chunks = [c async for c in s.synthesize_streaming("Hello world. This is a test! Is it working? yes it is.")]
+        await s.cleanup()
+        return chunks
+
+    chunks = asyncio.run(go())
+    assert len(chunks) == 3
+    assert all(c.dtype == np.float32 and c.ndim == 1 and np.isfinite(c).all() for c in chunks)
+    st = s.get_stats()
+    assert st["syntheses"] == 1 and st["errors"] == 0 and st["avg_first_chunk"] > 0

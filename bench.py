@@ -47,7 +47,9 @@ def parse():
     ap.add_argument("--frames", type=int, default=862)
     ap.add_argument("--tokens", type=int, default=144)
     ap.add_argument("--dtype", default="f16")
-    ap.add_argument("--workload", default="vocoder", choices=["vocoder", "full"])
+    ap.add_argument("--workload", default="vocoder", choices=["vocoder", "full", "c4"])
+    ap.add_argument("--c4-batch", type=int, default=256)
+    ap.add_argument("--no-streaming", action="store_true", help="skip the C5 streaming latency side measurement")
     ap.add_argument("--no-full", action="store_true", help="skip the full-pipeline side measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=862, help="frames in the CPU-baseline sample")
@@ -186,9 +188,80 @@ def bench_full(ctx, args, steps, warmup):
             "roofline": roofline(prof, el, steps, "bf16", "conv_gemm_kernel (all acoustic + vocoder GEMM launches)")}
 
 
+def bench_c4(ctx, args):
+    """Config C4: B utterances of mixed length (N_i ~ U{29..144} tokens x 6 frames) owned by rank 0,
+    broadcast -> per-rank length-bucketed synthesis -> RCCL P2P gather to rank 0 (strong scaling)."""
+    torch = ctx.torch
+    from gonova_tts_amd.dist import ShardedSynthesis
+    from gonova_tts_amd.model import GonovaTTS
+    B = args.c4_batch
+    m = GonovaTTS.from_pretrained(ctx.dev.index, vocoder_dtype="bf16", acoustic_dtype="bf16",
+                                  max_batch=32, max_frames=864, max_tokens=144)
+    rng = np.random.default_rng(7)
+    lens = rng.integers(29, 145, size=B).astype(np.int32)
+    tok = np.zeros((B, 144), np.int32)
+    for i, L in enumerate(lens):
+        tok[i, :L] = rng.integers(1, 78, size=L)
+
+    def synth(t, l):
+        d = np.where(np.arange(t.shape[1])[None, :] < l[:, None], 6, 0).astype(np.int32)
+        return m.synthesize_tokens(t, l, durations=d)
+
+    sh = ShardedSynthesis(synth, ctx.dev, bucket=32)
+    run = lambda: sh.run(tok if ctx.rank == 0 else None, lens if ctx.rank == 0 else None)  # noqa: E731
+    el, _ = ctx.timed(run, args.steps, args.warmup)
+    samples = int(lens.sum()) * 6 * 256 * args.steps
+    value = samples / el
+    return {"value": value, "ms_per_step": el * 1e3 / args.steps, "batch": B,
+            "audio_s_per_step": int(lens.sum()) * 6 * 256 / SR}
+
+
+def bench_streaming(ctx, trials=50, B=8, N=144, chunk=32):
+    """Config C5: batch-8 streaming; latency from host tokens to the first audio chunk on host."""
+    torch = ctx.torch
+    from gonova_tts_amd.model import GonovaTTS
+    m = GonovaTTS.from_pretrained(ctx.dev.index, vocoder_dtype="bf16", acoustic_dtype="bf16")
+    rng = np.random.default_rng(5)
+    tok = rng.integers(1, 78, size=(B, N)).astype(np.int32)
+    lens = np.full(B, N, np.int32)
+    dur = np.full((B, N), 6, np.int32)
+    lat = []
+    for i in range(trials + 5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        gen = m.stream_tokens(tok, lens, chunk_frames=chunk, durations=dur)
+        _, wav, valid = next(gen)
+        _ = wav.cpu()
+        t = time.perf_counter() - t0
+        gen.close()
+        if i >= 5:
+            lat.append(t * 1e3)
+    m.engine.close()
+    return {"p50_first_audio_ms": round(float(np.percentile(lat, 50)), 3),
+            "p90_first_audio_ms": round(float(np.percentile(lat, 90)), 3), "trials": trials,
+            "config": f"C5 batch-{B} x {N} tokens x 6 frames, chunk {chunk} frames (~{chunk * 256 / SR * 1e3:.0f} ms) "
+                      f"+ 16 frames context, bf16"}
+
+
 def main():
     args = parse()
     ctx = Ctx()
+    if args.workload == "c4":
+        c = bench_c4(ctx, args)
+        out = {"metric": METRIC, "value": round(c["value"], 1), "unit": "samples/s", "n_gpus": ctx.world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(c["ms_per_step"], 3),
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+               "data": "synthetic (token ids U[1,77], N_i ~ U{29..144}, forced 6 frames/token, seeded weights)",
+               "config": {"workload": f"C4 batch-{c['batch']} mixed-length utterances, length-bucketed, "
+                                      "broadcast + RCCL P2P gather to rank 0 inside the timed region",
+                          "global_batch": c["batch"], "parallelism": f"utterance-sharded dp{ctx.world}"},
+               "per_gpu_samples_per_s": round(c["value"] / ctx.world, 1),
+               "x_realtime_per_gpu": round(c["value"] / ctx.world / SR, 2)}
+        if ctx.rank == 0:
+            print(json.dumps(out), flush=True)
+        if ctx.world > 1:
+            ctx.dist.destroy_process_group()
+        return
     if args.workload == "vocoder":
         v = bench_vocoder(ctx, args)
         per_gpu = v["value"] / ctx.world
@@ -210,6 +283,8 @@ def main():
         }
         if not args.no_full:
             out["full_pipeline"] = bench_full(ctx, args, steps=max(3, args.steps // 2), warmup=1)
+        if not args.no_streaming and ctx.rank == 0:
+            out["streaming"] = bench_streaming(ctx)
     else:
         f = bench_full(ctx, args, args.steps, args.warmup)
         per_gpu = f["value"] / ctx.world

@@ -96,6 +96,45 @@ class GonovaTTS:
         wav_lens = mel_lens.to(torch.int64).cpu().numpy() * self.vocoder_cfg.hop
         return wav, wav_lens
 
+    # -------------------------------------------------------------- streaming
+    STREAM_CONTEXT = 16  # mel frames of context per side; HiFi-GAN V1's receptive field is < 13
+
+    def stream_tokens(self, tokens: np.ndarray, lens: np.ndarray, chunk_frames: int = 32,
+                      context: Optional[int] = None, durations: Optional[np.ndarray] = None, stream=None):
+        """Sub-sentence streaming: one acoustic pass, then the vocoder
+        runs on windows [c0 - ctx, c0 + chunk + ctx) and keeps the middle `chunk` frames.
+        With ctx >= the receptive field every kept sample is computed from the same inputs
+        in the same order as the full-utterance pass, so the concatenated chunks equal it.
+
+        Yields (c0, wav_chunk cuda float32 [B, chunk*256], valid samples per utterance np [B])."""
+        import torch
+        ctx = self.STREAM_CONTEXT if context is None else context
+        dev = self.engine.torch_device
+        B, N = tokens.shape
+        tok = torch.from_numpy(np.ascontiguousarray(tokens, np.int32)).to(dev)
+        tl = torch.from_numpy(np.ascontiguousarray(lens, np.int32)).to(dev)
+        dd = None if durations is None else torch.from_numpy(np.ascontiguousarray(durations, np.int32)).to(dev)
+        t_cap = max(64, int(self.FRAMES_PER_TOKEN_CAP * N)) if durations is None else \
+            max(1, int(np.asarray(durations).sum(axis=1).max()))
+        mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True)
+        if durations is None:
+            need = int(dur.sum(dim=1).max().item())
+            if need > t_cap:
+                mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
+                                                          return_durations=True)
+        lens_h = mel_lens.cpu().numpy().astype(np.int64)
+        T = int(lens_h.max()) if B else 0
+        hop = self.vocoder_cfg.hop
+        for c0 in range(0, T, chunk_frames):
+            tc = min(chunk_frames, T - c0)
+            w0 = max(0, c0 - ctx)
+            w1 = min(T, c0 + tc + ctx)
+            win = mel[:, w0:w1].contiguous()
+            win_lens = torch.clamp(mel_lens - w0, min=0, max=w1 - w0).to(torch.int32)
+            wav = self.engine.vocoder_chunk(win, win_lens, c0 - w0, tc, stream=stream)
+            valid = np.clip(lens_h - c0, 0, tc) * hop
+            yield c0, wav, valid
+
     def generate_batch(self, texts: List[str], **_ignored) -> List[np.ndarray]:
         """Synthesize many sentences in one batched pass -> list of float32 waveforms."""
         if not texts:

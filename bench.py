@@ -117,14 +117,28 @@ class Ctx:
         return self.max_over_ranks(el), prof
 
 
-def roofline(prof, elapsed, steps, dtype, kernel):
+def pmc_traffic():
+    """HBM bytes per conv_gemm launch from the committed PMC summary (tools/pmc_traffic.py), if any."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic_c2.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    return {"bytes_per_launch": round(d["traffic_bytes_per_launch"]),
+            "algorithmic_bytes_per_launch": round(d["algorithmic_bytes_per_launch"]),
+            "ratio": round(d["ratio_traffic_over_algorithmic"], 3),
+            "source": os.path.relpath(files[-1], ROOT)}
+
+
+def roofline(prof, elapsed, steps, dtype, kernel, traffic=None):
     gemm_ms, gemm_flops, n_launch = prof
     per_launch_flops = gemm_flops / max(n_launch, 1)
     avg_launch_ms = gemm_ms / max(n_launch, 1)
     achieved = per_launch_flops / (avg_launch_ms * 1e-3) / 1e12 if n_launch else 0.0
     peak = MFMA_PEAK_TFLOPS[dtype]
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 5), "traffic": None, "kernel": kernel,
+            "frac": round(achieved / peak, 5), "traffic": traffic, "kernel": kernel,
+            "flops_per_launch": round(per_launch_flops),
             "avg_launch_us": round(avg_launch_ms * 1e3, 2), "launches_per_step": n_launch // max(steps, 1),
             "gemm_share_of_step": round(gemm_ms / (elapsed * 1e3), 4)}
 
@@ -147,7 +161,8 @@ def bench_vocoder(ctx, args):
     out = {"value": value, "ms_per_step": el * 1e3 / args.steps, "samples_per_utt": T * 256,
            "algorithmic_tflops_per_gpu": value / ctx.world * vocoder_flops_per_sample() / 1e12,
            "roofline": roofline(prof, el, args.steps, args.dtype,
-                                "conv_gemm_kernel (implicit-GEMM MFMA conv, all vocoder launches)")}
+                                "conv_gemm_kernel (implicit-GEMM MFMA conv, all vocoder launches)",
+                                pmc_traffic() if (B, T, args.dtype) == (32, 862, "f16") else None)}
     eng.close()
     return out
 

@@ -50,7 +50,17 @@ struct VocoderWeights {
   float post_b = 0.f;
   int post_k = 7, post_c = 32;
   int hop = 256;
+  // fused MRF launch templates per stage (x/s/len/T/B filled per forward); empty = unfused
+  std::vector<MrfParams> fused;
+  std::vector<MrfTable> fused_tab;  // host copy (FLOP accounting)
+  std::vector<bool> has_fused;
 };
+
+// TTS_MRF_FUSED=0 selects the unfused per-conv path (A/B and parity tests); read per forward.
+static bool mrf_fused_enabled() {
+  const char* e = getenv("TTS_MRF_FUSED");
+  return e ? atoi(e) != 0 : true;
+}
 
 struct tts_engine {
   int device = 0;
@@ -131,6 +141,69 @@ struct tts_engine {
     return L;
   }
 
+  // Fused-MRF weights: every conv of the stage as [k][Cout][Cin] slabs, and the step table
+  // (one step per tap group of each conv) consumed by mrf_fused_kernel.
+  void prepare_fused_stage(int i, int nk, int dt) {
+    VocoderWeights& v = voc;
+    v.fused.resize(i + 1);
+    v.has_fused.resize(i + 1, false);
+    const int C = v.stage_ch[i];
+    if (dt == DT_F32 || (C != 32 && C != 64) || nk > 4) return;
+    MrfTable mp{};
+    MrfParams pp{};
+    mp.nblk = nk;
+    mp.npair = (int)v.mrf[i][0].size();
+    if (mp.npair > 4) return;
+    pp.slope = 0.1f;
+    pp.out_scale = 1.0f / (float)nk;
+    const int G = mrf_fused_taps_per_group(C);
+    int hmax = 0, n = 0;
+    for (int j = 0; j < nk; ++j) {
+      if ((int)v.mrf[i][j].size() != mp.npair) return;
+      const int k = v.mrf[i][j][0][0].taps;
+      const int hk = (k - 1) / 2;
+      mp.k[j] = k;
+      int h = 0;
+      for (int q = 0; q < mp.npair; ++q) {
+        mp.dil[j][q] = v.mrf[i][j][q][0].dil;
+        h += hk * mp.dil[j][q] + hk;
+      }
+      mp.halo[j] = h;
+      hmax = std::max(hmax, h);
+      const std::string pre = "resblocks." + std::to_string(i * nk + j) + ".";
+      for (int q = 0; q < mp.npair; ++q)
+        for (int cv = 0; cv < 2; ++cv) {
+          const HostTensor& w = get(pre + (cv ? "convs2." : "convs1.") + std::to_string(q) + ".weight");
+          std::vector<float> slab((size_t)k * C * C);
+          for (int t = 0; t < k; ++t)
+            for (int m = 0; m < C; ++m)
+              for (int c = 0; c < C; ++c) slab[((size_t)t * C + m) * C + c] = w.data[((size_t)m * C + c) * k + t];
+          char* dptr = (char*)track(upload(slab, dt));
+          for (int t0 = 0; t0 < k; t0 += G) {
+            if (n >= MRF_MAX_STEPS) return;
+            const int nt = std::min(G, k - t0);
+            const int last = (t0 + nt == k) ? 1 : 0;
+            mp.step[n] = make_int4(j | (q << 4) | (cv << 8) | (last << 12), t0, nt, 0);
+            mp.step_w[n] = dptr + (size_t)t0 * C * C * dtype_size(dt);
+            mp.step_b[n] = v.mrf[i][j][q][cv].bias;
+            ++n;
+          }
+        }
+    }
+    mp.nsteps = n;
+    const int BN = mrf_fused_bn(C);
+    pp.rp = BN + 2 * hmax + 32;
+    void* dtab = nullptr;
+    HIP_CHECK(hipMalloc(&dtab, sizeof(MrfTable)));
+    HIP_CHECK(hipMemcpy(dtab, &mp, sizeof(MrfTable), hipMemcpyHostToDevice));
+    track(dtab);
+    pp.tab = (const MrfTable*)dtab;
+    v.fused[i] = pp;
+    v.fused_tab.resize(i + 1);
+    v.fused_tab[i] = mp;
+    v.has_fused[i] = true;
+  }
+
   void finalize_vocoder() {
     if (!has("conv_pre.weight")) return;
     const int dt = cfg.vocoder_dtype;
@@ -180,6 +253,7 @@ struct tts_engine {
                                         pre + "convs2." + std::to_string(q) + ".bias", 1, (ks - 1) / 2, dt);
         }
       }
+      prepare_fused_stage(i, nk, dt);
     }
     const HostTensor& pw = get("conv_post.weight");  // [1][C][k]
     v.post_c = (int)pw.shape[1];
@@ -287,6 +361,25 @@ struct tts_engine {
       run_conv(v.ups[i], S, (long long)Tin * cin, cin, Lp(i), Tin, XS, sb, ch, Up(i), Tin + 1, slope,
                nullptr, nullptr, 0, 0, 1.f, B, Lp(i + 1), dt, s);
       const int nk = (int)v.mrf[i].size();
+      if (mrf_fused_enabled() && i < (int)v.has_fused.size() && v.has_fused[i]) {
+        MrfParams mp = v.fused[i];
+        mp.x = XS; mp.s = S; mp.len = Lp(i + 1); mp.T = Tout; mp.B = B;
+        const MrfTable& tab = v.fused_tab[i];
+        const double fl = 2.0 * ch * (double)ch * (double)B * Tout * 2.0 * tab.npair *
+                          [&] { double k = 0; for (int j = 0; j < nk; ++j) k += tab.k[j]; return k; }();
+        if (prof.on) {
+          Profiler::Rec r{prof.get(), prof.get(), fl};
+          HIP_CHECK(hipEventRecord(r.a, s));
+          HIP_CHECK(mrf_fused_launch(dt, ch, mp, s));
+          HIP_CHECK(hipEventRecord(r.b, s));
+          prof.recs.push_back(r);
+        } else {
+          HIP_CHECK(mrf_fused_launch(dt, ch, mp, s));
+        }
+        Tin = Tout;
+        cin = ch;
+        continue;
+      }
       for (int j = 0; j < nk; ++j) {
         const auto& blk = v.mrf[i][j];
         const int np = (int)blk.size();

@@ -34,6 +34,31 @@ inline ConvParams conv_params_default() {
 int conv_gemm_check(const ConvParams& p, int dtype, const char** why);
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s);
 
+// Fused MRF stage (mrf_fused.hip): all resblocks of one HiFi-GAN stage in one launch.
+constexpr int MRF_MAX_STEPS = 96;
+// Device-resident schedule of one stage (uploaded once; read with uniform indices -> scalar loads).
+struct MrfTable {
+  int nblk, npair, nsteps, pad0;
+  int k[4];
+  int dil[4][4];
+  int halo[4];        // receptive-field half-width of each resblock
+  int4 step[MRF_MAX_STEPS];             // {blk | pair<<4 | conv<<8 | last<<12, tap0, ntaps, 0}
+  const void* step_w[MRF_MAX_STEPS];    // [ntaps][C][C] weight slab of the step
+  const float* step_b[MRF_MAX_STEPS];   // bias of the step's conv
+};
+struct MrfParams {
+  const void* x;      // [B][T][C] stage input (upsampler output), compute dtype
+  void* s;            // [B][T][C] output: mean over resblocks
+  const int* len;     // per-utterance valid rows
+  const MrfTable* tab;
+  int T, B;
+  float slope, out_scale;
+  int rp;             // LDS rows per activation buffer
+};
+int mrf_fused_taps_per_group(int C);
+int mrf_fused_bn(int C);
+hipError_t mrf_fused_launch(int dtype, int C, const MrfParams& p, hipStream_t s);
+
 // elementwise.hip
 hipError_t launch_mel_in(int dtype, const float* mel, long long smb, int smr, const float* mean,
                          const float* scale, void* out, int B, int T, int C, hipStream_t s);

@@ -151,3 +151,21 @@ def test_vocoder_full_size_batch_invariance(vw):
     ref = vocoder_forward(mel[0, :200].cpu().numpy(), vw)
     got = eng.vocoder(mel[0:1, :200].contiguous()).cpu().numpy()[0]
     assert rel_rms(got, ref) <= 5e-3
+
+
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_fused_mrf_matches_unfused_path(vw, dtype, monkeypatch):
+    """The fused MRF stage kernel (stages with C=64/32) against the per-conv path on ragged input."""
+    eng = engine_for(dtype, vw)
+    rng = np.random.default_rng(21)
+    lens = [70, 3, 41, 66]
+    mel = torch.from_numpy(rng.standard_normal((4, 70, 80)).astype(np.float32)).to(DEV)
+    ln = torch.tensor(lens, dtype=torch.int32)
+    monkeypatch.setenv("TTS_MRF_FUSED", "1")
+    fused = eng.vocoder(mel, ln).cpu().numpy()
+    monkeypatch.setenv("TTS_MRF_FUSED", "0")
+    unfused = eng.vocoder(mel, ln).cpu().numpy()
+    for b, L in enumerate(lens):
+        e = rel_rms(fused[b, :L * 256], unfused[b, :L * 256])
+        assert e <= (2e-3 if dtype == "f16" else 1.5e-2), (b, e)
+        assert np.all(fused[b, L * 256:] == 0)

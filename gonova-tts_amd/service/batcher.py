@@ -1,0 +1,120 @@
+"""Cross-request dynamic batcher: the replacement for the reference's serial `_tts_worker`
+(`services/tts/server.py:110-186`, strictly one request in flight, one `generate` call per
+sentence).
+
+Each round takes every queued request (up to `max_requests`, waiting at most `max_wait`
+after the first), splits them into sentences with the reference's segmentation
+(`synthesizer.py:48-99`), sorts all sentences by length and synthesizes them in engine
+batches of up to `max_sentences` (one acoustic + one vocoder pass per batch, ragged
+lengths handled on device).  Audio goes back per request in sentence order, one binary
+frame per sentence, then the final marker -- the reference's framing
+(`server.py:150-164`) -- as soon as all earlier sentences of that request are done.
+
+Failure: the reference logs and swallows synthesis errors, so the client never gets a
+final marker (`server.py:173-179`).  That stays the default; `notify_errors=True` sends
+`{"type": "synthesis_error", "message": ...}` plus the final marker instead.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+from typing import Callable, List, Optional
+
+import numpy as np
+
+from ..text import split_into_sentences
+
+logger = logging.getLogger(__name__)
+
+
+class DynamicBatcher:
+    def __init__(self, queues, synth_batch: Callable[[List[str]], List[np.ndarray]], max_sentences: int = 32,
+                 max_requests: int = 64, max_wait: float = 0.004, notify_errors: bool = False,
+                 send_error: Optional[Callable] = None):
+        self.queues = queues
+        self.synth_batch = synth_batch
+        self.max_sentences = max_sentences
+        self.max_requests = max_requests
+        self.max_wait = max_wait
+        self.notify_errors = notify_errors
+        self.send_error = send_error
+        self.running = False
+        self.stats = {"rounds": 0, "engine_batches": 0, "sentences": 0, "requests": 0, "errors": 0,
+                      "audio_seconds": 0.0, "busy_seconds": 0.0, "max_batch_seen": 0}
+
+    async def run(self):
+        self.running = True
+        loop = asyncio.get_running_loop()
+        while self.running:
+            try:
+                reqs = await self.queues.take_batch(self.max_requests, self.max_wait)
+            except asyncio.CancelledError:
+                break
+            if not reqs:
+                continue
+            t0 = time.perf_counter()
+            try:
+                await self._round(reqs, loop)
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # never let the worker die (reference server.py:184-186)
+                logger.error("batcher round failed: %s", e, exc_info=True)
+            finally:
+                self.stats["busy_seconds"] += time.perf_counter() - t0
+                await self.queues.mark_request_done(len(reqs))
+
+    async def _round(self, reqs, loop):
+        self.stats["rounds"] += 1
+        self.stats["requests"] += len(reqs)
+        sentences = [split_into_sentences(r.text) for r in reqs]
+        work = [(i, j, s) for i, ss in enumerate(sentences) for j, s in enumerate(ss)]
+        results: List[List[Optional[np.ndarray]]] = [[None] * len(ss) for ss in sentences]
+        failed = [False] * len(reqs)
+        cursor = [0] * len(reqs)
+        finished = [False] * len(reqs)
+
+        async def flush():
+            for i, r in enumerate(reqs):
+                if finished[i]:
+                    continue
+                while cursor[i] < len(results[i]) and results[i][cursor[i]] is not None:
+                    a = results[i][cursor[i]]
+                    await self.queues.enqueue_audio_chunk(r.connection_id, a.astype(np.float32).tobytes(), cursor[i])
+                    cursor[i] += 1
+                if cursor[i] == len(results[i]) or failed[i]:
+                    if failed[i] and not self.notify_errors:
+                        finished[i] = True  # reference behaviour: no marker after a failure
+                        continue
+                    await self.queues.enqueue_audio_chunk(r.connection_id, b"", cursor[i], is_final=True)
+                    finished[i] = True
+
+        order = sorted(range(len(work)), key=lambda k: len(work[k][2]))
+        for b0 in range(0, len(order), self.max_sentences):
+            chunk = order[b0:b0 + self.max_sentences]
+            texts = [work[k][2] for k in chunk]
+            try:
+                audios = await loop.run_in_executor(None, self.synth_batch, texts)
+            except Exception as e:
+                self.stats["errors"] += 1
+                logger.error("synthesis_failed: %s", e)
+                for k in chunk:
+                    i = work[k][0]
+                    if not failed[i]:
+                        failed[i] = True
+                        if self.notify_errors and self.send_error is not None:
+                            await self.send_error(reqs[i].connection_id, str(e))
+                await flush()
+                continue
+            self.stats["engine_batches"] += 1
+            self.stats["sentences"] += len(chunk)
+            self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(chunk))
+            for k, a in zip(chunk, audios):
+                i, j, _ = work[k]
+                results[i][j] = a
+                self.stats["audio_seconds"] += len(a) / 22050.0
+            await flush()
+        await flush()
+
+    def stop(self):
+        self.running = False

@@ -1,0 +1,229 @@
+"""WebSocket TTS service on the MI355X engine, protocol-compatible with the reference
+(`services/tts/server.py`):
+
+* `WS /v1/stream/tts` (`server.py:421-444`): per-IP rate limit (100 per 60 s) and a
+  connection cap, both rejecting with close code 1008; messages
+  `{"type":"synthesize","text",...,"voice_id","chunk_size","exaggeration","streaming"}`
+  (`server.py:215-224`); replies are one binary frame of raw float32 PCM per sentence and
+  `{"type":"synthesis_complete","chunk_id":N}` (`server.py:279-286`);
+  `register_voice` / `list_voices` answer in the reference's message shapes
+  (`server.py:226-256`) -- this engine has no voice cloning, so registration reports
+  an error and the list is empty;
+* `GET /health` 503 until the model is loaded (`server.py:450-454`), plus the sample rate
+  the PCM is in (the reference never tells clients its 24 kHz);
+* `GET /metrics`: the queue metrics dict (`server.py:478-481`).
+
+The serial worker is replaced by `DynamicBatcher` (cross-request batching).  The model
+comes from a factory so tests can inject a CPU fake; production uses `GonovaTTS`.
+"""
+import asyncio
+import json
+import logging
+import os
+import time
+import uuid
+from typing import Callable, Optional
+
+from .batcher import DynamicBatcher
+from .queues import TTSQueueManager
+
+logger = logging.getLogger(__name__)
+
+
+class RateLimiter:
+    """Sliding-window admission per client (reference server.py:358-382)."""
+
+    def __init__(self, max_requests: int = 100, window: float = 60.0):
+        self.max_requests = max_requests
+        self.window = window
+        self.hits = {}
+
+    def check(self, client: str) -> bool:
+        now = time.time()
+        recent = [t for t in self.hits.get(client, []) if now - t < self.window]
+        if len(recent) >= self.max_requests:
+            self.hits[client] = recent
+            return False
+        recent.append(now)
+        self.hits[client] = recent
+        return True
+
+
+class TTSService:
+    def __init__(self, model_factory: Callable, max_connections: int = 50, chunk_size: int = 50,
+                 max_sentences: int = 32, max_wait: float = 0.004, notify_errors: bool = False,
+                 device: str = "cuda", device_index: int = 0):
+        self.model_factory = model_factory
+        self.max_connections = max_connections
+        self.chunk_size = chunk_size
+        self.device = device
+        self.device_index = device_index
+        self.model = None
+        self.is_loaded = False
+        self.queues: Optional[TTSQueueManager] = None
+        self.batcher: Optional[DynamicBatcher] = None
+        self.rate_limiter = RateLimiter()
+        self.active_connections = 0
+        self.sockets = {}
+        self.max_sentences = max_sentences
+        self.max_wait = max_wait
+        self.notify_errors = notify_errors
+        self._task = None
+
+    async def start(self):
+        loop = asyncio.get_running_loop()
+        self.model = await loop.run_in_executor(None, self.model_factory)
+        for text in ("Hello.", "Hello, this is a warmup test."):  # reference warmups (synthesizer.py:199-207)
+            await loop.run_in_executor(None, self.model.generate_batch, [text])
+        self.queues = TTSQueueManager(sample_rate=getattr(self.model, "sr", 22050))
+        await self.queues.start()
+        self.batcher = DynamicBatcher(self.queues, self.model.generate_batch, max_sentences=self.max_sentences,
+                                      max_wait=self.max_wait, notify_errors=self.notify_errors,
+                                      send_error=self._send_error)
+        self._task = asyncio.create_task(self.batcher.run())
+        self.is_loaded = True
+
+    async def _send_error(self, conn_id: str, message: str):
+        ws = self.sockets.get(conn_id)
+        if ws is not None:
+            try:
+                await ws.send_json({"type": "synthesis_error", "message": message})
+            except Exception:
+                pass
+
+    async def shutdown(self):
+        if self.queues is not None:
+            await self.queues.wait_until_empty(timeout=30.0)
+        if self.batcher is not None:
+            self.batcher.stop()
+        if self._task is not None:
+            self._task.cancel()
+            await asyncio.gather(self._task, return_exceptions=True)
+        if self.queues is not None:
+            await self.queues.stop()
+        eng = getattr(self.model, "engine", None)
+        if eng is not None:
+            eng.close()
+        self.is_loaded = False
+
+    async def handle_connection(self, ws, conn_id: str):
+        from starlette.websockets import WebSocketDisconnect
+        out_q = self.queues.register_connection(conn_id)
+        self.sockets[conn_id] = ws
+        self.active_connections += 1
+
+        async def receive():
+            async for message in ws.iter_text():
+                try:
+                    data = json.loads(message)
+                except ValueError:
+                    continue
+                kind = data.get("type")
+                if kind == "synthesize":
+                    await self.queues.enqueue_request(
+                        connection_id=conn_id, text=data.get("text", ""), voice_id=data.get("voice_id", "default"),
+                        chunk_size=data.get("chunk_size", self.chunk_size),
+                        exaggeration=data.get("exaggeration", 0.5), streaming=data.get("streaming", True))
+                elif kind == "register_voice":
+                    await ws.send_json({"type": "error", "message": "Voice registration failed: "
+                                        "this engine has no voice cloning (FastSpeech2 + HiFi-GAN)"})
+                elif kind == "list_voices":
+                    await ws.send_json({"type": "voice_list", "voices": []})
+
+        async def send():
+            while True:
+                try:
+                    chunk = await asyncio.wait_for(out_q.get(), timeout=1.0)
+                except asyncio.TimeoutError:
+                    continue
+                try:
+                    if chunk.is_final:
+                        await ws.send_json({"type": "synthesis_complete", "chunk_id": chunk.chunk_id})
+                    else:
+                        await ws.send_bytes(chunk.audio_data)
+                except WebSocketDisconnect:
+                    break
+
+        tasks = [asyncio.create_task(receive()), asyncio.create_task(send())]
+        try:
+            await asyncio.wait(tasks, return_when=asyncio.FIRST_COMPLETED)
+        except WebSocketDisconnect:
+            pass
+        finally:
+            for t in tasks:
+                t.cancel()
+            await asyncio.gather(*tasks, return_exceptions=True)
+            self.queues.unregister_connection(conn_id)
+            self.sockets.pop(conn_id, None)
+            self.active_connections -= 1
+
+    def health(self):
+        info = {"status": "healthy", "device": f"{self.device}:{self.device_index}",
+                "sample_rate": getattr(self.model, "sr", 22050), "active_connections": self.active_connections,
+                "queue_metrics": self.queues.get_metrics(), "synthesizer_stats": dict(self.batcher.stats),
+                "voice_stats": {"total_voices": 0}}
+        try:
+            import torch
+            if torch.cuda.is_available():
+                i = self.device_index
+                info["gpu"] = {"gpu_id": i, "gpu_name": torch.cuda.get_device_name(i),
+                               "memory_allocated_gb": torch.cuda.memory_allocated(i) / 1e9,
+                               "memory_reserved_gb": torch.cuda.memory_reserved(i) / 1e9}
+        except Exception:
+            pass
+        return info
+
+
+def create_app(model_factory: Optional[Callable] = None, **service_kwargs):
+    from fastapi import FastAPI, WebSocket, status
+    from fastapi.responses import JSONResponse
+
+    if model_factory is None:
+        def model_factory():
+            from ..model import GonovaTTS
+            return GonovaTTS.from_pretrained(device="cuda:0", ckpt_dir=os.environ.get("TTS_CKPT_DIR"))
+
+    app = FastAPI(title="TTS Service (MI355X)", version="0.1.0")
+    svc = TTSService(model_factory, **service_kwargs)
+    app.state.service = svc
+
+    @app.on_event("startup")
+    async def _startup():
+        await svc.start()
+
+    @app.on_event("shutdown")
+    async def _shutdown():
+        await svc.shutdown()
+
+    @app.websocket("/v1/stream/tts")
+    async def ws_endpoint(websocket: WebSocket):
+        client = websocket.client.host if websocket.client else "unknown"
+        if not svc.rate_limiter.check(client):
+            await websocket.close(code=status.WS_1008_POLICY_VIOLATION, reason="Rate limit exceeded")
+            return
+        if svc.active_connections >= svc.max_connections:
+            await websocket.close(code=status.WS_1008_POLICY_VIOLATION, reason="Max connections reached")
+            return
+        await websocket.accept()
+        await svc.handle_connection(websocket, str(uuid.uuid4()))
+
+    @app.get("/health")
+    async def health():
+        if not svc.is_loaded:
+            return JSONResponse(status_code=503, content={"status": "unhealthy", "reason": "Model not loaded"})
+        return svc.health()
+
+    @app.get("/metrics")
+    async def metrics():
+        return svc.queues.get_metrics() if svc.queues else {}
+
+    return app
+
+
+def main():  # pragma: no cover - process entry
+    import uvicorn
+    uvicorn.run(create_app(), host="0.0.0.0", port=int(os.getenv("TTS_PORT", "8002")), log_level="info")
+
+
+if __name__ == "__main__":  # pragma: no cover
+    main()

@@ -1,0 +1,117 @@
+"""Service protocol tests on CPU with a fake model (no GPU): WS framing and final marker
+as in the reference (server.py:215-224, 279-286), /health 503 rule, /metrics keys,
+cross-request batching, error path."""
+import json
+import threading
+import time
+
+import numpy as np
+import pytest
+
+pytest.importorskip("fastapi")
+from fastapi.testclient import TestClient  # noqa: E402
+
+from gonova_tts_amd.service.server import create_app  # noqa: E402
+
+
+class FakeModel:
+    sr = 22050
+
+    def __init__(self, delay=0.0, fail_on=None):
+        self.batches = []
+        self.delay = delay
+        self.fail_on = fail_on
+        self.lock = threading.Lock()
+
+    def generate_batch(self, texts):
+        if self.fail_on and any(self.fail_on in t for t in texts):
+            raise RuntimeError("boom")
+        time.sleep(self.delay)
+        with self.lock:
+            self.batches.append(list(texts))
+        return [np.full(100 * len(t), len(t), np.float32) for t in texts]
+
+
+def recv_until_complete(ws):
+    frames = []
+    while True:
+        m = ws.receive()
+        if m.get("bytes") is not None:
+            frames.append(np.frombuffer(m["bytes"], np.float32))
+        elif m.get("text") is not None:
+            return frames, json.loads(m["text"])
+
+
+def test_ws_protocol_per_sentence_frames_and_final_marker():
+    model = FakeModel()
+    app = create_app(lambda: model)
+    with TestClient(app) as c:
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            ws.send_text(json.dumps({"type": "synthesize", "text": "Hello world. This is a test! Is it working? yes it is."}))
+            frames, final = recv_until_complete(ws)
+        assert final == {"type": "synthesis_complete", "chunk_id": 3}
+        assert [len(f) for f in frames] == [1200, 1500, 2500]
+        assert all(f.dtype == np.float32 for f in frames)
+        m = c.get("/metrics").json()
+        for k in ("requests_received", "requests_processed", "requests_dropped", "chunks_sent",
+                  "active_connections", "input_queue_size", "output_queues_count", "total_output_queue_items"):
+            assert k in m
+        assert m["chunks_sent"] == 4  # final marker counts (reference queue_manager.py:232)
+        h = c.get("/health").json()
+        assert h["status"] == "healthy" and h["sample_rate"] == 22050
+
+
+def test_empty_text_gets_only_the_marker_and_voice_routes():
+    app = create_app(lambda: FakeModel())
+    with TestClient(app) as c:
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            ws.send_text(json.dumps({"type": "synthesize", "text": "   "}))
+            frames, final = recv_until_complete(ws)
+            assert frames == [] and final["chunk_id"] == 0
+            ws.send_text(json.dumps({"type": "list_voices"}))
+            assert ws.receive_json() == {"type": "voice_list", "voices": []}
+            ws.send_text(json.dumps({"type": "register_voice", "voice_id": "x", "reference_audio": "AA=="}))
+            assert ws.receive_json()["type"] == "error"
+
+
+def test_health_is_503_until_loaded():
+    from gonova_tts_amd.service.server import TTSService
+    app = create_app(lambda: FakeModel())
+    svc = app.state.service
+    assert isinstance(svc, TTSService) and not svc.is_loaded
+    # without running the startup event the model is not loaded
+    from starlette.testclient import TestClient as TC
+    c = TC(app)  # no context manager -> startup not run
+    r = c.get("/health")
+    assert r.status_code == 503 and r.json()["status"] == "unhealthy"
+
+
+def test_concurrent_connections_are_batched_together():
+    model = FakeModel(delay=0.05)
+    app = create_app(lambda: model, max_wait=0.05)
+    results = {}
+    with TestClient(app) as c:
+        def client(i):
+            with c.websocket_connect("/v1/stream/tts") as ws:
+                ws.send_text(json.dumps({"type": "synthesize", "text": f"Sentence number {i} here. And one more."}))
+                results[i] = recv_until_complete(ws)
+        ts = [threading.Thread(target=client, args=(i,)) for i in range(6)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=30)
+    assert len(results) == 6
+    for i, (frames, final) in results.items():
+        assert final["chunk_id"] == 2 and len(frames) == 2
+    assert max(len(b) for b in model.batches) > 2  # sentences of different connections shared an engine pass
+
+
+def test_failure_follows_reference_by_default_and_notifies_when_asked():
+    app = create_app(lambda: FakeModel(fail_on="bad"), notify_errors=True)
+    with TestClient(app) as c:
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            ws.send_text(json.dumps({"type": "synthesize", "text": "bad input"}))
+            err = ws.receive_json()
+            assert err["type"] == "synthesis_error"
+            fin = ws.receive_json()
+            assert fin["type"] == "synthesis_complete"

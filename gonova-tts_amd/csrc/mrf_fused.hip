@@ -14,17 +14,20 @@
 // once: ~0.26 KB/row.  Every conv is an implicit GEMM on v_mfma_f32_32x32x16_{f16,bf16}:
 // M = C output channels, N = 32-row time tiles, K = taps x C.
 //
+// VALU budget (measured: the first version issued 38 VALU per MFMA and was VALU-bound):
+//  * H holds g = lrelu(h), the conv1 operand, so conv1 B fragments go LDS -> MFMA with no
+//    arithmetic; the residual h is recovered in the conv2 epilogue as g >= 0 ? g : g/slope
+//    (LeakyReLU is invertible), once per output element instead of once per tap.
+//  * H/T rows are padded by 16 bytes (80 B at C=32, 144 B at C=64: ds_read_b128 of 16
+//    consecutive rows hits 16 distinct bank slots), so a tap is one address add.
+//  * weight slabs are XOR-swizzled with a tap-invariant pattern (one add per tap as well).
+//  * tiles are dealt round robin; reads and MFMAs of a wave's absent tiles are skipped by
+//    wave-uniform branches.
+//
 // Each conv phase computes only the rows its successor needs (the halo shrinks by the
 // conv's half-width every phase), rounded up to 32-row tiles; rows outside the utterance
 // are forced to 0 after every conv, which reproduces the per-utterance zero padding of
-// the unfused convs exactly.
-//
-// LDS (one block per CU): H, T = [RP rows][C] in the compute dtype, 16-byte chunks
-// XOR-swizzled by row (chunk ^ (row / (256/rowbytes)) & (chunks-1)) so ds_read_b128 of any
-// 16 consecutive rows at one chunk hits 16 distinct 4-bank slots; weights stream per tap
-// group through a double-buffered LDS slab, prefetched through registers one group ahead.
-// 8 waves; 32-row tiles are dealt to waves round robin; the final phase's tiles are fixed
-// per wave so the S accumulators stay in registers across the three resblocks.
+// the unfused convs.
 #include "common.h"
 #include "kernels.h"
 
@@ -32,27 +35,40 @@ namespace tts {
 
 template <int C>
 struct MrfGeom {
-  static constexpr int RB = C * 2;              // LDS row bytes (16-bit dtype)
+  static constexpr int RB = C * 2;              // payload bytes per row (16-bit dtype)
+  static constexpr int RBP = RB + 16;           // padded activation row stride in LDS
   static constexpr int CPR = RB / 16;           // 16-byte chunks per row
-  static constexpr int SWZ_DIV = 256 / RB;      // rows sharing one 256-byte bank row
+  static constexpr int SWZ_DIV = 256 / RB;      // weight rows sharing one 256-byte bank row
   static constexpr int G = C == 32 ? 11 : 2;    // taps per weight group
   static constexpr int WG_BYTES = G * C * RB;   // weight slab bytes per group
 };
 
+// weight slab layout: row = tap*C + m, 16-byte chunk XOR-swizzled by (row / SWZ_DIV) & (CPR-1);
+// the swizzle term is unchanged by a +C row step (C / SWZ_DIV is a multiple of CPR).
 template <int C>
-__device__ inline int lds_off(int row, int chunk) {
+__device__ inline int w_off(int row, int chunk) {
   using Gm = MrfGeom<C>;
   return row * Gm::RB + 16 * (chunk ^ ((row / Gm::SWZ_DIV) & (Gm::CPR - 1)));
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+// 16-byte load through the global address space: a pointer read from the step table is
+// generic, and flat loads are counted on lgkmcnt too, which would make every LDS wait of
+// the MFMA loop also wait for the in-flight weight prefetch.
+__device__ inline uint4 gload16(const char* p) {
+  const u32x4 v = *(gu32x4*)(p);
+  uint4 r;
+  r.x = v[0]; r.y = v[1]; r.z = v[2]; r.w = v[3];
+  return r;
+}
+
 template <typename T>
-__device__ inline typename Mfma<T>::frag lrelu_frag(typename Mfma<T>::frag v, float slope) {
+__device__ inline uint4 lrelu16(uint4 u, float slope) {
+  T* e = reinterpret_cast<T*>(&u);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const float f = (float)v[i];
-    v[i] = (T)(f >= 0.f ? f : f * slope);
-  }
-  return v;
+  for (int i = 0; i < 8; ++i) e[i] = from_f32<T>(leaky(to_f32(e[i]), slope));
+  return u;
 }
 
 template <typename T, int C, int BN>
@@ -68,12 +84,13 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
   constexpr int SU = BN / 32 / NW;                // final-phase tiles per wave
   constexpr int WPF = (Gm::WG_BYTES + 16 * NTHR - 1) / (16 * NTHR);  // weight prefetch vectors
   static_assert(BN % (32 * NW) == 0, "BN must be a multiple of 256");
+  static_assert(WPF <= 3, "weight prefetch sized for <= 3 vectors per thread");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const MrfTable* __restrict__ tb = p.tab;
   char* Hs = smem;
-  char* Ts = smem + p.rp * Gm::RB;
-  char* Ws = smem + 2 * p.rp * Gm::RB;
+  char* Ts = smem + p.rp * Gm::RBP;
+  char* Ws = smem + 2 * p.rp * Gm::RBP;
 
   const int b = blockIdx.y;
   const int n0 = blockIdx.x * BN;
@@ -81,36 +98,37 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
   if (n0 >= len) return;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar tile branches
   const int l31 = lane & 31;
   const int hh = lane >> 5;
   const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
+  const float inv_slope = 1.0f / p.slope;
 
+  // x tile of resblock j -> H as g0 = lrelu(x); rows outside the utterance are 0
   auto load_x = [&](int halo) {
     const int rows = BN + 2 * halo;
     for (int v = tid; v < rows * Gm::CPR; v += NTHR) {
       const int r = v / Gm::CPR, c = v - r * Gm::CPR;
       const int g = n0 - halo + r;
       uint4 u = *reinterpret_cast<const uint4*>(X + (long long)min(max(g, 0), len - 1) * C + c * 8);
-      if (g < 0 || g >= len) u = uint4{0u, 0u, 0u, 0u};
-      *reinterpret_cast<uint4*>(Hs + lds_off<C>(r, c)) = u;
+      u = (g < 0 || g >= len) ? uint4{0u, 0u, 0u, 0u} : lrelu16<T>(u, p.slope);
+      *reinterpret_cast<uint4*>(Hs + r * Gm::RBP + c * 16) = u;
     }
   };
-  // weight group s: [ntaps][C][C] contiguous in HBM -> registers (WPF <= 3 named vectors)
-  static_assert(WPF <= 3, "weight prefetch sized for <= 3 vectors per thread");
+
   uint4 wp0 = {}, wp1 = {}, wp2 = {};
 #define TTS_LOAD_W(S_)                                                                    \
   do {                                                                                    \
     const char* src_ = reinterpret_cast<const char*>(tb->step_w[S_]);                     \
     const int nb_ = tb->step[S_].z * C * Gm::RB;                                          \
-    wp0 = *reinterpret_cast<const uint4*>(src_ + min(tid * 16, nb_ - 16));               \
-    if (WPF > 1) wp1 = *reinterpret_cast<const uint4*>(src_ + min((tid + NTHR) * 16, nb_ - 16));     \
-    if (WPF > 2) wp2 = *reinterpret_cast<const uint4*>(src_ + min((tid + 2 * NTHR) * 16, nb_ - 16)); \
+    wp0 = gload16(src_ + min(tid * 16, nb_ - 16));                                       \
+    if (WPF > 1) wp1 = gload16(src_ + min((tid + NTHR) * 16, nb_ - 16));                   \
+    if (WPF > 2) wp2 = gload16(src_ + min((tid + 2 * NTHR) * 16, nb_ - 16));               \
   } while (0)
 #define TTS_STORE_W1(V_, W_, NB_, BUF_)                                                  \
   if ((V_) * 16 < (NB_)) {                                                                \
     const int row_ = (V_) / Gm::CPR, c_ = (V_) - row_ * Gm::CPR;                          \
-    *reinterpret_cast<uint4*>((BUF_) + lds_off<C>(row_, c_)) = (W_);                      \
+    *reinterpret_cast<uint4*>((BUF_) + w_off<C>(row_, c_)) = (W_);                        \
   }
 #define TTS_STORE_W(S_, BUF_)                                                             \
   do {                                                                                    \
@@ -131,6 +149,13 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) sacc[u][m] = f32x16{};
 
+  // per-lane A-fragment byte offsets in a weight slab (tap 0); + tap * C * RB per tap
+  int aoff[MT][KS];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) aoff[m][ks] = w_off<C>(m * 32 + l31, 2 * ks + hh);
+
   load_x(tb->halo[0]);
   TTS_LOAD_W(0);
   TTS_STORE_W(0, Ws);
@@ -140,66 +165,56 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
     const int4 st = tb->step[s];
     const int j = st.x & 15, pr = (st.x >> 4) & 15, cv = (st.x >> 8) & 1, last = (st.x >> 12) & 1;
     const int tap0 = st.y, ntap = st.z;
-    const int k = tb->k[j];
-    const int hk = (k - 1) / 2;
+    const int hk = (tb->k[j] - 1) / 2;
     const int halo = tb->halo[j];
     const int R0 = BN + 2 * halo;
-    // input range of this pair and the conv's output range
     int lo = 0;
     for (int q = 0; q < pr; ++q) lo += hk * tb->dil[j][q] + hk;
-    const int a = cv == 0 ? hk * tb->dil[j][pr] : hk;     // this conv's half-width
-    const int d = cv == 0 ? tb->dil[j][pr] : 1;
-    const int olo = lo + (cv == 0 ? a : hk * tb->dil[j][pr] + hk);
-    const int ohi = R0 - olo;
-    const int nt = (ohi - olo + 31) / 32;
+    const int dp = tb->dil[j][pr];
+    const int a = cv == 0 ? hk * dp : hk;           // this conv's half-width
+    const int d = cv == 0 ? dp : 1;
+    const int olo = lo + (cv == 0 ? a : hk * dp + hk);
+    const int nt = (R0 - 2 * olo + 31) / 32;
+    const int nu = nt > wave ? (nt - wave + NW - 1) / NW : 0;
     const bool final_phase = cv == 1 && pr == tb->npair - 1;
     const char* in = cv == 0 ? Hs : Ts;
     const char* wbuf = Ws + (s & 1) * Gm::WG_BYTES;
     if (s + 1 < tb->nsteps) TTS_LOAD_W(s + 1);
 
     // ---- MFMA: my tiles x this tap group ----
-    // Per tap: all B fragments of this wave's tiles are read first (rows clamped in-bounds,
-    // no branch around any LDS read), the next tap's A fragments are prefetched, then the
-    // MFMA batch runs; tiles past nt are skipped with a wave-uniform branch.
-    const int nu = nt > wave ? (nt - wave + NW - 1) / NW : 0;
-    const int rbase = olo + wave * 32 + l31 - a;
+    const int bbase = (olo + wave * 32 + l31 - a + tap0 * d) * Gm::RBP + 16 * hh;
+    const int dstep = d * Gm::RBP;
     Frag af[MT][KS];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-        af[m][ks] = *reinterpret_cast<const Frag*>(wbuf + lds_off<C>(m * 32 + l31, 2 * ks + hh));
+      for (int ks = 0; ks < KS; ++ks) af[m][ks] = *reinterpret_cast<const Frag*>(wbuf + aoff[m][ks]);
     for (int tl = 0; tl < ntap; ++tl) {
-      const int tap = tap0 + tl;
+      // all LDS reads of this tap first (B of every present tile, A of the next tap) ...
+      const char* bt = in + bbase + tl * dstep;
       Frag bf[MAXU][KS];
 #pragma unroll
-      for (int u = 0; u < MAXU; ++u) {
-        const int row = min(rbase + u * NW * 32 + tap * d, p.rp - 1);
+      for (int u = 0; u < MAXU; ++u)
+        if (u < nu) {
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) bf[u][ks] = *reinterpret_cast<const Frag*>(in + lds_off<C>(row, 2 * ks + hh));
-      }
+          for (int ks = 0; ks < KS; ++ks)
+            bf[u][ks] = *reinterpret_cast<const Frag*>(bt + u * (NW * 32 * Gm::RBP) + 32 * ks);
+        }
       Frag an[MT][KS];
-      const int tn = tl + 1 < ntap ? tl + 1 : tl;
+      const char* wn = wbuf + (tl + 1 < ntap ? tl + 1 : tl) * C * Gm::RB;
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          an[m][ks] = *reinterpret_cast<const Frag*>(wbuf + lds_off<C>(tn * C + m * 32 + l31, 2 * ks + hh));
-      if (cv == 0) {
+        for (int ks = 0; ks < KS; ++ks) an[m][ks] = *reinterpret_cast<const Frag*>(wn + aoff[m][ks]);
+      // ... then the MFMA batch
 #pragma unroll
-        for (int u = 0; u < MAXU; ++u)
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) bf[u][ks] = lrelu_frag<T>(bf[u][ks], p.slope);
-      }
-#pragma unroll
-      for (int u = 0; u < MAXU; ++u) {
+      for (int u = 0; u < MAXU; ++u)
         if (u < nu) {
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
             for (int m = 0; m < MT; ++m) acc[u][m] = MF::mma(af[m][ks], bf[u][ks], acc[u][m]);
         }
-      }
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -211,9 +226,8 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
       const float* bias = tb->step_b[s];
 #pragma unroll
       for (int u = 0; u < MAXU; ++u) {
-        const int t = wave + u * NW;
-        if (t < nt) {
-          const int row = olo + t * 32 + l31;
+        if (u < nu) {
+          const int row = olo + (wave + u * NW) * 32 + l31;
           const int grow = n0 - halo + row;
           const bool valid = grow >= 0 && grow < len;
 #pragma unroll
@@ -221,8 +235,8 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
               const int ch = m * 32 + 8 * g + 4 * hh;
-              const int off = lds_off<C>(row, ch >> 3) + (ch & 7) * 2;
-              const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + ch);
+              const int off = row * Gm::RBP + ch * 2;
+              const f32x4 bb = *(__attribute__((address_space(1))) const f32x4*)(bias + ch);
               f32x4 v = {acc[u][m][4 * g + 0], acc[u][m][4 * g + 1], acc[u][m][4 * g + 2], acc[u][m][4 * g + 3]};
               v += bb;
               if (cv == 0) {
@@ -231,9 +245,10 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
                 if (!valid) v = f32x4{};
                 Vec4<T>::store(reinterpret_cast<T*>(Ts + off), v);
               } else {
-                v += Vec4<T>::load(reinterpret_cast<const T*>(Hs + off));
+                f32x4 gr = Vec4<T>::load(reinterpret_cast<const T*>(Hs + off));
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] += gr[i] >= 0.f ? gr[i] : gr[i] * inv_slope;  // + h (residual)
                 if (final_phase) {
-                  // t < BN/32 here: tile t belongs to this wave as slot u (t = wave + u*NW)
 #pragma unroll
                   for (int su = 0; su < SU; ++su)
                     if (su == u) {
@@ -241,6 +256,8 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
                       for (int i = 0; i < 4; ++i) sacc[su][m][4 * g + i] += v[i];
                     }
                 } else {
+#pragma unroll
+                  for (int i = 0; i < 4; ++i) v[i] = leaky(v[i], p.slope);  // store g = lrelu(h)
                   if (!valid) v = f32x4{};
                   Vec4<T>::store(reinterpret_cast<T*>(Hs + off), v);
                 }
@@ -258,6 +275,9 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
     }
     __syncthreads();
   }
+#undef TTS_LOAD_W
+#undef TTS_STORE_W1
+#undef TTS_STORE_W
 
   // ---- S = mean over resblocks -> HBM ----
   T* S = reinterpret_cast<T*>(p.s) + (long long)b * p.T * C;
@@ -281,7 +301,7 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
 template <typename T, int C, int BN>
 static hipError_t launch_mrf_t(const MrfParams& p, hipStream_t s) {
   using Gm = MrfGeom<C>;
-  const size_t lds = (size_t)2 * p.rp * Gm::RB + 2 * Gm::WG_BYTES;
+  const size_t lds = (size_t)2 * p.rp * Gm::RBP + 2 * Gm::WG_BYTES;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   dim3 grid((p.T + BN - 1) / BN, p.B);
   hipLaunchKernelGGL((mrf_fused_kernel<T, C, BN>), grid, dim3(512), lds, s, p);

@@ -157,7 +157,9 @@ struct tts_engine {
     pp.slope = 0.1f;
     pp.out_scale = 1.0f / (float)nk;
     const int G = mrf_fused_taps_per_group(C);
+    const int BN = mrf_fused_bn(C);
     int hmax = 0, n = 0;
+    std::vector<float> biases;
     for (int j = 0; j < nk; ++j) {
       if ((int)v.mrf[i][j].size() != mp.npair) return;
       const int k = v.mrf[i][j][0][0].taps;
@@ -171,9 +173,20 @@ struct tts_engine {
       mp.halo[j] = h;
       hmax = std::max(hmax, h);
       const std::string pre = "resblocks." + std::to_string(i * nk + j) + ".";
+      int lo = 0;  // first LDS row of the pair's input range
       for (int q = 0; q < mp.npair; ++q)
         for (int cv = 0; cv < 2; ++cv) {
-          const HostTensor& w = get(pre + (cv ? "convs2." : "convs1.") + std::to_string(q) + ".weight");
+          const std::string cname = pre + (cv ? "convs2." : "convs1.") + std::to_string(q);
+          const int conv_idx = (j * mp.npair + q) * 2 + cv;
+          const auto& bh = get(cname + ".bias").data;
+          biases.insert(biases.end(), bh.begin(), bh.end());
+          const int dq = mp.dil[j][q];
+          const int a = cv == 0 ? hk * dq : hk;
+          const int olo = lo + (cv == 0 ? a : hk * dq + hk);
+          const int nt = (BN + 2 * h - 2 * olo + 31) / 32;
+          const int fin = (cv == 1 && q == mp.npair - 1) ? 1 : 0;
+          if (cv == 1) lo += hk * dq + hk;
+          const HostTensor& w = get(cname + ".weight");
           std::vector<float> slab((size_t)k * C * C);
           for (int t = 0; t < k; ++t)
             for (int m = 0; m < C; ++m)
@@ -181,17 +194,18 @@ struct tts_engine {
           char* dptr = (char*)track(upload(slab, dt));
           for (int t0 = 0; t0 < k; t0 += G) {
             if (n >= MRF_MAX_STEPS) return;
-            const int nt = std::min(G, k - t0);
-            const int last = (t0 + nt == k) ? 1 : 0;
-            mp.step[n] = make_int4(j | (q << 4) | (cv << 8) | (last << 12), t0, nt, 0);
+            const int ntp = std::min(G, k - t0);
+            const int last = (t0 + ntp == k) ? 1 : 0;
+            mp.step[n] = make_int4(j | (q << 4) | (cv << 8) | (last << 12) | (fin << 13), t0, ntp, conv_idx);
+            mp.geo[n] = make_int4(olo, a, cv == 0 ? dq : 1, nt);
             mp.step_w[n] = dptr + (size_t)t0 * C * C * dtype_size(dt);
-            mp.step_b[n] = v.mrf[i][j][q][cv].bias;
             ++n;
           }
         }
     }
     mp.nsteps = n;
-    const int BN = mrf_fused_bn(C);
+    mp.nconv = nk * mp.npair * 2;
+    mp.bias = (const float*)track(upload_f32(biases));
     pp.rp = BN + 2 * hmax + 32;
     void* dtab = nullptr;
     HIP_CHECK(hipMalloc(&dtab, sizeof(MrfTable)));

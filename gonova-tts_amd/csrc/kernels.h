@@ -38,13 +38,14 @@ hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s);
 constexpr int MRF_MAX_STEPS = 96;
 // Device-resident schedule of one stage (uploaded once; read with uniform indices -> scalar loads).
 struct MrfTable {
-  int nblk, npair, nsteps, pad0;
+  int nblk, npair, nsteps, nconv;
   int k[4];
   int dil[4][4];
   int halo[4];        // receptive-field half-width of each resblock
-  int4 step[MRF_MAX_STEPS];             // {blk | pair<<4 | conv<<8 | last<<12, tap0, ntaps, 0}
+  int4 step[MRF_MAX_STEPS];             // {blk | pair<<4 | conv<<8 | last<<12 | final<<13, tap0, ntaps, conv index}
+  int4 geo[MRF_MAX_STEPS];              // {olo (first output row in LDS), a (half-width), d (dilation), nt (tiles)}
   const void* step_w[MRF_MAX_STEPS];    // [ntaps][C][C] weight slab of the step
-  const float* step_b[MRF_MAX_STEPS];   // bias of the step's conv
+  const float* bias;                    // [nconv][C] biases of every conv of the stage, fp32
 };
 struct MrfParams {
   const void* x;      // [B][T][C] stage input (upsampler output), compute dtype

@@ -104,17 +104,36 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
   const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
   const float inv_slope = 1.0f / p.slope;
 
-  // x tile of resblock j -> H as g0 = lrelu(x); rows outside the utterance are 0
-  auto load_x = [&](int halo) {
-    const int rows = BN + 2 * halo;
-    for (int v = tid; v < rows * Gm::CPR; v += NTHR) {
-      const int r = v / Gm::CPR, c = v - r * Gm::CPR;
-      const int g = n0 - halo + r;
-      uint4 u = *reinterpret_cast<const uint4*>(X + (long long)min(max(g, 0), len - 1) * C + c * 8);
-      u = (g < 0 || g >= len) ? uint4{0u, 0u, 0u, 0u} : lrelu16<T>(u, p.slope);
-      *reinterpret_cast<uint4*>(Hs + r * Gm::RBP + c * 16) = u;
-    }
-  };
+  // x tile of resblock j -> H as g0 = lrelu(x); rows outside the utterance are 0.
+  // Loaded into registers first (xload) so the next resblock's tile is in flight during
+  // the current resblock's last conv, then written to LDS (xstore).
+  constexpr int XPF = ((BN + 2 * 60) * Gm::CPR + NTHR - 1) / NTHR;
+  uint4 xr[XPF];
+#define TTS_XLOAD(HALO_)                                                                  \
+  do {                                                                                    \
+    _Pragma("unroll") for (int i_ = 0; i_ < XPF; ++i_) {                                  \
+      const int v_ = tid + i_ * NTHR;                                                     \
+      const int r_ = v_ / Gm::CPR, c_ = v_ - r_ * Gm::CPR;                                \
+      const int g_ = min(max(n0 - (HALO_) + r_, 0), len - 1);                             \
+      xr[i_] = *reinterpret_cast<const uint4*>(X + (long long)g_ * C + c_ * 8);          \
+    }                                                                                     \
+  } while (0)
+#define TTS_XSTORE(HALO_)                                                                 \
+  do {                                                                                    \
+    const int rows_ = BN + 2 * (HALO_);                                                   \
+    _Pragma("unroll") for (int i_ = 0; i_ < XPF; ++i_) {                                  \
+      const int v_ = tid + i_ * NTHR;                                                     \
+      if (v_ < rows_ * Gm::CPR) {                                                         \
+        const int r_ = v_ / Gm::CPR, c_ = v_ - r_ * Gm::CPR;                              \
+        const int g_ = n0 - (HALO_) + r_;                                                 \
+        const uint4 u_ = (g_ < 0 || g_ >= len) ? uint4{0u, 0u, 0u, 0u} : lrelu16<T>(xr[i_], p.slope); \
+        *reinterpret_cast<uint4*>(Hs + r_ * Gm::RBP + c_ * 16) = u_;                       \
+      }                                                                                   \
+    }                                                                                     \
+  } while (0)
+  // all biases of the stage -> LDS once per block
+  float* Bs = reinterpret_cast<float*>(smem + 2 * p.rp * Gm::RBP + 2 * Gm::WG_BYTES);
+  for (int i = tid; i < tb->nconv * C; i += NTHR) Bs[i] = tb->bias[i];
 
   uint4 wp0 = {}, wp1 = {}, wp2 = {};
 #define TTS_LOAD_W(S_)                                                                    \
@@ -156,30 +175,25 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) aoff[m][ks] = w_off<C>(m * 32 + l31, 2 * ks + hh);
 
-  load_x(tb->halo[0]);
+  TTS_XLOAD(tb->halo[0]);
+  TTS_XSTORE(tb->halo[0]);
   TTS_LOAD_W(0);
   TTS_STORE_W(0, Ws);
   __syncthreads();
 
   for (int s = 0; s < tb->nsteps; ++s) {
     const int4 st = tb->step[s];
-    const int j = st.x & 15, pr = (st.x >> 4) & 15, cv = (st.x >> 8) & 1, last = (st.x >> 12) & 1;
+    const int4 geo = tb->geo[s];
+    const int j = st.x & 15, cv = (st.x >> 8) & 1, last = (st.x >> 12) & 1;
+    const bool final_phase = (st.x >> 13) & 1;
     const int tap0 = st.y, ntap = st.z;
-    const int hk = (tb->k[j] - 1) / 2;
+    const int olo = geo.x, a = geo.y, d = geo.z, nt = geo.w;
     const int halo = tb->halo[j];
-    const int R0 = BN + 2 * halo;
-    int lo = 0;
-    for (int q = 0; q < pr; ++q) lo += hk * tb->dil[j][q] + hk;
-    const int dp = tb->dil[j][pr];
-    const int a = cv == 0 ? hk * dp : hk;           // this conv's half-width
-    const int d = cv == 0 ? dp : 1;
-    const int olo = lo + (cv == 0 ? a : hk * dp + hk);
-    const int nt = (R0 - 2 * olo + 31) / 32;
     const int nu = nt > wave ? (nt - wave + NW - 1) / NW : 0;
-    const bool final_phase = cv == 1 && pr == tb->npair - 1;
     const char* in = cv == 0 ? Hs : Ts;
     const char* wbuf = Ws + (s & 1) * Gm::WG_BYTES;
     if (s + 1 < tb->nsteps) TTS_LOAD_W(s + 1);
+    const bool next_blk = final_phase && last && j + 1 < tb->nblk;
 
     // ---- MFMA: my tiles x this tap group ----
     const int bbase = (olo + wave * 32 + l31 - a + tap0 * d) * Gm::RBP + 16 * hh;
@@ -221,9 +235,11 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
         for (int ks = 0; ks < KS; ++ks) af[m][ks] = an[m][ks];
     }
 
+    // next resblock's x tile in flight during this epilogue (fragment registers are dead here)
+
     // ---- epilogue of the conv (after its last tap group) ----
     if (last) {
-      const float* bias = tb->step_b[s];
+      const float* bias = Bs + st.w * C;
 #pragma unroll
       for (int u = 0; u < MAXU; ++u) {
         if (u < nu) {
@@ -236,7 +252,7 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
             for (int g = 0; g < 4; ++g) {
               const int ch = m * 32 + 8 * g + 4 * hh;
               const int off = row * Gm::RBP + ch * 2;
-              const f32x4 bb = *(__attribute__((address_space(1))) const f32x4*)(bias + ch);
+              const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + ch);
               f32x4 v = {acc[u][m][4 * g + 0], acc[u][m][4 * g + 1], acc[u][m][4 * g + 2], acc[u][m][4 * g + 3]};
               v += bb;
               if (cv == 0) {
@@ -269,9 +285,10 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
       }
     }
     if (s + 1 < tb->nsteps) TTS_STORE_W(s + 1, Ws + ((s + 1) & 1) * Gm::WG_BYTES);
-    if (final_phase && last && j + 1 < tb->nblk) {
+    if (next_blk) {
       __syncthreads();   // every wave is done with H / T of resblock j
-      load_x(tb->halo[j + 1]);
+      TTS_XLOAD(tb->halo[j + 1]);
+      TTS_XSTORE(tb->halo[j + 1]);
     }
     __syncthreads();
   }
@@ -301,7 +318,7 @@ __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {
 template <typename T, int C, int BN>
 static hipError_t launch_mrf_t(const MrfParams& p, hipStream_t s) {
   using Gm = MrfGeom<C>;
-  const size_t lds = (size_t)2 * p.rp * Gm::RBP + 2 * Gm::WG_BYTES;
+  const size_t lds = (size_t)2 * p.rp * Gm::RBP + 2 * Gm::WG_BYTES + (size_t)4 * 4 * 2 * 4 * C;  // + biases
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   dim3 grid((p.T + BN - 1) / BN, p.B);
   hipLaunchKernelGGL((mrf_fused_kernel<T, C, BN>), grid, dim3(512), lds, s, p);

@@ -28,6 +28,7 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace tts {
@@ -37,12 +38,7 @@ constexpr int HALO_MAX = 64;  // max (taps-1)*dil supported (HiFi-GAN V1: 50)
 template <typename T>
 __device__ inline uint4 act16(uint4 u, bool valid, float slope) {
   if (!valid) return uint4{0u, 0u, 0u, 0u};
-  if (slope != 1.0f) {
-    constexpr int N = 16 / sizeof(T);
-    T* e = reinterpret_cast<T*>(&u);
-#pragma unroll
-    for (int i = 0; i < N; ++i) e[i] = from_f32<T>(leaky(to_f32(e[i]), slope));
-  }
+  if (slope != 1.0f) u = lrelu_chunk<T>(u, slope);
   return u;
 }
 
@@ -59,8 +55,55 @@ __device__ inline typename Mfma<T>::frag load_afrag(const T* ptr, bool valid) {
   }
 }
 
+// Epilogue shared by both kernels: lane (l31, hh) of a wave holds, for each 32x32 tile
+// (mt, nt), rows n = n_base + nt*32 + l31 and channels m_base + mt*32 + 8g + 4hh + [0, 4).
+//   y = ((alpha * (acc + bias)) -> act) + r1 + r2, times out_scale; transposed-conv row map.
+template <typename T, int MT, int NT>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x16 (&acc)[MT][NT], int b, int hd,
+                                              int n_base, int m_base, int ylen, int l31, int hh) {
+  T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.syb + (long long)hd * p.syh;
+  const T* R1 = p.r1 ? reinterpret_cast<const T*>(p.r1) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
+  const T* R2 = p.r2 ? reinterpret_cast<const T*>(p.r2) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
+  const int tlen = p.up_len ? min(p.up_len[b], (p.y_rows - 1) * p.up_s) : 0;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = n_base + nt * 32 + l31;
+      if (n >= ylen) continue;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int m = m_base + mt * 32 + 8 * g + 4 * hh;
+        if (m >= p.M) continue;
+        int row = n, col = m;
+        if (p.up_s) {
+          const int q = m / p.up_cout;
+          row = n * p.up_s + q - p.up_p;
+          col = m - q * p.up_cout;
+          if (row < 0 || row >= tlen) continue;
+        }
+        f32x4 v = {acc[mt][nt][4 * g + 0], acc[mt][nt][4 * g + 1], acc[mt][nt][4 * g + 2],
+                   acc[mt][nt][4 * g + 3]};
+        if (p.bias) {
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + m);
+          v += bb;
+        }
+        if (p.alpha != 1.0f) v *= p.alpha;
+        if (p.act_out) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = apply_act(v[i], p.act_out, p.out_slope);
+        }
+        if (R1) v += Vec4<T>::load(R1 + (long long)row * p.srr + col);
+        if (R2) v += Vec4<T>::load(R2 + (long long)row * p.srr + col);
+        if (p.out_scale != 1.0f) v *= p.out_scale;
+        Vec4<T>::store(Y + (long long)row * p.syr + col, v);
+      }
+    }
+  }
+}
+
 template <typename T, int MT, int NT, int WM, int WN, int CK>
-__global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(ConvParams p) {
+__global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p) {
   using MF = Mfma<T>;
   typedef typename MF::frag Frag;
   constexpr int BM = 32 * MT * WM;
@@ -194,46 +237,251 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(ConvParams p) {
     __syncthreads();
   }
 
-  // ---------------- epilogue ----------------
+  conv_epilogue<T, MT, NT>(p, acc, b, hd, n0 + n_w0, m_w0, ylen, l31, hh);
+}
+
+// ---------------------------------------------------------------------------------------
+// X-resident variant for M >= 128, 16-bit dtypes, Cin % 64 == 0, fragment-packed weights
+// (ConvParams::wpk): HiFi-GAN stages 0-1 and upsamplers, acoustic linears/FFN.
+//
+// Why (measured on conv_gemm_kernel at C=128/256: 70-83 % of wave cycles in s_waitcnt,
+// MFMA busy 13-32 %):
+//  * its weight fragments are loaded straight from L2 in fragment shape, 32 rows x 32 B per
+//    wave instruction (32 cache lines touched per 1 KiB), which loads the address path;
+//    here weights come pre-packed in fragment order, so every weight load is one
+//    contiguous 1 KiB wave read;
+//  * the next chunk's X rows (an HBM read) were issued before the next tap's weights, and
+//    vmcnt retires loads in order; here a block stages one channel group of its X tile
+//    (every tap's rows, LeakyReLU applied) in LDS once, and the MFMA loop then has only
+//    weight loads in flight: no barriers, weights one quad (4 k-steps = 4*NT MFMAs) ahead;
+//  * the epilogue's residual reads and output writes were fragment-shaped too (32 rows x
+//    8 B); here the fp32 tile goes through LDS (two 64-row halves) and the bias / act /
+//    residual / scale pass reads and writes whole 16-byte row pieces.
+// The group's X load latency is covered by the other blocks on the CU (LDS <= 53 KB: 3).
+//
+// Block: 4 waves stacked along M (32 output channels each), BN = 32*NT rows.  X tile row
+// stride CG*2+16 bytes (an odd number of 16-byte slots: conflict-free ds_read_b128 of 32
+// consecutive rows).
+constexpr int XRES_OS = 128 * 4 + 16;  // fp32 output staging row stride (bytes)
+constexpr int XRES_HR = 64;            // output rows staged per half
+
+template <typename T>
+__device__ inline void ld8(const T* p, f32x4& a, f32x4& b) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const T* e = reinterpret_cast<const T*>(&u);
+  a = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
+  b = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
+}
+template <typename T>
+__device__ inline void st8(T* p, f32x4 a, f32x4 b) {
+  T e[8] = {(T)a[0], (T)a[1], (T)a[2], (T)a[3], (T)b[0], (T)b[1], (T)b[2], (T)b[3]};
+  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(e);
+}
+
+template <typename T, int NT>
+__global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG) {
+  using MF = Mfma<T>;
+  typedef typename MF::frag Frag;
+  static_assert(sizeof(T) == 2, "16-bit dtypes only");
+  static_assert(NT % 2 == 0, "output staged in 64-row halves");
+  constexpr int BN = 32 * NT;
+  constexpr int NTHR = 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nh = p.nh;
+  const int b = blockIdx.z / nh;
+  const int hd = blockIdx.z - b * nh;
+  const int n0 = blockIdx.x * BN;
+  const int ylen = p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows;
+  if (n0 >= ylen) return;
+  const int xlen = p.x_len ? min(p.x_len[b], p.x_rows) : p.x_rows;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l31 = lane & 31;
+  const int hh = lane >> 5;
+
+  const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.sxb + (long long)hd * p.sxh;
+  // packed weights: [MB][taps][Cin/16][64][8]; a wave past M reads the last block (its
+  // results are never stored)
+  const int KST = p.Cin / 16;
+  const int mb = min((int)blockIdx.y * 4 + wave, (p.M + 31) / 32 - 1);
+  const char* wl = reinterpret_cast<const char*>(p.wpk) + ((long long)mb * p.taps * KST) * 1024 + lane * 16;
+  const int R = BN + (p.taps - 1) * p.dil;
+  const int RS = CG * 2 + 16;
+  const int VPR = CG / 8;
+  const int NQ = CG / 64;              // weight quads (4 k-steps of 16) per tap
+  const int QT = p.taps * NQ;          // quads per channel group
+  const int x_start = n0 - p.pad;
+  const int xlast = xlen > 0 ? xlen - 1 : 0;
+  const int tot = R * VPR;
+  const int dstep = p.dil * RS;        // LDS bytes per tap
+  const char* xl = smem + l31 * RS + hh * 16;
+
+  f32x16 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x16{};
+
+  // quad (tap, kq) of channel group g0: 4 contiguous 1 KiB fragments
+#define TTS_LOADQ(A_, TAP_, KQ_)                                                          \
+  do {                                                                                    \
+    const char* q_ = wl + (long long)((TAP_) * KST + g0 / 16 + (KQ_) * 4) * 1024;          \
+    _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) A_[j_] = *reinterpret_cast<const Frag*>(q_ + j_ * 1024); \
+  } while (0)
+#define TTS_MMAQ(A_, TAP_, KQ_)                                                           \
+  do {                                                                                    \
+    const char* bq_ = xl + (TAP_) * dstep + (KQ_) * 128;                                  \
+    _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                    \
+      Frag bf_[NT];                                                                       \
+      _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_)                                \
+        bf_[nt_] = *reinterpret_cast<const Frag*>(bq_ + nt_ * 32 * RS + j_ * 32);         \
+      _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_)                                \
+        acc[nt_] = MF::mma(A_[j_], bf_[nt_], acc[nt_]);                                   \
+    }                                                                                     \
+  } while (0)
+
+  for (int g0 = 0; g0 < p.Cin; g0 += CG) {
+    Frag a0[4], a1[4];
+    // first two quads of the group in flight before the X loads (in-order vmcnt: they
+    // complete first and are ready when the MFMA loop starts)
+    int ptap = 0, pkq = 0;
+    TTS_LOADQ(a0, ptap, pkq);
+    if (++pkq == NQ) { pkq = 0; ++ptap; }
+    if (QT > 1) TTS_LOADQ(a1, ptap, pkq);
+    if (++pkq == NQ) { pkq = 0; ++ptap; }
+    if (g0) __syncthreads();  // previous group's B reads are done
+    for (int v0 = 0; v0 < tot; v0 += 4 * NTHR) {
+      uint4 r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int v = min(v0 + i * NTHR + tid, tot - 1);
+        const int rr = v / VPR, cc = v - rr * VPR;
+        const int xr = min(max(x_start + rr, 0), xlast);
+        r[i] = *reinterpret_cast<const uint4*>(X + (long long)xr * p.sxr + g0 + cc * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int v = v0 + i * NTHR + tid;
+        if (v < tot) {
+          const int rr = v / VPR, cc = v - rr * VPR;
+          const int xr = x_start + rr;
+          *reinterpret_cast<uint4*>(smem + rr * RS + cc * 16) = act16<T>(r[i], xr >= 0 && xr < xlen, p.in_slope);
+        }
+      }
+    }
+    __syncthreads();
+    int ctap = 0, ckq = 0;
+    for (int q = 0; q < QT; q += 2) {
+      TTS_MMAQ(a0, ctap, ckq);
+      if (++ckq == NQ) { ckq = 0; ++ctap; }
+      if (q + 2 < QT) {
+        TTS_LOADQ(a0, ptap, pkq);
+        if (++pkq == NQ) { pkq = 0; ++ptap; }
+      }
+      if (q + 1 < QT) {
+        TTS_MMAQ(a1, ctap, ckq);
+        if (++ckq == NQ) { ckq = 0; ++ctap; }
+        if (q + 3 < QT) {
+          TTS_LOADQ(a1, ptap, pkq);
+          if (++pkq == NQ) { pkq = 0; ++ptap; }
+        }
+      }
+    }
+  }
+#undef TTS_LOADQ
+#undef TTS_MMAQ
+
+  // ---- epilogue through LDS: fragments -> fp32 rows -> 8-channel row pieces ----
   T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.syb + (long long)hd * p.syh;
   const T* R1 = p.r1 ? reinterpret_cast<const T*>(p.r1) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const T* R2 = p.r2 ? reinterpret_cast<const T*>(p.r2) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const int tlen = p.up_len ? min(p.up_len[b], (p.y_rows - 1) * p.up_s) : 0;
+  const int cl = tid & 15;                    // 8-channel piece of the block's 128 channels
+  const int m8 = blockIdx.y * 128 + cl * 8;
+  const bool mok = m8 < p.M;
+  f32x4 bias0 = {}, bias1 = {};
+  if (p.bias && mok) {
+    bias0 = *reinterpret_cast<const f32x4*>(p.bias + m8);
+    bias1 = *reinterpret_cast<const f32x4*>(p.bias + m8 + 4);
+  }
+  int q = 0, col = m8;
+  if (p.up_s) { q = m8 / p.up_cout; col = m8 - q * p.up_cout; }
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
+  for (int half = 0; half < NT / 2; ++half) {
+    __syncthreads();  // X tile / previous half no longer read
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int n = n0 + n_w0 + nt * 32 + l31;
-      if (n >= ylen) continue;
+    for (int k = 0; k < 2; ++k)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int m = m_w0 + mt * 32 + 8 * g + 4 * hh;
-        if (m >= p.M) continue;
-        int row = n, col = m;
-        if (p.up_s) {
-          const int q = m / p.up_cout;
-          row = n * p.up_s + q - p.up_p;
-          col = m - q * p.up_cout;
-          if (row < 0 || row >= tlen) continue;
-        }
-        f32x4 v = {acc[mt][nt][4 * g + 0], acc[mt][nt][4 * g + 1], acc[mt][nt][4 * g + 2],
-                   acc[mt][nt][4 * g + 3]};
-        if (p.bias) {
-          const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + m);
-          v += bb;
-        }
-        if (p.alpha != 1.0f) v *= p.alpha;
-        if (p.act_out) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = apply_act(v[i], p.act_out, p.out_slope);
-        }
-        if (R1) v += Vec4<T>::load(R1 + (long long)row * p.srr + col);
-        if (R2) v += Vec4<T>::load(R2 + (long long)row * p.srr + col);
-        if (p.out_scale != 1.0f) v *= p.out_scale;
-        Vec4<T>::store(Y + (long long)row * p.syr + col, v);
+        const f32x16& a = acc[2 * half + k];
+        *reinterpret_cast<f32x4*>(smem + (k * 32 + l31) * XRES_OS + (wave * 32 + 8 * g + 4 * hh) * 4) =
+            f32x4{a[4 * g + 0], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]};
       }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < XRES_HR * 16 / NTHR; ++it) {
+      const int rl = (tid >> 4) + it * (NTHR / 16);
+      const int n = n0 + half * XRES_HR + rl;
+      if (n >= ylen || !mok) continue;
+      int row = n;
+      if (p.up_s) {
+        row = n * p.up_s + q - p.up_p;
+        if (row < 0 || row >= tlen) continue;
+      }
+      f32x4 v0 = *reinterpret_cast<const f32x4*>(smem + rl * XRES_OS + cl * 32);
+      f32x4 v1 = *reinterpret_cast<const f32x4*>(smem + rl * XRES_OS + cl * 32 + 16);
+      v0 += bias0; v1 += bias1;
+      if (p.alpha != 1.0f) { v0 *= p.alpha; v1 *= p.alpha; }
+      if (p.act_out) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v0[i] = apply_act(v0[i], p.act_out, p.out_slope);
+          v1[i] = apply_act(v1[i], p.act_out, p.out_slope);
+        }
+      }
+      if (R1) { f32x4 a, c; ld8<T>(R1 + (long long)row * p.srr + col, a, c); v0 += a; v1 += c; }
+      if (R2) { f32x4 a, c; ld8<T>(R2 + (long long)row * p.srr + col, a, c); v0 += a; v1 += c; }
+      if (p.out_scale != 1.0f) { v0 *= p.out_scale; v1 *= p.out_scale; }
+      st8<T>(Y + (long long)row * p.syr + col, v0, v1);
     }
   }
+}
+
+constexpr int XRES_LDS_MAX = 53 * 1024;  // 3 blocks per CU
+
+// channel group for the X-resident kernel: largest CG | Cin, CG % 64 == 0, tile within
+// XRES_LDS_MAX; 0 = not eligible
+static int xres_group(const ConvParams& p, int BN) {
+  if (!p.wpk || p.M < 128 || p.Cin % 64 || p.M % 8 || p.nh != 1) return 0;
+  if (p.syr % 8 || p.syb % 8 || ((p.r1 || p.r2) && (p.srr % 8 || p.srb % 8))) return 0;
+  if (p.up_s && p.up_cout % 8) return 0;
+  const int R = BN + (p.taps - 1) * p.dil;
+  for (int cg = p.Cin; cg >= 64; cg -= 64) {
+    if (p.Cin % cg) continue;
+    if ((size_t)R * (cg * 2 + 16) <= XRES_LDS_MAX) return cg;
+  }
+  return 0;
+}
+
+static int xres_mode() {  // TTS_CONV_XRES=0 disables the X-resident kernel (A/B runs)
+  static int m = [] {
+    const char* e = getenv("TTS_CONV_XRES");
+    return e ? atoi(e) : 1;
+  }();
+  return m;
+}
+
+template <typename T>
+static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err) {
+  constexpr int NT = 4, BN = 32 * NT;
+  if (!xres_mode()) return false;
+  const int cg = xres_group(p, BN);
+  if (!cg) return false;
+  const size_t lds = std::max((size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16), (size_t)XRES_HR * XRES_OS);
+  dim3 grid((p.y_rows + BN - 1) / BN, (p.M + 127) / 128, p.B * p.nh);
+  hipLaunchKernelGGL((conv_xres_kernel<T, NT>), grid, dim3(256), lds, s, p, cg);
+  *err = hipGetLastError();
+  return true;
 }
 
 template <typename T, int MT, int NT, int WM, int WN, int CK>
@@ -270,6 +518,9 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
     if (wide) return launch_cfg<T, 1, 2, 2, 2, CKWW>(p, s);
     return launch_cfg<T, 1, 2, 2, 2, CKW>(p, s);
   }
+  // M >= 128: 4 waves stacked along M, 32 x 128 per wave.  (A 32 x 256 strip per wave
+  // cuts the L2-served weight bytes per MFMA in half but needs 235 VGPRs -> 2 waves/SIMD,
+  // and measured 1.8x slower: the kernel is latency/issue-bound, not weight-bandwidth-bound.)
   if (wide) return launch_cfg<T, 1, 4, 4, 1, CKWW>(p, s);
   return launch_cfg<T, 1, 4, 4, 1, CKW>(p, s);
 }
@@ -295,8 +546,16 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why) {
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s) {
   switch (dtype) {
     case DT_F32: return launch_t<float>(p, s);
-    case DT_F16: return launch_t<half_t>(p, s);
-    case DT_BF16: return launch_t<bf16_t>(p, s);
+    case DT_F16: {
+      hipError_t e;
+      if (launch_xres<half_t>(p, s, &e)) return e;
+      return launch_t<half_t>(p, s);
+    }
+    case DT_BF16: {
+      hipError_t e;
+      if (launch_xres<bf16_t>(p, s, &e)) return e;
+      return launch_t<bf16_t>(p, s);
+    }
   }
   return hipErrorInvalidValue;
 }

@@ -131,6 +131,7 @@ struct tts_engine {
         }
     ConvLayer L;
     L.w = track(upload(p, dt));
+    L.wpk = frag_pack(p, M, taps, ci, dt, allocs);
     const auto& bh = get(bname).data;
     std::vector<float> b(M);
     for (int r = 0; r < s; ++r)
@@ -317,7 +318,7 @@ struct tts_engine {
                 const int* up_len, int dt, hipStream_t s) {
     ConvParams p = conv_params_default();
     p.x = x; p.sxb = sxb; p.sxr = sxr; p.x_len = x_len; p.x_rows = x_rows;
-    p.w = L.w; p.w_ld = L.taps * L.Cin;
+    p.w = L.w; p.w_ld = L.taps * L.Cin; p.wpk = L.wpk;
     p.bias = L.bias;
     p.y = y; p.syb = syb; p.syr = syr;
     p.r1 = r1; p.r2 = r2; p.srb = srb; p.srr = srr;

@@ -22,6 +22,9 @@ struct ConvParams {
   // optional head batching: grid z = B * nh, z -> (b = z / nh, h = z % nh); every pointer is
   // offset by b * s?b + h * s?h (lengths are indexed by b)
   int nh; long long sxh, swh, syh, srh;
+  // optional fragment-packed copy of w (frag_pack in runtime.h): enables the X-resident
+  // kernel, whose weight loads are then contiguous 1 KiB wave reads
+  const void* wpk;
 };
 
 inline ConvParams conv_params_default() {

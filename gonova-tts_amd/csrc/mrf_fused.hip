@@ -64,12 +64,7 @@ __device__ inline uint4 gload16(const char* p) {
 }
 
 template <typename T>
-__device__ inline uint4 lrelu16(uint4 u, float slope) {
-  T* e = reinterpret_cast<T*>(&u);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) e[i] = from_f32<T>(leaky(to_f32(e[i]), slope));
-  return u;
-}
+__device__ inline uint4 lrelu16(uint4 u, float slope) { return lrelu_chunk<T>(u, slope); }
 
 template <typename T, int C, int BN>
 __global__ __launch_bounds__(512, 2) void mrf_fused_kernel(MrfParams p) {

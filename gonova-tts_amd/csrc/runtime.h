@@ -63,10 +63,34 @@ inline float* upload_f32(const std::vector<float>& h) { return (float*)upload(h,
 // A packed implicit-GEMM conv layer: W[M][taps][Cin] in the compute dtype, bias fp32 [M].
 struct ConvLayer {
   void* w = nullptr;
+  void* wpk = nullptr;  // fragment-packed copy (frag_pack), or null
   float* bias = nullptr;
   int M = 0, Cin = 0, taps = 1, dil = 1, pad = 0;
   int up_s = 0, up_cout = 0, up_p = 0;  // transposed-conv output mapping
 };
+
+// Fragment-packed weights for conv_xres_kernel: W[M][taps][Cin] (host fp32) ->
+//   P[M/32][taps][Cin/16][lane 0..63][8],  lane l holding row 32*mb + (l & 31),
+//   channels 16*ks + 8*(l >> 5) + [0, 8)   (the A operand of v_mfma_f32_32x32x16_*),
+// so one wave's fragment for (32-row block, tap, k-step) is 1 KiB contiguous.  Rows past
+// M are zero.  Only for 16-bit dtypes with Cin % 64 == 0 and M >= 128 (else null).
+inline void* frag_pack(const std::vector<float>& w, int M, int taps, int ci, int dt, std::vector<void*>& allocs) {
+  if (dt == DT_F32 || ci % 64 || M < 128) return nullptr;
+  const int MB = (M + 31) / 32, KS = ci / 16;
+  std::vector<float> p((size_t)MB * 32 * taps * ci, 0.f);
+  size_t o = 0;
+  for (int mb = 0; mb < MB; ++mb)
+    for (int t = 0; t < taps; ++t)
+      for (int ks = 0; ks < KS; ++ks)
+        for (int l = 0; l < 64; ++l) {
+          const int m = mb * 32 + (l & 31);
+          for (int j = 0; j < 8; ++j, ++o)
+            if (m < M) p[o] = w[((size_t)m * taps + t) * ci + ks * 16 + 8 * (l >> 5) + j];
+        }
+  void* d = upload(p, dt);
+  allocs.push_back(d);
+  return d;
+}
 
 // nn.Conv1d weight [Cout][Cin][k] (host fp32) -> ConvLayer; scale[o] (optional) folds a
 // per-output-channel factor (BatchNorm) into the weights.
@@ -83,6 +107,7 @@ inline ConvLayer make_conv(const std::vector<float>& w, int co, int ci, int k, c
   ConvLayer L;
   L.w = upload(p, dt);
   allocs.push_back(L.w);
+  L.wpk = frag_pack(p, co, k, ci, dt, allocs);
   std::vector<float> b = bias;
   if (b.empty()) b.assign(co, 0.f);
   if (b.size() != (size_t)co) throw TtsError(TTS_ERR_INVALID, "conv bias size mismatch");
@@ -148,7 +173,7 @@ inline void run_layer(const ConvLayer& L, const void* x, int x_rows, const int* 
   ConvParams p = conv_params_default();
   const int xl = x_ld ? x_ld : L.Cin, yl = y_ld ? y_ld : L.M;
   p.x = x; p.sxb = (long long)x_rows * xl; p.sxr = xl; p.x_len = lens; p.x_rows = x_rows;
-  p.w = L.w; p.w_ld = L.taps * L.Cin; p.bias = L.bias;
+  p.w = L.w; p.w_ld = L.taps * L.Cin; p.bias = L.bias; p.wpk = L.wpk;
   p.y = y; p.syb = (long long)y_rows * yl; p.syr = yl;
   p.r1 = r1; p.r2 = r2; p.srb = p.syb; p.srr = yl;
   p.y_len = lens; p.y_rows = y_rows;

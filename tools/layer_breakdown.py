@@ -29,7 +29,7 @@ def main():
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 32
     T = int(sys.argv[3]) if len(sys.argv) > 3 else 862
     rows = [r for r in csv.DictReader(open(path))
-            if "conv_gemm" in r["Kernel_Name"] or "conv_post" in r["Kernel_Name"] or "pair" in r["Kernel_Name"]]
+            if "conv_gemm" in r["Kernel_Name"] or "conv_xres" in r["Kernel_Name"] or "conv_post" in r["Kernel_Name"] or "pair" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     layers = vocoder_layers(T)
     last = rows[-len(layers):]

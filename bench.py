@@ -16,9 +16,11 @@ utterances are independent, so every rank runs its own batch-32 shard with no
 data-path collective (weak scaling); the timed loop is bracketed by barriers and
 the max time over ranks is used.  value = samples of all ranks / max time.
 
-`roofline` is for the dominant kernel family (the implicit-GEMM MFMA conv, timed
-live with hipEvents around every launch on its stream); `cpu_baseline` is the
-NumPy oracle on the host cores (bounded sample, rank 0 only).
+`roofline` is for the dominant kernel family (largest summed time per step: today the
+X-resident implicit-GEMM conv of stages 0-1), timed live with hipEvents around every
+launch on the stream it runs on; `roofline.kernels` lists every family the same way
+(conv_gemm_kernel, conv_xres_kernel, mrf_fused_kernel).  `cpu_baseline` is the NumPy
+oracle on the host cores (bounded sample, rank 0 only).
 """
 from __future__ import annotations
 
@@ -113,34 +115,49 @@ class Ctx:
         prof = None
         if eng is not None:
             eng.profile(False)
-            prof = eng.profile_read()
+            prof = eng.profile_read_kinds()
         return self.max_over_ranks(el), prof
 
 
-def pmc_traffic():
-    """HBM bytes per conv_gemm launch from the committed PMC summary (tools/pmc_traffic.py), if any."""
+def pmc_traffic(kernel):
+    """HBM bytes per launch of one kernel family from the newest committed PMC summary
+    (tools/pmc_traffic.py, profiles/*_pmc_traffic_c2.json), if it covers that family."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic_c2.json")))
     if not files:
         return None
     d = json.load(open(files[-1]))
-    return {"bytes_per_launch": round(d["traffic_bytes_per_launch"]),
-            "algorithmic_bytes_per_launch": round(d["algorithmic_bytes_per_launch"]),
-            "ratio": round(d["ratio_traffic_over_algorithmic"], 3),
+    fam = d.get("families", {}).get(kernel.replace("_kernel", ""))
+    if fam is None:
+        return None
+    return {"bytes_per_launch": round(fam["traffic_bytes_per_launch"]),
+            "algorithmic_bytes_per_launch": round(fam["algorithmic_bytes_per_launch"]),
+            "ratio": round(fam["ratio_traffic_over_algorithmic"], 3),
             "source": os.path.relpath(files[-1], ROOT)}
 
 
-def roofline(prof, elapsed, steps, dtype, kernel, traffic=None):
-    gemm_ms, gemm_flops, n_launch = prof
-    per_launch_flops = gemm_flops / max(n_launch, 1)
-    avg_launch_ms = gemm_ms / max(n_launch, 1)
-    achieved = per_launch_flops / (avg_launch_ms * 1e-3) / 1e12 if n_launch else 0.0
+def roofline(prof, elapsed, steps, dtype, traffic_for=None):
+    """Roofline of the dominant kernel family (largest summed time in the timed steps),
+    from the engine's live hipEvent timing: achieved = algorithmic FLOPs per launch / that
+    family's average launch duration.  `kernels` lists every family the same way."""
+    kernels = {}
+    for name, (ms, fl, n) in prof.items():
+        if n:
+            kernels[name] = {"ms_per_step": round(ms / steps, 3), "launches_per_step": n // max(steps, 1),
+                             "avg_launch_us": round(ms / n * 1e3, 2),
+                             "achieved_tflops": round(fl / (ms * 1e-3) / 1e12, 2)}
+    name = max(prof, key=lambda k: prof[k][0])
+    ms, fl, n = prof[name]
+    per_launch_flops = fl / max(n, 1)
+    avg_launch_ms = ms / max(n, 1)
+    achieved = per_launch_flops / (avg_launch_ms * 1e-3) / 1e12 if n else 0.0
     peak = MFMA_PEAK_TFLOPS[dtype]
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 5), "traffic": traffic, "kernel": kernel,
+            "frac": round(achieved / peak, 5),
+            "traffic": traffic_for(name) if traffic_for else None, "kernel": name,
             "flops_per_launch": round(per_launch_flops),
-            "avg_launch_us": round(avg_launch_ms * 1e3, 2), "launches_per_step": n_launch // max(steps, 1),
-            "gemm_share_of_step": round(gemm_ms / (elapsed * 1e3), 4)}
+            "avg_launch_us": round(avg_launch_ms * 1e3, 2), "launches_per_step": n // max(steps, 1),
+            "share_of_step": round(ms / (elapsed * 1e3), 4), "kernels": kernels}
 
 
 def bench_vocoder(ctx, args):
@@ -161,8 +178,7 @@ def bench_vocoder(ctx, args):
     out = {"value": value, "ms_per_step": el * 1e3 / args.steps, "samples_per_utt": T * 256,
            "algorithmic_tflops_per_gpu": value / ctx.world * vocoder_flops_per_sample() / 1e12,
            "roofline": roofline(prof, el, args.steps, args.dtype,
-                                "conv_gemm_kernel (implicit-GEMM MFMA conv, all vocoder launches)",
-                                pmc_traffic() if (B, T, args.dtype) == (32, 862, "f16") else None)}
+                                pmc_traffic if (B, T, args.dtype) == (32, 862, "f16") else None)}
     eng.close()
     return out
 
@@ -200,7 +216,7 @@ def bench_full(ctx, args, steps, warmup):
             "x_realtime_per_gpu": round(value / ctx.world / SR, 2), "dtype": "bf16",
             "config": {"workload": "C3 full pipeline (tokens -> FS2-Conformer -> HiFi-GAN), "
                                    f"batch-{B} x {N} tokens x {dur} frames = {T} frames (10.03 s)"},
-            "roofline": roofline(prof, el, steps, "bf16", "conv_gemm_kernel (all acoustic + vocoder GEMM launches)")}
+            "roofline": roofline(prof, el, steps, "bf16")}
 
 
 def bench_c4(ctx, args):

@@ -253,7 +253,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
 //  * the next chunk's X rows (an HBM read) were issued before the next tap's weights, and
 //    vmcnt retires loads in order; here a block stages one channel group of its X tile
 //    (every tap's rows, LeakyReLU applied) in LDS once, and the MFMA loop then has only
-//    weight loads in flight: no barriers, weights one quad (4 k-steps = 4*NT MFMAs) ahead;
+//    weight loads in flight: no barriers, weights two quads (4 k-steps = 4*NT MFMAs each)
+//    ahead in a 3-deep register ring;
 //  * the epilogue's residual reads and output writes were fragment-shaped too (32 rows x
 //    8 B); here the fp32 tile goes through LDS (two 64-row halves) and the bias / act /
 //    residual / scale pass reads and writes whole 16-byte row pieces.
@@ -314,7 +315,6 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
   const int QT = p.taps * NQ;          // quads per channel group
   const int x_start = n0 - p.pad;
   const int xlast = xlen > 0 ? xlen - 1 : 0;
-  const int tot = R * VPR;
   const int dstep = p.dil * RS;        // LDS bytes per tap
   const char* xl = smem + l31 * RS + hh * 16;
 
@@ -340,30 +340,46 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
     }                                                                                     \
   } while (0)
 
+  // X staging: thread owns 16-byte column cc of the group and rows r0, r0 + rstep, ...
+  // (CG is a power of two: no per-vector division)
+  const int lvpr = __builtin_ctz(VPR);
+  const int cc = tid & (VPR - 1);
+  const int r0 = tid >> lvpr;
+  const int rstep = NTHR >> lvpr;
+  // quad ring, 3 deep: quad q's weights are issued while quads q-2 and q-1 compute
+#define TTS_STEP(A_, QQ_)                                                                 \
+  if ((QQ_) < QT) {                                                                       \
+    TTS_MMAQ(A_, ctap, ckq);                                                              \
+    if (++ckq == NQ) { ckq = 0; ++ctap; }                                                 \
+    if ((QQ_) + 3 < QT) {                                                                 \
+      TTS_LOADQ(A_, ptap, pkq);                                                           \
+      if (++pkq == NQ) { pkq = 0; ++ptap; }                                               \
+    }                                                                                     \
+  }
   for (int g0 = 0; g0 < p.Cin; g0 += CG) {
-    Frag a0[4], a1[4];
-    // first two quads of the group in flight before the X loads (in-order vmcnt: they
+    Frag a0[4], a1[4], a2[4];
+    // first quads of the group in flight before the X loads (in-order vmcnt: they
     // complete first and are ready when the MFMA loop starts)
     int ptap = 0, pkq = 0;
     TTS_LOADQ(a0, ptap, pkq);
     if (++pkq == NQ) { pkq = 0; ++ptap; }
     if (QT > 1) TTS_LOADQ(a1, ptap, pkq);
     if (++pkq == NQ) { pkq = 0; ++ptap; }
+    if (QT > 2) TTS_LOADQ(a2, ptap, pkq);
+    if (++pkq == NQ) { pkq = 0; ++ptap; }
     if (g0) __syncthreads();  // previous group's B reads are done
-    for (int v0 = 0; v0 < tot; v0 += 4 * NTHR) {
+    const T* xg = X + g0 + cc * 8;
+    for (int rb = r0; rb < R; rb += 4 * rstep) {
       uint4 r[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int v = min(v0 + i * NTHR + tid, tot - 1);
-        const int rr = v / VPR, cc = v - rr * VPR;
-        const int xr = min(max(x_start + rr, 0), xlast);
-        r[i] = *reinterpret_cast<const uint4*>(X + (long long)xr * p.sxr + g0 + cc * 8);
+        const int xr = min(max(x_start + min(rb + i * rstep, R - 1), 0), xlast);
+        r[i] = *reinterpret_cast<const uint4*>(xg + xr * p.sxr);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int v = v0 + i * NTHR + tid;
-        if (v < tot) {
-          const int rr = v / VPR, cc = v - rr * VPR;
+        const int rr = rb + i * rstep;
+        if (rr < R) {
           const int xr = x_start + rr;
           *reinterpret_cast<uint4*>(smem + rr * RS + cc * 16) = act16<T>(r[i], xr >= 0 && xr < xlen, p.in_slope);
         }
@@ -371,23 +387,13 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
     }
     __syncthreads();
     int ctap = 0, ckq = 0;
-    for (int q = 0; q < QT; q += 2) {
-      TTS_MMAQ(a0, ctap, ckq);
-      if (++ckq == NQ) { ckq = 0; ++ctap; }
-      if (q + 2 < QT) {
-        TTS_LOADQ(a0, ptap, pkq);
-        if (++pkq == NQ) { pkq = 0; ++ptap; }
-      }
-      if (q + 1 < QT) {
-        TTS_MMAQ(a1, ctap, ckq);
-        if (++ckq == NQ) { ckq = 0; ++ctap; }
-        if (q + 3 < QT) {
-          TTS_LOADQ(a1, ptap, pkq);
-          if (++pkq == NQ) { pkq = 0; ++ptap; }
-        }
-      }
+    for (int q = 0; q < QT; q += 3) {
+      TTS_STEP(a0, q)
+      TTS_STEP(a1, q + 1)
+      TTS_STEP(a2, q + 2)
     }
   }
+#undef TTS_STEP
 #undef TTS_LOADQ
 #undef TTS_MMAQ
 
@@ -449,15 +455,15 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
 
 constexpr int XRES_LDS_MAX = 53 * 1024;  // 3 blocks per CU
 
-// channel group for the X-resident kernel: largest CG | Cin, CG % 64 == 0, tile within
+// channel group for the X-resident kernel: largest power-of-two CG | Cin, CG >= 64, tile within
 // XRES_LDS_MAX; 0 = not eligible
 static int xres_group(const ConvParams& p, int BN) {
   if (!p.wpk || p.M < 128 || p.Cin % 64 || p.M % 8 || p.nh != 1) return 0;
   if (p.syr % 8 || p.syb % 8 || ((p.r1 || p.r2) && (p.srr % 8 || p.srb % 8))) return 0;
   if (p.up_s && p.up_cout % 8) return 0;
   const int R = BN + (p.taps - 1) * p.dil;
-  for (int cg = p.Cin; cg >= 64; cg -= 64) {
-    if (p.Cin % cg) continue;
+  for (int cg = 2048; cg >= 64; cg /= 2) {  // powers of two (division-free staging)
+    if (cg > p.Cin || p.Cin % cg) continue;
     if ((size_t)R * (cg * 2 + 16) <= XRES_LDS_MAX) return cg;
   }
   return 0;
@@ -541,6 +547,10 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why) {
   if (p.x_rows <= 0 || p.y_rows <= 0) { *why = "empty rows"; return -1; }
   if (p.nh < 1 || p.sxh % epv || p.swh % epv || p.syh % 4 || p.srh % 4) { *why = "bad head batching"; return -1; }
   return 0;
+}
+
+int conv_gemm_kind(int dtype, const ConvParams& p) {
+  return (dtype != DT_F32 && xres_mode() && xres_group(p, 128)) ? PK_CONV_XRES : PK_CONV_GEMM;
 }
 
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s) {

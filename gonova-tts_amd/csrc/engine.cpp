@@ -383,7 +383,7 @@ struct tts_engine {
         const double fl = 2.0 * ch * (double)ch * (double)B * Tout * 2.0 * tab.npair *
                           [&] { double k = 0; for (int j = 0; j < nk; ++j) k += tab.k[j]; return k; }();
         if (prof.on) {
-          Profiler::Rec r{prof.get(), prof.get(), fl};
+          Profiler::Rec r{prof.get(), prof.get(), fl, PK_MRF_FUSED};
           HIP_CHECK(hipEventRecord(r.a, s));
           HIP_CHECK(mrf_fused_launch(dt, ch, mp, s));
           HIP_CHECK(hipEventRecord(r.b, s));
@@ -579,6 +579,13 @@ int tts_engine_profile(tts_engine* eng, int enable) {
 
 int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops, int* n_launches) {
   return guarded(eng, [&] { eng->prof.read(gemm_ms, gemm_flops, n_launches); });
+}
+
+int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, double* flops, int* n_launches) {
+  return guarded(eng, [&] {
+    if (nkinds < 1 || !ms || !flops || !n_launches) throw TtsError(TTS_ERR_INVALID, "profile_read_kinds: bad arguments");
+    eng->prof.read_kinds(nkinds, ms, flops, n_launches);
+  });
 }
 
 int tts_op_conv1d(int dtype, const tts_conv_desc* d, void* stream) {

@@ -37,6 +37,10 @@ inline ConvParams conv_params_default() {
 int conv_gemm_check(const ConvParams& p, int dtype, const char** why);
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s);
 
+// kernel family a launch runs as (live profiling buckets; tts_engine_profile_read_kinds)
+enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_MRF_FUSED = 2, PK_N = 3 };
+int conv_gemm_kind(int dtype, const ConvParams& p);
+
 // Fused MRF stage (mrf_fused.hip): all resblocks of one HiFi-GAN stage in one launch.
 constexpr int MRF_MAX_STEPS = 96;
 // Device-resident schedule of one stage (uploaded once; read with uniform indices -> scalar loads).

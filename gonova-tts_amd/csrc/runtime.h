@@ -120,7 +120,7 @@ inline ConvLayer make_conv(const std::vector<float>& w, int co, int ci, int k, c
 // Live kernel timing (bench.py roofline): hipEvents around every implicit-GEMM launch.
 struct Profiler {
   bool on = false;
-  struct Rec { hipEvent_t a, b; double flops; };
+  struct Rec { hipEvent_t a, b; double flops; int kind; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
   hipEvent_t get() {
@@ -129,20 +129,28 @@ struct Profiler {
     HIP_CHECK(hipEventCreate(&e));
     return e;
   }
-  void read(double* ms, double* fl, int* n) {
-    double m = 0, f = 0;
-    int c = 0;
+  // sums per ProfKind (arrays of nk entries; kinds >= nk are dropped), then resets
+  void read_kinds(int nk, double* ms, double* fl, int* n) {
+    for (int k = 0; k < nk; ++k) { ms[k] = 0; fl[k] = 0; n[k] = 0; }
     for (auto& r : recs) {
       HIP_CHECK(hipEventSynchronize(r.b));
       float e = 0.f;
       HIP_CHECK(hipEventElapsedTime(&e, r.a, r.b));
-      m += e; f += r.flops; ++c;
+      if (r.kind < nk) { ms[r.kind] += e; fl[r.kind] += r.flops; ++n[r.kind]; }
       pool.push_back(r.a); pool.push_back(r.b);
     }
     recs.clear();
-    if (ms) *ms = m;
-    if (fl) *fl = f;
-    if (n) *n = c;
+  }
+  void read(double* ms, double* fl, int* n) {
+    double m[PK_N], f[PK_N];
+    int c[PK_N];
+    read_kinds(PK_N, m, f, c);
+    double tm = 0, tf = 0;
+    int tc = 0;
+    for (int k = 0; k < PK_N; ++k) { tm += m[k]; tf += f[k]; tc += c[k]; }
+    if (ms) *ms = tm;
+    if (fl) *fl = tf;
+    if (n) *n = tc;
   }
   ~Profiler() {
     for (auto& r : recs) { hipEventDestroy(r.a); hipEventDestroy(r.b); }
@@ -155,7 +163,7 @@ inline void launch_conv_checked(const ConvParams& p, int dt, hipStream_t s, Prof
   const char* why = nullptr;
   if (conv_gemm_check(p, dt, &why)) throw TtsError(TTS_ERR_INVALID, std::string("conv: ") + why);
   if (prof && prof->on) {
-    Profiler::Rec r{prof->get(), prof->get(), flops};
+    Profiler::Rec r{prof->get(), prof->get(), flops, conv_gemm_kind(dt, p)};
     HIP_CHECK(hipEventRecord(r.a, s));
     HIP_CHECK(conv_gemm_launch(dt, p, s));
     HIP_CHECK(hipEventRecord(r.b, s));

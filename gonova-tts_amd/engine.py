@@ -65,6 +65,8 @@ C_API = [
     ("tts_engine_profile", _I, [_VP, _I]),
     ("tts_engine_profile_read", _I, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_int)]),
+    ("tts_engine_profile_read_kinds", _I, [_VP, _I, ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     ("tts_last_error", ctypes.c_char_p, []),
     ("tts_op_conv1d", _I, [_I, ctypes.POINTER(TtsConvDesc), _VP]),
 ]
@@ -231,6 +233,15 @@ class HipEngine:
         check(self.lib.tts_engine_profile_read(self.handle, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(n)),
               "profile_read")
         return ms.value, fl.value, n.value
+
+    PROFILE_KINDS = ("conv_gemm_kernel", "conv_xres_kernel", "mrf_fused_kernel")
+
+    def profile_read_kinds(self):
+        """-> {kernel name: (summed ms, algorithmic FLOPs, launch count)}; resets."""
+        k = len(self.PROFILE_KINDS)
+        ms, fl, n = (ctypes.c_double * k)(), (ctypes.c_double * k)(), (ctypes.c_int * k)()
+        check(self.lib.tts_engine_profile_read_kinds(self.handle, k, ms, fl, n), "profile_read_kinds")
+        return {name: (ms[i], fl[i], n[i]) for i, name in enumerate(self.PROFILE_KINDS)}
 
     def close(self):
         if getattr(self, "handle", None):

@@ -102,6 +102,9 @@ int tts_acoustic_forward(tts_engine* eng, const int32_t* d_tokens, const int32_t
  * kernel time (ms), the algorithmic FLOPs of those launches and their count, then resets. */
 int tts_engine_profile(tts_engine* eng, int enable);
 int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops, int* n_launches);
+/* The same, split by kernel family into arrays of nkinds entries:
+ * 0 = conv_gemm_kernel, 1 = conv_xres_kernel, 2 = mrf_fused_kernel. */
+int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, double* flops, int* n_launches);
 
 /* Thread-local message describing the last failure on this thread. */
 const char* tts_last_error(void);

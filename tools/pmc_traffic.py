@@ -1,45 +1,78 @@
-"""HBM traffic of the implicit-GEMM conv launches from two rocprofv3 PMC passes.
+"""HBM traffic per kernel family of the default (fused) vocoder step, from two rocprofv3 PMC
+passes (tools/pmc_traffic.sh).
 
 usage: python tools/pmc_traffic.py <FETCH_SIZE dir> <WRITE_SIZE dir> [out.json] [B T]
 
 Counters are collected in separate passes (TCC slots: FETCH_SIZE costs 3, WRITE_SIZE 2),
 each with --kernel-trace only (MI355X_MICROARCH.md §rocprofv3 PMC slots).  Both are in
 KB.  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports exactly half the
-bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled; every operand
-load of conv_gemm_kernel is a 16-byte-per-lane load.  WRITE_SIZE is exact for 16-B
-stores and is used as is (the kernel's 8-byte stores are uncalibrated -- stated).
+bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled; every HBM load of
+these kernels is a 16-byte-per-lane load.  WRITE_SIZE is exact for 16-B stores (conv_xres
+and mrf_fused write 16-B row pieces / 8-B fragments -- the latter uncalibrated, stated).
 
-The last vocoder step's 77 conv launches are averaged and compared with their
-algorithmic bytes (read X once, read W once, write Y once, read residuals once).
+The last step's launches are mapped onto the step's layer sequence
+  pre, s0.up, 18 x s0 conv, s1.up, 18 x s1 conv, s2.up, s2 MRF (fused), s3.up, s3 MRF, post
+and each family's traffic is compared with its algorithmic bytes: every conv reads its
+input rows once, its weights once, writes its output once (+ the residual read of a
+ResBlock's second conv); a fused MRF stage reads the stage input once, writes the MRF mean
+once and reads its 18 weight slabs once.
 """
 import csv
 import json
+import os
 import sys
+from collections import defaultdict
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tools.layer_breakdown import vocoder_layers  # noqa: E402
+
+FAMILIES = ("conv_gemm", "conv_xres", "mrf_fused", "conv_post")
+
+
+def family(name):
+    for f in FAMILIES:
+        if f in name:
+            return f
+    return None
 
 
 def per_dispatch(path, counter):
-    vals = {}
+    vals, names = {}, {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter or "conv_gemm" not in r["Kernel_Name"]:
+        if r["Counter_Name"] != counter or family(r["Kernel_Name"]) is None:
             continue
         d = int(r["Dispatch_Id"])
         vals[d] = vals.get(d, 0.0) + float(r["Counter_Value"])
-    return [vals[k] for k in sorted(vals)]
+        names[d] = family(r["Kernel_Name"])
+    ids = sorted(vals)
+    return [vals[i] for i in ids], [names[i] for i in ids]
 
 
-def algorithmic_bytes(B, T, elt=2):
+def fused_step_layers(B, T, elt=2):
+    """[(label, algorithmic bytes)] of one fused-path step, in launch order."""
     out = []
-    for name, M, cin, k, n in vocoder_layers(T):
+    layers = vocoder_layers(T)
+    mrf = defaultdict(list)
+    for name, M, cin, k, n in layers:
+        st = name.split(".")[0]
         if name == "post":
+            out.append(("post", B * n * cin * elt + B * n * 4))
             continue
-        x = B * n * cin * elt          # input rows read once
-        y = B * n * M * elt            # output written once (upsampler: M = s*Cout per input row)
-        w = M * cin * k * elt          # weights read once
-        r = y if name.endswith(".c2") else 0  # ResBlock residual (the MRF running sum adds 2/9 more)
-        out.append(x + y + w + r)
+        if name == "pre" or name.endswith(".up"):
+            out.append((name, B * n * cin * elt + B * n * M * elt + M * cin * k * elt))
+            if name.endswith(".up") and st in ("s2", "s3"):
+                out.append((f"{st}.mrf", None))  # filled below
+            continue
+        if st in ("s2", "s3"):
+            mrf[st].append((M, cin, k, n))
+            continue
+        r = B * n * M * elt if name.endswith(".c2") else 0
+        out.append((name, B * n * cin * elt + B * n * M * elt + M * cin * k * elt + r))
+    for i, (lab, b) in enumerate(out):
+        if lab.endswith(".mrf"):
+            convs = mrf[lab.split(".")[0]]
+            C, n = convs[0][0], convs[0][3]
+            out[i] = (lab, 2 * B * n * C * elt + sum(M * c * k * elt for M, c, k, _ in convs))
     return out
 
 
@@ -48,22 +81,30 @@ def main():
     outp = sys.argv[3] if len(sys.argv) > 3 else None
     B = int(sys.argv[4]) if len(sys.argv) > 4 else 32
     T = int(sys.argv[5]) if len(sys.argv) > 5 else 862
-    fetch = per_dispatch(f"{fdir}/run_counter_collection.csv", "FETCH_SIZE")
-    write = per_dispatch(f"{wdir}/run_counter_collection.csv", "WRITE_SIZE")
-    n = 77
-    fetch, write = fetch[-n:], write[-n:]
-    alg = algorithmic_bytes(B, T)
-    hbm = [(2.0 * f + w) * 1024.0 for f, w in zip(fetch, write)]
-    res = {
-        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace), last C2 step",
-        "correction": "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 FETCH_SIZE halves 16-B/lane reads)",
-        "launches": len(hbm),
-        "traffic_bytes_per_launch": sum(hbm) / len(hbm),
-        "algorithmic_bytes_per_launch": sum(alg) / len(alg),
-        "ratio_traffic_over_algorithmic": (sum(hbm) / sum(alg)),
-        "raw_fetch_kb_per_launch": sum(fetch) / len(fetch),
-        "raw_write_kb_per_launch": sum(write) / len(write),
-    }
+    fetch, fam = per_dispatch(f"{fdir}/run_counter_collection.csv", "FETCH_SIZE")
+    write, fam_w = per_dispatch(f"{wdir}/run_counter_collection.csv", "WRITE_SIZE")
+    step = fused_step_layers(B, T)
+    n = len(step)
+    fetch, fam, write, fam_w = fetch[-n:], fam[-n:], write[-n:], fam_w[-n:]
+    if fam != fam_w:
+        raise SystemExit("FETCH and WRITE passes dispatched different kernel sequences")
+    fams = {}
+    for f in FAMILIES:
+        idx = [i for i in range(n) if fam[i] == f]
+        if not idx:
+            continue
+        hbm = sum((2.0 * fetch[i] + write[i]) * 1024.0 for i in idx)
+        alg = sum(step[i][1] for i in idx)
+        fams[f] = {"launches_per_step": len(idx), "layers": [step[i][0] for i in idx],
+                   "traffic_bytes_per_launch": hbm / len(idx),
+                   "algorithmic_bytes_per_launch": alg / len(idx),
+                   "ratio_traffic_over_algorithmic": hbm / alg,
+                   "raw_fetch_kb_per_launch": sum(fetch[i] for i in idx) / len(idx),
+                   "raw_write_kb_per_launch": sum(write[i] for i in idx) / len(idx)}
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace), "
+                     "last C2 step of the default (fused) path",
+           "correction": "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 FETCH_SIZE halves 16-B/lane reads)",
+           "batch": B, "frames": T, "families": fams}
     print(json.dumps(res, indent=1))
     if outp:
         json.dump(res, open(outp, "w"), indent=1)

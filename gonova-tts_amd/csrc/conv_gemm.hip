@@ -265,6 +265,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
 // consecutive rows).
 constexpr int XRES_OS = 128 * 4 + 16;  // fp32 output staging row stride (bytes)
 constexpr int XRES_HR = 64;            // output rows staged per half
+constexpr int XRES_SU = 4;             // X staging loads in flight per thread
 
 template <typename T>
 __device__ inline void ld8(const T* p, f32x4& a, f32x4& b) {
@@ -369,15 +370,15 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
     if (++pkq == NQ) { pkq = 0; ++ptap; }
     if (g0) __syncthreads();  // previous group's B reads are done
     const T* xg = X + g0 + cc * 8;
-    for (int rb = r0; rb < R; rb += 4 * rstep) {
-      uint4 r[4];
+    for (int rb = r0; rb < R; rb += XRES_SU * rstep) {
+      uint4 r[XRES_SU];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < XRES_SU; ++i) {
         const int xr = min(max(x_start + min(rb + i * rstep, R - 1), 0), xlast);
         r[i] = *reinterpret_cast<const uint4*>(xg + xr * p.sxr);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < XRES_SU; ++i) {
         const int rr = rb + i * rstep;
         if (rr < R) {
           const int xr = x_start + rr;
@@ -412,6 +413,20 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
   }
   int q = 0, col = m8;
   if (p.up_s) { q = m8 / p.up_cout; col = m8 - q * p.up_cout; }
+  // every item's first-residual rows in flight before the staging barriers (the weight
+  // ring is dead here, so these registers do not raise the kernel's peak; prefetching r2
+  // as well would spill)
+  constexpr int NIT = XRES_HR * 16 / NTHR;
+  uint4 res1[NT / 2][NIT];
+#pragma unroll
+  for (int half = 0; half < NT / 2; ++half)
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int n = n0 + half * XRES_HR + (tid >> 4) + it * (NTHR / 16);
+      int row = min(n, ylen - 1);
+      if (p.up_s) row = min(max(row * p.up_s + q - p.up_p, 0), max(tlen - 1, 0));
+      if (R1) res1[half][it] = *reinterpret_cast<const uint4*>(R1 + (long long)row * p.srr + (mok ? col : 0));
+    }
 #pragma unroll
   for (int half = 0; half < NT / 2; ++half) {
     __syncthreads();  // X tile / previous half no longer read
@@ -425,7 +440,7 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
       }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < XRES_HR * 16 / NTHR; ++it) {
+    for (int it = 0; it < NIT; ++it) {
       const int rl = (tid >> 4) + it * (NTHR / 16);
       const int n = n0 + half * XRES_HR + rl;
       if (n >= ylen || !mok) continue;
@@ -445,7 +460,7 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
           v1[i] = apply_act(v1[i], p.act_out, p.out_slope);
         }
       }
-      if (R1) { f32x4 a, c; ld8<T>(R1 + (long long)row * p.srr + col, a, c); v0 += a; v1 += c; }
+      if (R1) { f32x4 a, c; ld8<T>(reinterpret_cast<const T*>(&res1[half][it]), a, c); v0 += a; v1 += c; }
       if (R2) { f32x4 a, c; ld8<T>(R2 + (long long)row * p.srr + col, a, c); v0 += a; v1 += c; }
       if (p.out_scale != 1.0f) { v0 *= p.out_scale; v1 *= p.out_scale; }
       st8<T>(Y + (long long)row * p.syr + col, v0, v1);

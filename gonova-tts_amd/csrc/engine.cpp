@@ -61,6 +61,11 @@ static bool mrf_fused_enabled() {
   const char* e = getenv("TTS_MRF_FUSED");
   return e ? atoi(e) != 0 : true;
 }
+// fused MRF flavour: pair kernels (default) or the whole-stage kernel (TTS_MRF_PAIR=0)
+static bool mrf_pair_enabled() {
+  const char* e = getenv("TTS_MRF_PAIR");
+  return e ? atoi(e) != 0 : true;
+}
 
 struct tts_engine {
   int device = 0;
@@ -266,6 +271,12 @@ struct tts_engine {
                                         pre + "convs1." + std::to_string(q) + ".bias", d, (ks * d - d) / 2, dt);
           v.mrf[i][j][q][1] = pack_conv(pre + "convs2." + std::to_string(q) + ".weight",
                                         pre + "convs2." + std::to_string(q) + ".bias", 1, (ks - 1) / 2, dt);
+          // pair-kernel copies (C in {32, 64}, 16-bit): 16x16 fragment-packed
+          for (int cv = 0; cv < 2; ++cv) {
+            const HostTensor& cw = get(pre + (cv ? "convs2." : "convs1.") + std::to_string(q) + ".weight");
+            if (mrf_pair_supported(dt, ch, ks) && cw.shape[0] == ch && cw.shape[1] == ch)
+              v.mrf[i][j][q][cv].wpk16 = frag_pack16(cw.data, ch, ks, dt, allocs);
+          }
         }
       }
       prepare_fused_stage(i, nk, dt);
@@ -376,6 +387,44 @@ struct tts_engine {
       run_conv(v.ups[i], S, (long long)Tin * cin, cin, Lp(i), Tin, XS, sb, ch, Up(i), Tin + 1, slope,
                nullptr, nullptr, 0, 0, 1.f, B, Lp(i + 1), dt, s);
       const int nk = (int)v.mrf[i].size();
+      bool pair_ok = mrf_fused_enabled() && mrf_pair_enabled();
+      for (int j = 0; j < nk && pair_ok; ++j)
+        for (const auto& pr : v.mrf[i][j]) pair_ok = pair_ok && pr[0].wpk16 && pr[1].wpk16;
+      if (pair_ok) {
+        // 9 pair launches: X -> HA -> HB -> S per resblock; S accumulates over resblocks
+        for (int j = 0; j < nk; ++j) {
+          const auto& blk = v.mrf[i][j];
+          const int np = (int)blk.size();
+          const void* h = XS;
+          for (int q = 0; q < np; ++q) {
+            const bool last = q == np - 1;
+            MrfPairParams pp{};
+            pp.x = h;
+            pp.y = last ? S : (q % 2 == 0 ? HA : HB);
+            pp.len = Lp(i + 1);
+            pp.w1 = blk[q][0].wpk16; pp.w2 = blk[q][1].wpk16;
+            pp.b1 = blk[q][0].bias; pp.b2 = blk[q][1].bias;
+            pp.T = Tout; pp.B = B; pp.k = blk[q][0].taps; pp.d = blk[q][0].dil;
+            pp.slope = slope;
+            pp.accum = (last && j > 0) ? 1 : 0;
+            pp.scale = (last && j == nk - 1) ? 1.0f / (float)nk : 1.f;
+            const double fl = 2.0 * 2.0 * ch * (double)ch * pp.k * (double)B * Tout;
+            if (prof.on) {
+              Profiler::Rec r{prof.get(), prof.get(), fl, PK_MRF_PAIR};
+              HIP_CHECK(hipEventRecord(r.a, s));
+              HIP_CHECK(mrf_pair_launch(dt, ch, pp, s));
+              HIP_CHECK(hipEventRecord(r.b, s));
+              prof.recs.push_back(r);
+            } else {
+              HIP_CHECK(mrf_pair_launch(dt, ch, pp, s));
+            }
+            h = pp.y;
+          }
+        }
+        Tin = Tout;
+        cin = ch;
+        continue;
+      }
       if (mrf_fused_enabled() && i < (int)v.has_fused.size() && v.has_fused[i]) {
         MrfParams mp = v.fused[i];
         mp.x = XS; mp.s = S; mp.len = Lp(i + 1); mp.T = Tout; mp.B = B;

@@ -38,7 +38,7 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why);
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s);
 
 // kernel family a launch runs as (live profiling buckets; tts_engine_profile_read_kinds)
-enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_MRF_FUSED = 2, PK_N = 3 };
+enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_MRF_FUSED = 2, PK_MRF_PAIR = 3, PK_N = 4 };
 int conv_gemm_kind(int dtype, const ConvParams& p);
 
 // Fused MRF stage (mrf_fused.hip): all resblocks of one HiFi-GAN stage in one launch.
@@ -63,6 +63,23 @@ struct MrfParams {
   float slope, out_scale;
   int rp;             // LDS rows per activation buffer
 };
+// Fused ResBlock pair (mrf_pair.hip): t = lrelu(conv_{k,d}(lrelu(h)) + b1);
+// h' = conv_{k,1}(t) + b2 + h;  y = ((accum ? y : 0) + h') * scale.
+struct MrfPairParams {
+  const void* x;      // [B][T][C] pair input h, compute dtype
+  void* y;            // [B][T][C] h' (accum = 0) or the MRF sum S (accum = 1); never aliases x
+  const int* len;     // per-utterance valid rows
+  const void* w1;     // conv1 / conv2 weights, 16x16 fragment-packed (frag_pack16)
+  const void* w2;
+  const float* b1;    // fp32 [C]
+  const float* b2;
+  int T, B, k, d;
+  float slope, scale;
+  int accum;
+};
+bool mrf_pair_supported(int dtype, int C, int k);
+hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s);
+
 int mrf_fused_taps_per_group(int C);
 int mrf_fused_bn(int C);
 hipError_t mrf_fused_launch(int dtype, int C, const MrfParams& p, hipStream_t s);

@@ -1,0 +1,311 @@
+// Fused HiFi-GAN ResBlock pair, one launch per (dilation) pair of an MRF stage:
+//
+//   t  = lrelu( conv_{k,d}( lrelu(h) ) + b1 )          (oracle: vocoder.resblock, one q)
+//   h' = conv_{k,1}( t ) + b2 + h
+//   out = h'                      (accum = 0)       next pair's input
+//   S   = (S + h') * scale        (accum = 1)       MRF sum over resblocks (scale 1/3 last)
+//
+// A block owns BN output rows.  It stages its input tile once from HBM as g = lrelu(h)
+// (rows n0-a1-a2 .. n0+BN+a1+a2, a1 = d(k-1)/2, a2 = (k-1)/2; zero outside the utterance)
+// in LDS, computes t for the BN + 2*a2 rows conv2 needs into LDS, then conv2 for the BN
+// output rows, recovering the residual h from g (LeakyReLU is invertible).  HBM traffic
+// per pair: read h once (+ halo, mostly L2), write h' once (S: read + write).
+//
+// Why pairs, not whole stages (mrf_fused.hip): a whole-stage tile must carry the
+// receptive-field halo of all three pairs of a resblock (60 rows per side at k=11) and
+// recompute it in every conv -- 55 % (C=64, BN=256) / 71 % (C=32, BN=512) of the issued
+// MFMA work was useful.  A pair recomputes only conv1's 2*a2 <= 10 extra rows (~95 %),
+// for one extra HBM round trip per pair, which at C <= 64 is cheaper than the halo.
+//
+// MFMA: v_mfma_f32_16x16x32_{f16,bf16}, M = output channels (2 x 16 per wave), N = time
+// rows in 16-row tiles (fine tiles keep the 8 or 9 + 1 conv1 tiles per wave balanced),
+// K = taps x C.  Weights are fragment-packed on the host (frag_pack16, runtime.h) so each
+// wave's A fragment is one contiguous 1 KiB load, streamed through a 6-step register ring
+// (no barriers inside a conv).  Activation tiles use a padded row stride (C*2 + 16 bytes).
+// The output tile goes through LDS as fp32 and leaves as 16-byte row pieces.
+#include "common.h"
+#include "kernels.h"
+
+#include <algorithm>
+
+namespace tts {
+
+template <int C>
+struct PairGeom;
+template <>
+struct PairGeom<32> {
+  static constexpr int BN = 256, WM = 1, WN = 4, RS = 80;
+};
+template <>
+struct PairGeom<64> {
+  static constexpr int BN = 128, WM = 2, WN = 2, RS = 144;
+};
+
+template <typename T>
+struct Mfma16;
+template <>
+struct Mfma16<half_t> {
+  __device__ static inline f32x4 mma(half8 a, half8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+template <>
+struct Mfma16<bf16_t> {
+  __device__ static inline f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+constexpr int PAIR_D = 6;        // weight ring depth (k-steps)
+constexpr int PAIR_KMAX = 17;    // 2*a2 <= 16 keeps conv1 within NU2 + 1 tiles per wave
+
+template <typename T>
+__device__ inline void pair_ld8(const T* p, f32x4& a, f32x4& b) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const T* e = reinterpret_cast<const T*>(&u);
+  a = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
+  b = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
+}
+template <typename T>
+__device__ inline void pair_st8(T* p, f32x4 a, f32x4 b) {
+  T e[8] = {(T)a[0], (T)a[1], (T)a[2], (T)a[3], (T)b[0], (T)b[1], (T)b[2], (T)b[3]};
+  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(e);
+}
+
+// LDS bytes of one launch (G tile incl. conv1 overrun rows, T tile; >= fp32 output tile)
+template <int C>
+static size_t pair_lds_bytes(int k, int d) {
+  using G = PairGeom<C>;
+  const int a1 = (k - 1) / 2 * d, a2 = (k - 1) / 2;
+  const int nt1 = (G::BN + 2 * a2 + 15) / 16;
+  const size_t g = (size_t)(16 * nt1 + 2 * a1) * G::RS;
+  const size_t t = (size_t)16 * nt1 * G::RS;
+  return std::max(g + t, (size_t)G::BN * (C * 4 + 16));
+}
+
+template <typename T, int C>
+__global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
+  using G = PairGeom<C>;
+  using MF = Mfma16<T>;
+  typedef typename Mfma<T>::frag Frag;
+  constexpr int BN = G::BN, WM = G::WM, WN = G::WN, RS = G::RS;
+  constexpr int NTHR = 256;
+  constexpr int KS = C / 32;           // k-steps (of 32 channels) per tap
+  constexpr int MT = 2;                // 16-channel M tiles per wave
+  constexpr int NU2 = BN / 16 / WN;    // conv2 tiles per wave
+  constexpr int NU1 = NU2 + 1;         // conv1 tiles per wave (upper bound)
+  constexpr int VPR = C / 8;           // 16-byte pieces per row
+  constexpr int YS = C * 4 + 16;       // fp32 output staging row stride
+  static_assert(WM * WN * 64 == NTHR && WM * 32 == C, "wave grid");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int b = blockIdx.y;
+  const int n0 = blockIdx.x * BN;
+  const int len = min(p.len[b], p.T);
+  if (n0 >= len) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int l15 = lane & 15, lq = lane >> 4;
+  const int k = p.k, d = p.d;
+  const int a2 = (k - 1) / 2, a1 = a2 * d;
+  const int RG = BN + 2 * (a1 + a2);
+  const int RT = BN + 2 * a2;
+  const int NT1 = (RT + 15) / 16;
+  const int nu1 = NT1 > wn ? (NT1 - wn + WN - 1) / WN : 0;
+  const int S = k * KS;                // k-steps per conv
+  char* Gs = smem;
+  char* Ts = smem + (16 * NT1 + 2 * a1) * RS;
+  const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
+  const float slope = p.slope, inv_slope = 1.0f / p.slope;
+  const int ch0 = 32 * wm + 4 * lq;    // + 16*mt: this lane's 4 output channels
+
+  // weights: [C/16][k][KS][64][8] -> step s = tap*KS + ks of m-tile mb at (mb*S + s) KiB
+  const char* w1 = reinterpret_cast<const char*>(p.w1) + (long long)(2 * wm) * S * 1024 + lane * 16;
+  const char* w2 = reinterpret_cast<const char*>(p.w2) + (long long)(2 * wm) * S * 1024 + lane * 16;
+  Frag ring[PAIR_D][MT];
+#define TTS_PLOAD(W_, SLOT_, S_)                                                          \
+  _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_)                                    \
+    ring[SLOT_][mt_] = *reinterpret_cast<const Frag*>((W_) + ((long long)mt_ * S + (S_)) * 1024);
+#pragma unroll
+  for (int i = 0; i < PAIR_D; ++i)
+    if (i < S) { TTS_PLOAD(w1, i, i) }
+
+  // ---- stage g = lrelu(h) (zero outside the utterance) ----
+  {
+    const int cc = tid % VPR, r0 = tid / VPR;
+    constexpr int rstep = NTHR / VPR;
+    const int gs = n0 - a1 - a2;
+    const T* xc = X + cc * 8;
+    for (int rb = r0; rb < RG; rb += 4 * rstep) {
+      uint4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int gr = min(max(gs + min(rb + i * rstep, RG - 1), 0), len - 1);
+        v[i] = *reinterpret_cast<const uint4*>(xc + (long long)gr * C);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = rb + i * rstep;
+        if (r < RG) {
+          const int gr = gs + r;
+          *reinterpret_cast<uint4*>(Gs + r * RS + cc * 16) =
+              (gr >= 0 && gr < len) ? lrelu_chunk<T>(v[i], slope) : uint4{0u, 0u, 0u, 0u};
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- conv1 over T rows [0, 16*NT1): T row t <-> global row n0 - a2 + t ----
+  f32x4 acc1[NU1][MT];
+#pragma unroll
+  for (int u = 0; u < NU1; ++u)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = f32x4{};
+  {
+    const char* gb = Gs + (16 * wn + l15) * RS + lq * 16;
+    for (int s0 = 0; s0 < S; s0 += PAIR_D) {
+#pragma unroll
+      for (int i = 0; i < PAIR_D; ++i) {
+        const int s = s0 + i;
+        if (s < S) {
+          const int tap = KS == 1 ? s : s / KS, ks = KS == 1 ? 0 : s % KS;
+          const char* bp = gb + tap * d * RS + ks * 64;
+          Frag bf[NU1];
+#pragma unroll
+          for (int u = 0; u < NU1; ++u)
+            if (u < nu1) bf[u] = *reinterpret_cast<const Frag*>(bp + u * (16 * WN) * RS);
+#pragma unroll
+          for (int u = 0; u < NU1; ++u)
+            if (u < nu1) {
+#pragma unroll
+              for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = MF::mma(ring[i][mt], bf[u], acc1[u][mt]);
+            }
+          if (s + PAIR_D < S) { TTS_PLOAD(w1, i, s + PAIR_D) }
+        }
+      }
+    }
+  }
+  // conv2's first weight steps in flight during the conv1 epilogue
+#pragma unroll
+  for (int i = 0; i < PAIR_D; ++i)
+    if (i < S) { TTS_PLOAD(w2, i, i) }
+  {
+    f32x4 bias[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b1 + ch0 + 16 * mt);
+#pragma unroll
+    for (int u = 0; u < NU1; ++u)
+      if (u < nu1) {
+        const int tr = 16 * (wn + WN * u) + l15;
+        const int gr = n0 - a2 + tr;
+        const bool valid = gr >= 0 && gr < len;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          f32x4 v = acc1[u][mt] + bias[mt];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = leaky(v[e], slope);
+          if (!valid) v = f32x4{};
+          Vec4<T>::store(reinterpret_cast<T*>(Ts + tr * RS + (ch0 + 16 * mt) * 2), v);
+        }
+      }
+  }
+  __syncthreads();
+
+  // ---- conv2 over the BN output rows: output row o reads T rows o .. o + 2*a2 ----
+  f32x4 acc2[NU2][MT];
+#pragma unroll
+  for (int u = 0; u < NU2; ++u)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = f32x4{};
+  {
+    const char* tb = Ts + (16 * wn + l15) * RS + lq * 16;
+    for (int s0 = 0; s0 < S; s0 += PAIR_D) {
+#pragma unroll
+      for (int i = 0; i < PAIR_D; ++i) {
+        const int s = s0 + i;
+        if (s < S) {
+          const int tap = KS == 1 ? s : s / KS, ks = KS == 1 ? 0 : s % KS;
+          const char* bp = tb + tap * RS + ks * 64;
+          Frag bf[NU2];
+#pragma unroll
+          for (int u = 0; u < NU2; ++u) bf[u] = *reinterpret_cast<const Frag*>(bp + u * (16 * WN) * RS);
+#pragma unroll
+          for (int u = 0; u < NU2; ++u)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = MF::mma(ring[i][mt], bf[u], acc2[u][mt]);
+          if (s + PAIR_D < S) { TTS_PLOAD(w2, i, s + PAIR_D) }
+        }
+      }
+    }
+  }
+#undef TTS_PLOAD
+  // y = acc + b2 + h, h = inverse lrelu of the staged g
+  {
+    f32x4 bias[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2 + ch0 + 16 * mt);
+#pragma unroll
+    for (int u = 0; u < NU2; ++u) {
+      const int o = 16 * (wn + WN * u) + l15;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x4 g = Vec4<T>::load(reinterpret_cast<const T*>(Gs + (o + a1 + a2) * RS + (ch0 + 16 * mt) * 2));
+        f32x4 v = acc2[u][mt] + bias[mt];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += g[e] >= 0.f ? g[e] : g[e] * inv_slope;
+        acc2[u][mt] = v;
+      }
+    }
+  }
+  __syncthreads();  // G / T no longer read: reuse LDS for the fp32 output tile
+#pragma unroll
+  for (int u = 0; u < NU2; ++u) {
+    const int o = 16 * (wn + WN * u) + l15;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<f32x4*>(smem + o * YS + (ch0 + 16 * mt) * 4) = acc2[u][mt];
+  }
+  __syncthreads();
+  T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
+#pragma unroll
+  for (int it = 0; it < BN * VPR / NTHR; ++it) {
+    const int idx = tid + it * NTHR;
+    const int o = idx / VPR, c8 = idx % VPR;
+    const int gr = n0 + o;
+    if (gr >= len) continue;
+    f32x4 v0 = *reinterpret_cast<const f32x4*>(smem + o * YS + c8 * 32);
+    f32x4 v1 = *reinterpret_cast<const f32x4*>(smem + o * YS + c8 * 32 + 16);
+    T* dst = Y + (long long)gr * C + c8 * 8;
+    if (p.accum) {
+      f32x4 a, c;
+      pair_ld8<T>(dst, a, c);
+      v0 += a; v1 += c;
+    }
+    if (p.scale != 1.0f) { v0 *= p.scale; v1 *= p.scale; }
+    pair_st8<T>(dst, v0, v1);
+  }
+}
+
+template <typename T, int C>
+static hipError_t launch_pair_t(const MrfPairParams& p, hipStream_t s) {
+  using G = PairGeom<C>;
+  const size_t lds = pair_lds_bytes<C>(p.k, p.d);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  dim3 grid((p.T + G::BN - 1) / G::BN, p.B);
+  hipLaunchKernelGGL((mrf_pair_kernel<T, C>), grid, dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+bool mrf_pair_supported(int dtype, int C, int k) {
+  return (dtype == DT_F16 || dtype == DT_BF16) && (C == 32 || C == 64) && k >= 1 && k % 2 == 1 && k <= PAIR_KMAX;
+}
+
+hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s) {
+  if (!mrf_pair_supported(dtype, C, p.k) || p.d < 1) return hipErrorInvalidValue;
+  if (dtype == DT_F16) return C == 32 ? launch_pair_t<half_t, 32>(p, s) : launch_pair_t<half_t, 64>(p, s);
+  return C == 32 ? launch_pair_t<bf16_t, 32>(p, s) : launch_pair_t<bf16_t, 64>(p, s);
+}
+
+}  // namespace tts

@@ -63,7 +63,8 @@ inline float* upload_f32(const std::vector<float>& h) { return (float*)upload(h,
 // A packed implicit-GEMM conv layer: W[M][taps][Cin] in the compute dtype, bias fp32 [M].
 struct ConvLayer {
   void* w = nullptr;
-  void* wpk = nullptr;  // fragment-packed copy (frag_pack), or null
+  void* wpk = nullptr;    // fragment-packed copy (frag_pack), or null
+  void* wpk16 = nullptr;  // 16x16 fragment-packed copy (frag_pack16, MRF convs at C <= 64), or null
   float* bias = nullptr;
   int M = 0, Cin = 0, taps = 1, dil = 1, pad = 0;
   int up_s = 0, up_cout = 0, up_p = 0;  // transposed-conv output mapping
@@ -86,6 +87,25 @@ inline void* frag_pack(const std::vector<float>& w, int M, int taps, int ci, int
           const int m = mb * 32 + (l & 31);
           for (int j = 0; j < 8; ++j, ++o)
             if (m < M) p[o] = w[((size_t)m * taps + t) * ci + ks * 16 + 8 * (l >> 5) + j];
+        }
+  void* d = upload(p, dt);
+  allocs.push_back(d);
+  return d;
+}
+
+// 16x16 fragment packing for mrf_pair_kernel: nn.Conv1d weight [C][C][k] (host fp32) ->
+//   P[C/16][k][C/32][lane 0..63][8],  lane l holding output channel 16*mb + (l & 15),
+//   input channels 32*ks + 8*(l >> 4) + [0, 8)  (the A operand of v_mfma_f32_16x16x32_*).
+inline void* frag_pack16(const std::vector<float>& w, int C, int k, int dt, std::vector<void*>& allocs) {
+  if (dt == DT_F32 || C % 32) return nullptr;
+  std::vector<float> p((size_t)C * C * k);
+  size_t o = 0;
+  for (int mb = 0; mb < C / 16; ++mb)
+    for (int t = 0; t < k; ++t)
+      for (int ks = 0; ks < C / 32; ++ks)
+        for (int l = 0; l < 64; ++l) {
+          const int m = mb * 16 + (l & 15);
+          for (int j = 0; j < 8; ++j, ++o) p[o] = w[((size_t)m * C + ks * 32 + 8 * (l >> 4) + j) * k + t];
         }
   void* d = upload(p, dt);
   allocs.push_back(d);

@@ -153,15 +153,18 @@ def test_vocoder_full_size_batch_invariance(vw):
     assert rel_rms(got, ref) <= 5e-3
 
 
+@pytest.mark.parametrize("pair", ["1", "0"], ids=["pair", "stage"])
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-def test_fused_mrf_matches_unfused_path(vw, dtype, monkeypatch):
-    """The fused MRF stage kernel (stages with C=64/32) against the per-conv path on ragged input."""
+def test_fused_mrf_matches_unfused_path(vw, dtype, pair, monkeypatch):
+    """The fused MRF kernels of the C=64/32 stages -- ResBlock-pair kernels (default) and the
+    whole-stage kernel (TTS_MRF_PAIR=0) -- against the per-conv path on ragged input."""
     eng = engine_for(dtype, vw)
     rng = np.random.default_rng(21)
     lens = [70, 3, 41, 66]
     mel = torch.from_numpy(rng.standard_normal((4, 70, 80)).astype(np.float32)).to(DEV)
     ln = torch.tensor(lens, dtype=torch.int32)
     monkeypatch.setenv("TTS_MRF_FUSED", "1")
+    monkeypatch.setenv("TTS_MRF_PAIR", pair)
     fused = eng.vocoder(mel, ln).cpu().numpy()
     monkeypatch.setenv("TTS_MRF_FUSED", "0")
     unfused = eng.vocoder(mel, ln).cpu().numpy()

@@ -3,7 +3,7 @@ import csv
 import sys
 
 rows = [r for r in csv.DictReader(open(sys.argv[1]))
-        if any(k in r["Kernel_Name"] for k in ("mrf_fused", "conv_gemm", "conv_xres", "conv_post"))]
+        if any(k in r["Kernel_Name"] for k in ("mrf_fused", "mrf_pair", "conv_gemm", "conv_xres", "conv_post"))]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # a step ends with conv_post
 ends = [i for i, r in enumerate(rows) if "conv_post" in r["Kernel_Name"]]

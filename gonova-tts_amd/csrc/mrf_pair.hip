@@ -21,7 +21,7 @@
 // rows in 16-row tiles (fine tiles keep the 8 or 9 + 1 conv1 tiles per wave balanced),
 // K = taps x C.  Weights are fragment-packed on the host (frag_pack16, runtime.h) so each
 // wave's A fragment is one contiguous 1 KiB load, streamed through a 6-step register ring
-// (no barriers inside a conv).  Activation tiles use a padded row stride (C*2 + 16 bytes).
+// (no barriers inside a conv).  Activation tiles are XOR-swizzled (PairGeom).
 // The output tile goes through LDS as fp32 and leaves as 16-byte row pieces.
 #include "common.h"
 #include "kernels.h"
@@ -32,13 +32,20 @@ namespace tts {
 
 template <int C>
 struct PairGeom;
+// Activation tiles in LDS: unpadded rows (RS = C*2 bytes), 16-byte chunk c of row r stored
+// at chunk c ^ ((r >> SW_S) & SW_M).  Chosen with an LDS bank model of every access
+// (MI355X_MICROARCH.md §LDS lane groups): the MFMA B-fragment ds_read_b128 (16 rows x 4
+// chunks per lane group) and the staging ds_write_b128 are conflict-free; the once-per-tile
+// 8-byte epilogue accesses are 2-way.  (Padded rows of 80/144 B made the B reads 2-way:
+// measured 43-47 % of LDS cycles were bank conflicts.)  The swizzle depends on r mod 8
+// only, so it is shared by every 16-row tile and computed once per tap.
 template <>
 struct PairGeom<32> {
-  static constexpr int BN = 256, WM = 1, WN = 4, RS = 80;
+  static constexpr int BN = 256, WM = 1, WN = 4, RS = 64, SW_S = 1, SW_M = 3;
 };
 template <>
 struct PairGeom<64> {
-  static constexpr int BN = 128, WM = 2, WN = 2, RS = 144;
+  static constexpr int BN = 128, WM = 2, WN = 2, RS = 128, SW_S = 0, SW_M = 7;
 };
 
 template <typename T>
@@ -57,6 +64,7 @@ struct Mfma16<bf16_t> {
 };
 
 constexpr int PAIR_D = 6;        // weight ring depth (k-steps)
+constexpr int PAIR_SU = 8;       // input-tile loads in flight per thread (one round for every shape)
 constexpr int PAIR_KMAX = 17;    // 2*a2 <= 16 keeps conv1 within NU2 + 1 tiles per wave
 
 template <typename T>
@@ -65,6 +73,11 @@ __device__ inline void pair_ld8(const T* p, f32x4& a, f32x4& b) {
   const T* e = reinterpret_cast<const T*>(&u);
   a = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
   b = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
+}
+template <typename T>
+__device__ inline uint2 pack4(f32x4 v) {
+  T e[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
+  return *reinterpret_cast<const uint2*>(e);
 }
 template <typename T>
 __device__ inline void pair_st8(T* p, f32x4 a, f32x4 b) {
@@ -89,13 +102,15 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   using MF = Mfma16<T>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int BN = G::BN, WM = G::WM, WN = G::WN, RS = G::RS;
+  auto swz = [](int r) { return (r >> G::SW_S) & G::SW_M; };  // chunk XOR of row r
   constexpr int NTHR = 256;
   constexpr int KS = C / 32;           // k-steps (of 32 channels) per tap
   constexpr int MT = 2;                // 16-channel M tiles per wave
   constexpr int NU2 = BN / 16 / WN;    // conv2 tiles per wave
   constexpr int NU1 = NU2 + 1;         // conv1 tiles per wave (upper bound)
   constexpr int VPR = C / 8;           // 16-byte pieces per row
-  constexpr int YS = C * 4 + 16;       // fp32 output staging row stride
+  constexpr int YS = C * 4 + 16;       // fp32 output staging row stride (accumulating launches)
+  constexpr int YS16 = C * 2 + 16;     // compute-dtype output staging row stride (plain launches)
   static_assert(WM * WN * 64 == NTHR && WM * 32 == C, "wave grid");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -138,19 +153,32 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     constexpr int rstep = NTHR / VPR;
     const int gs = n0 - a1 - a2;
     const T* xc = X + cc * 8;
-    for (int rb = r0; rb < RG; rb += 4 * rstep) {
-      uint4 v[4];
+    if (gs >= 0 && gs + RG <= len) {  // interior tile: no clamps, no masks
+      for (int rb = r0; rb < RG; rb += PAIR_SU * rstep) {
+        uint4 v[PAIR_SU];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < PAIR_SU; ++i)
+          v[i] = *reinterpret_cast<const uint4*>(xc + (long long)(gs + min(rb + i * rstep, RG - 1)) * C);
+#pragma unroll
+        for (int i = 0; i < PAIR_SU; ++i) {
+          const int r = rb + i * rstep;
+          if (r < RG) *reinterpret_cast<uint4*>(Gs + r * RS + (cc ^ swz(r)) * 16) = lrelu_chunk<T>(v[i], slope);
+        }
+      }
+    } else
+    for (int rb = r0; rb < RG; rb += PAIR_SU * rstep) {
+      uint4 v[PAIR_SU];
+#pragma unroll
+      for (int i = 0; i < PAIR_SU; ++i) {
         const int gr = min(max(gs + min(rb + i * rstep, RG - 1), 0), len - 1);
         v[i] = *reinterpret_cast<const uint4*>(xc + (long long)gr * C);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < PAIR_SU; ++i) {
         const int r = rb + i * rstep;
         if (r < RG) {
           const int gr = gs + r;
-          *reinterpret_cast<uint4*>(Gs + r * RS + cc * 16) =
+          *reinterpret_cast<uint4*>(Gs + r * RS + (cc ^ swz(r)) * 16) =
               (gr >= 0 && gr < len) ? lrelu_chunk<T>(v[i], slope) : uint4{0u, 0u, 0u, 0u};
         }
       }
@@ -165,14 +193,14 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = f32x4{};
   {
-    const char* gb = Gs + (16 * wn + l15) * RS + lq * 16;
+    const char* gb = Gs + (16 * wn + l15) * RS;
     for (int s0 = 0; s0 < S; s0 += PAIR_D) {
 #pragma unroll
       for (int i = 0; i < PAIR_D; ++i) {
         const int s = s0 + i;
         if (s < S) {
           const int tap = KS == 1 ? s : s / KS, ks = KS == 1 ? 0 : s % KS;
-          const char* bp = gb + tap * d * RS + ks * 64;
+          const char* bp = gb + tap * d * RS + ((lq + 4 * ks) ^ swz(l15 + tap * d)) * 16;
           Frag bf[NU1];
 #pragma unroll
           for (int u = 0; u < NU1; ++u)
@@ -206,13 +234,28 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
         for (int mt = 0; mt < MT; ++mt) {
           f32x4 v = acc1[u][mt] + bias[mt];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = leaky(v[e], slope);
-          if (!valid) v = f32x4{};
-          Vec4<T>::store(reinterpret_cast<T*>(Ts + tr * RS + (ch0 + 16 * mt) * 2), v);
+          for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaxf(v[e], v[e] * slope);  // lrelu, 0 <= slope <= 1
+          uint2 pk = pack4<T>(v);
+          if (!valid) pk = uint2{0u, 0u};
+          const int cb = (ch0 + 16 * mt) * 2;  // byte offset in the row
+          *reinterpret_cast<uint2*>(Ts + tr * RS + (((cb >> 4) ^ swz(tr)) << 4) + (cb & 15)) = pk;
         }
       }
   }
   __syncthreads();
+
+  // the MRF sum rows this thread will accumulate into, in flight during conv2
+  constexpr int NIT = BN * VPR / NTHR;
+  T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
+  uint4 sprev[NIT];
+  if (p.accum) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NTHR;
+      const int gr = min(n0 + idx / VPR, len - 1);
+      sprev[it] = *reinterpret_cast<const uint4*>(Y + (long long)gr * C + (idx % VPR) * 8);
+    }
+  }
 
   // ---- conv2 over the BN output rows: output row o reads T rows o .. o + 2*a2 ----
   f32x4 acc2[NU2][MT];
@@ -221,14 +264,14 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = f32x4{};
   {
-    const char* tb = Ts + (16 * wn + l15) * RS + lq * 16;
+    const char* tb = Ts + (16 * wn + l15) * RS;
     for (int s0 = 0; s0 < S; s0 += PAIR_D) {
 #pragma unroll
       for (int i = 0; i < PAIR_D; ++i) {
         const int s = s0 + i;
         if (s < S) {
           const int tap = KS == 1 ? s : s / KS, ks = KS == 1 ? 0 : s % KS;
-          const char* bp = tb + tap * RS + ks * 64;
+          const char* bp = tb + tap * RS + ((lq + 4 * ks) ^ swz(l15 + tap)) * 16;
           Frag bf[NU2];
 #pragma unroll
           for (int u = 0; u < NU2; ++u) bf[u] = *reinterpret_cast<const Frag*>(bp + u * (16 * WN) * RS);
@@ -252,15 +295,40 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
       const int o = 16 * (wn + WN * u) + l15;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const f32x4 g = Vec4<T>::load(reinterpret_cast<const T*>(Gs + (o + a1 + a2) * RS + (ch0 + 16 * mt) * 2));
+        const int gr = o + a1 + a2, cb = (ch0 + 16 * mt) * 2;
+        const f32x4 g = Vec4<T>::load(reinterpret_cast<const T*>(Gs + gr * RS + (((cb >> 4) ^ swz(gr)) << 4) + (cb & 15)));
         f32x4 v = acc2[u][mt] + bias[mt];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += g[e] >= 0.f ? g[e] : g[e] * inv_slope;
+        for (int e = 0; e < 4; ++e) v[e] += __builtin_fminf(g[e], g[e] * inv_slope);  // h = lrelu^-1(g)
         acc2[u][mt] = v;
       }
     }
   }
-  __syncthreads();  // G / T no longer read: reuse LDS for the fp32 output tile
+  __syncthreads();  // G / T no longer read: reuse LDS for the output tile
+  if (!p.accum) {
+    // plain output (the next pair's input): final values in the compute dtype, staged as
+    // such; the row pass is then a 16-byte copy
+#pragma unroll
+    for (int u = 0; u < NU2; ++u) {
+      const int o = 16 * (wn + WN * u) + l15;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        f32x4 v = acc2[u][mt];
+        if (p.scale != 1.0f) v *= p.scale;
+        *reinterpret_cast<uint2*>(smem + o * YS16 + (ch0 + 16 * mt) * 2) = pack4<T>(v);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NTHR;
+      const int o = idx / VPR, c8 = idx % VPR;
+      const int gr = n0 + o;
+      if (gr < len)
+        *reinterpret_cast<uint4*>(Y + (long long)gr * C + c8 * 8) = *reinterpret_cast<const uint4*>(smem + o * YS16 + c8 * 16);
+    }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < NU2; ++u) {
     const int o = 16 * (wn + WN * u) + l15;
@@ -268,9 +336,8 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<f32x4*>(smem + o * YS + (ch0 + 16 * mt) * 4) = acc2[u][mt];
   }
   __syncthreads();
-  T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
 #pragma unroll
-  for (int it = 0; it < BN * VPR / NTHR; ++it) {
+  for (int it = 0; it < NIT; ++it) {
     const int idx = tid + it * NTHR;
     const int o = idx / VPR, c8 = idx % VPR;
     const int gr = n0 + o;
@@ -278,9 +345,9 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     f32x4 v0 = *reinterpret_cast<const f32x4*>(smem + o * YS + c8 * 32);
     f32x4 v1 = *reinterpret_cast<const f32x4*>(smem + o * YS + c8 * 32 + 16);
     T* dst = Y + (long long)gr * C + c8 * 8;
-    if (p.accum) {
+    {
       f32x4 a, c;
-      pair_ld8<T>(dst, a, c);
+      pair_ld8<T>(reinterpret_cast<const T*>(&sprev[it]), a, c);
       v0 += a; v1 += c;
     }
     if (p.scale != 1.0f) { v0 *= p.scale; v1 *= p.scale; }

@@ -39,13 +39,26 @@ struct PairGeom;
 // 8-byte epilogue accesses are 2-way.  (Padded rows of 80/144 B made the B reads 2-way:
 // measured 43-47 % of LDS cycles were bank conflicts.)  The swizzle depends on r mod 8
 // only, so it is shared by every 16-row tile and computed once per tap.
+//
+// C = 128 (TOG, "T over G"): G and T do not both fit 3 blocks/CU at BN = 128, so conv1's
+// output T overwrites G after a barrier, and the residual h is re-read from the input rows
+// (L2-hot: this block just staged them) in the row pass instead of being recovered from g.
+// 256-byte rows are one LDS bank row each; chunk ^ ((2r) & 15) keeps the B reads
+// conflict-free for every tap offset (exhaustive check over r mod 16).
 template <>
 struct PairGeom<32> {
-  static constexpr int BN = 256, WM = 1, WN = 4, RS = 64, SW_S = 1, SW_M = 3;
+  static constexpr int BN = 256, WM = 1, WN = 4, RS = 64, SW_MUL = 1, SW_S = 1, SW_M = 3, D = 6;
+  static constexpr bool TOG = false;
 };
 template <>
 struct PairGeom<64> {
-  static constexpr int BN = 128, WM = 2, WN = 2, RS = 128, SW_S = 0, SW_M = 7;
+  static constexpr int BN = 128, WM = 2, WN = 2, RS = 128, SW_MUL = 1, SW_S = 0, SW_M = 7, D = 6;
+  static constexpr bool TOG = false;
+};
+template <>
+struct PairGeom<128> {
+  static constexpr int BN = 128, WM = 4, WN = 1, RS = 256, SW_MUL = 2, SW_S = 0, SW_M = 15, D = 4;
+  static constexpr bool TOG = true;
 };
 
 template <typename T>
@@ -63,7 +76,6 @@ struct Mfma16<bf16_t> {
   }
 };
 
-constexpr int PAIR_D = 6;        // weight ring depth (k-steps)
 constexpr int PAIR_SU = 8;       // input-tile loads in flight per thread (one round for every shape)
 constexpr int PAIR_KMAX = 17;    // 2*a2 <= 16 keeps conv1 within NU2 + 1 tiles per wave
 
@@ -93,6 +105,7 @@ static size_t pair_lds_bytes(int k, int d) {
   const int nt1 = (G::BN + 2 * a2 + 15) / 16;
   const size_t g = (size_t)(16 * nt1 + 2 * a1) * G::RS;
   const size_t t = (size_t)16 * nt1 * G::RS;
+  if (G::TOG) return std::max(std::max(g, t), (size_t)G::BN * (C * 2 + 16));
   return std::max(g + t, (size_t)G::BN * (C * 4 + 16));
 }
 
@@ -102,7 +115,8 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   using MF = Mfma16<T>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int BN = G::BN, WM = G::WM, WN = G::WN, RS = G::RS;
-  auto swz = [](int r) { return (r >> G::SW_S) & G::SW_M; };  // chunk XOR of row r
+  constexpr int PAIR_D = G::D;         // weight ring depth (k-steps)
+  auto swz = [](int r) { return ((r * G::SW_MUL) >> G::SW_S) & G::SW_M; };  // chunk XOR of row r
   constexpr int NTHR = 256;
   constexpr int KS = C / 32;           // k-steps (of 32 channels) per tap
   constexpr int MT = 2;                // 16-channel M tiles per wave
@@ -112,6 +126,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   constexpr int YS = C * 4 + 16;       // fp32 output staging row stride (accumulating launches)
   constexpr int YS16 = C * 2 + 16;     // compute-dtype output staging row stride (plain launches)
   static_assert(WM * WN * 64 == NTHR && WM * 32 == C, "wave grid");
+  static_assert(NTHR % VPR == 0, "staging");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int b = blockIdx.y;
@@ -131,7 +146,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   const int nu1 = NT1 > wn ? (NT1 - wn + WN - 1) / WN : 0;
   const int S = k * KS;                // k-steps per conv
   char* Gs = smem;
-  char* Ts = smem + (16 * NT1 + 2 * a1) * RS;
+  char* Ts = G::TOG ? smem : smem + (16 * NT1 + 2 * a1) * RS;
   const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
   const float slope = p.slope, inv_slope = 1.0f / p.slope;
   const int ch0 = 32 * wm + 4 * lq;    // + 16*mt: this lane's 4 output channels
@@ -220,6 +235,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
 #pragma unroll
   for (int i = 0; i < PAIR_D; ++i)
     if (i < S) { TTS_PLOAD(w2, i, i) }
+  if constexpr (G::TOG) __syncthreads();  // T overwrites G: every wave is done reading it
   {
     f32x4 bias[MT];
 #pragma unroll
@@ -248,7 +264,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   constexpr int NIT = BN * VPR / NTHR;
   T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
   uint4 sprev[NIT];
-  if (p.accum) {
+  if (p.accum && !G::TOG) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int idx = tid + it * NTHR;
@@ -285,6 +301,47 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     }
   }
 #undef TTS_PLOAD
+  if constexpr (G::TOG) {
+    // residual h (input rows) in flight while the tile is staged (the MRF-sum rows of
+    // accumulating launches are read in the row pass: prefetching both spills)
+    uint4 xin[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NTHR;
+      xin[it] = *reinterpret_cast<const uint4*>(X + (long long)min(n0 + idx / VPR, len - 1) * C + (idx % VPR) * 8);
+    }
+    f32x4 bias[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2 + ch0 + 16 * mt);
+    __syncthreads();  // T no longer read
+#pragma unroll
+    for (int u = 0; u < NU2; ++u) {
+      const int o = 16 * (wn + WN * u) + l15;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        *reinterpret_cast<uint2*>(smem + o * YS16 + (ch0 + 16 * mt) * 2) = pack4<T>(acc2[u][mt] + bias[mt]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NTHR;
+      const int o = idx / VPR, c8 = idx % VPR;
+      const int gr = n0 + o;
+      if (gr >= len) continue;
+      f32x4 v0, v1, a, c;
+      pair_ld8<T>(reinterpret_cast<const T*>(smem + o * YS16 + c8 * 16), v0, v1);
+      pair_ld8<T>(reinterpret_cast<const T*>(&xin[it]), a, c);
+      v0 += a; v1 += c;
+      T* dst = Y + (long long)gr * C + c8 * 8;
+      if (p.accum) {
+        pair_ld8<T>(dst, a, c);
+        v0 += a; v1 += c;
+      }
+      if (p.scale != 1.0f) { v0 *= p.scale; v1 *= p.scale; }
+      pair_st8<T>(dst, v0, v1);
+    }
+    return;
+  }
   // y = acc + b2 + h, h = inverse lrelu of the staged g
   {
     f32x4 bias[MT];
@@ -366,13 +423,20 @@ static hipError_t launch_pair_t(const MrfPairParams& p, hipStream_t s) {
 }
 
 bool mrf_pair_supported(int dtype, int C, int k) {
-  return (dtype == DT_F16 || dtype == DT_BF16) && (C == 32 || C == 64) && k >= 1 && k % 2 == 1 && k <= PAIR_KMAX;
+  return (dtype == DT_F16 || dtype == DT_BF16) && (C == 32 || C == 64 || C == 128) && k >= 1 && k % 2 == 1 &&
+         k <= PAIR_KMAX;
 }
 
 hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s) {
   if (!mrf_pair_supported(dtype, C, p.k) || p.d < 1) return hipErrorInvalidValue;
-  if (dtype == DT_F16) return C == 32 ? launch_pair_t<half_t, 32>(p, s) : launch_pair_t<half_t, 64>(p, s);
-  return C == 32 ? launch_pair_t<bf16_t, 32>(p, s) : launch_pair_t<bf16_t, 64>(p, s);
+  if (dtype == DT_F16) {
+    if (C == 32) return launch_pair_t<half_t, 32>(p, s);
+    if (C == 64) return launch_pair_t<half_t, 64>(p, s);
+    return launch_pair_t<half_t, 128>(p, s);
+  }
+  if (C == 32) return launch_pair_t<bf16_t, 32>(p, s);
+  if (C == 64) return launch_pair_t<bf16_t, 64>(p, s);
+  return launch_pair_t<bf16_t, 128>(p, s);
 }
 
 }  // namespace tts

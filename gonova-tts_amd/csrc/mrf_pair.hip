@@ -7,22 +7,29 @@
 //
 // A block owns BN output rows.  It stages its input tile once from HBM as g = lrelu(h)
 // (rows n0-a1-a2 .. n0+BN+a1+a2, a1 = d(k-1)/2, a2 = (k-1)/2; zero outside the utterance)
-// in LDS, computes t for the BN + 2*a2 rows conv2 needs into LDS, then conv2 for the BN
-// output rows, recovering the residual h from g (LeakyReLU is invertible).  HBM traffic
-// per pair: read h once (+ halo, mostly L2), write h' once (S: read + write).
+// in LDS ("G"), computes conv1 for the BN + 2*a2 rows conv2 needs, writes t over G ("T",
+// after a barrier: both tiles at once would not leave 3 blocks per CU), runs conv2 for
+// the BN output rows, stages the output tile in LDS and leaves through 16-byte row pieces,
+// adding the residual h from the input rows (L2-hot: the block just staged them) and, for
+// the last pair of a resblock, the running MRF sum.  HBM traffic per pair: read h once
+// (+ halo, mostly L2), write h' once (S: read + write).
 //
-// Why pairs, not whole stages (mrf_fused.hip): a whole-stage tile must carry the
-// receptive-field halo of all three pairs of a resblock (60 rows per side at k=11) and
-// recompute it in every conv -- 55 % (C=64, BN=256) / 71 % (C=32, BN=512) of the issued
-// MFMA work was useful.  A pair recomputes only conv1's 2*a2 <= 10 extra rows (~95 %),
-// for one extra HBM round trip per pair, which at C <= 64 is cheaper than the halo.
+// Why pairs, not whole stages (mrf_fused.hip) or single convs (conv_xres): a whole-stage
+// tile must carry the receptive-field halo of all three pairs of a resblock (60 rows per
+// side at k=11) and recompute it in every conv -- 55 % (C=64) / 71 % (C=32) of its issued
+// MFMA work was useful; a pair recomputes only conv1's 2*a2 <= 10 extra rows.  Against two
+// single-conv launches a pair saves t's HBM round trip and the residual pass.
+//
+// Tile size: weights are streamed from L2 per block, so a block's L2 traffic is dominated
+// by its 2*k*C*C weight elements; BN = 512 / 256 / 128 rows at C = 32 / 64 / 128 keeps
+// that near 1.4 KB per row (measured: at BN = 128, C = 64 the L2 request rate sat at the
+// per-CU L2 limit).
 //
 // MFMA: v_mfma_f32_16x16x32_{f16,bf16}, M = output channels (2 x 16 per wave), N = time
-// rows in 16-row tiles (fine tiles keep the 8 or 9 + 1 conv1 tiles per wave balanced),
+// rows in 16-row tiles (fine tiles keep the 8 + 1 conv1 tiles per wave balanced),
 // K = taps x C.  Weights are fragment-packed on the host (frag_pack16, runtime.h) so each
-// wave's A fragment is one contiguous 1 KiB load, streamed through a 6-step register ring
+// wave's A fragment is one contiguous 1 KiB load, streamed through a 4-step register ring
 // (no barriers inside a conv).  Activation tiles are XOR-swizzled (PairGeom).
-// The output tile goes through LDS as fp32 and leaves as 16-byte row pieces.
 #include "common.h"
 #include "kernels.h"
 
@@ -33,32 +40,25 @@ namespace tts {
 template <int C>
 struct PairGeom;
 // Activation tiles in LDS: unpadded rows (RS = C*2 bytes), 16-byte chunk c of row r stored
-// at chunk c ^ ((r >> SW_S) & SW_M).  Chosen with an LDS bank model of every access
+// at chunk c ^ (((r * SW_MUL) >> SW_S) & SW_M).  Chosen with an LDS bank model of every access
 // (MI355X_MICROARCH.md §LDS lane groups): the MFMA B-fragment ds_read_b128 (16 rows x 4
 // chunks per lane group) and the staging ds_write_b128 are conflict-free; the once-per-tile
 // 8-byte epilogue accesses are 2-way.  (Padded rows of 80/144 B made the B reads 2-way:
 // measured 43-47 % of LDS cycles were bank conflicts.)  The swizzle depends on r mod 8
-// only, so it is shared by every 16-row tile and computed once per tap.
-//
-// C = 128 (TOG, "T over G"): G and T do not both fit 3 blocks/CU at BN = 128, so conv1's
-// output T overwrites G after a barrier, and the residual h is re-read from the input rows
-// (L2-hot: this block just staged them) in the row pass instead of being recovered from g.
+// only, so it is shared by every 16-row tile and computed once per tap.  At C = 128 the
 // 256-byte rows are one LDS bank row each; chunk ^ ((2r) & 15) keeps the B reads
 // conflict-free for every tap offset (exhaustive check over r mod 16).
 template <>
 struct PairGeom<32> {
-  static constexpr int BN = 256, WM = 1, WN = 4, RS = 64, SW_MUL = 1, SW_S = 1, SW_M = 3, D = 6;
-  static constexpr bool TOG = false;
+  static constexpr int BN = 512, WM = 1, WN = 4, RS = 64, SW_MUL = 1, SW_S = 1, SW_M = 3, D = 4;
 };
 template <>
 struct PairGeom<64> {
-  static constexpr int BN = 128, WM = 2, WN = 2, RS = 128, SW_MUL = 1, SW_S = 0, SW_M = 7, D = 6;
-  static constexpr bool TOG = false;
+  static constexpr int BN = 256, WM = 2, WN = 2, RS = 128, SW_MUL = 1, SW_S = 0, SW_M = 7, D = 4;
 };
 template <>
 struct PairGeom<128> {
   static constexpr int BN = 128, WM = 4, WN = 1, RS = 256, SW_MUL = 2, SW_S = 0, SW_M = 15, D = 4;
-  static constexpr bool TOG = true;
 };
 
 template <typename T>
@@ -105,8 +105,7 @@ static size_t pair_lds_bytes(int k, int d) {
   const int nt1 = (G::BN + 2 * a2 + 15) / 16;
   const size_t g = (size_t)(16 * nt1 + 2 * a1) * G::RS;
   const size_t t = (size_t)16 * nt1 * G::RS;
-  if (G::TOG) return std::max(std::max(g, t), (size_t)G::BN * (C * 2 + 16));
-  return std::max(g + t, (size_t)G::BN * (C * 4 + 16));
+  return std::max(std::max(g, t), (size_t)G::BN * (C * 2 + 16));
 }
 
 template <typename T, int C>
@@ -123,8 +122,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   constexpr int NU2 = BN / 16 / WN;    // conv2 tiles per wave
   constexpr int NU1 = NU2 + 1;         // conv1 tiles per wave (upper bound)
   constexpr int VPR = C / 8;           // 16-byte pieces per row
-  constexpr int YS = C * 4 + 16;       // fp32 output staging row stride (accumulating launches)
-  constexpr int YS16 = C * 2 + 16;     // compute-dtype output staging row stride (plain launches)
+  constexpr int YS16 = C * 2 + 16;     // output tile staging row stride
   static_assert(WM * WN * 64 == NTHR && WM * 32 == C, "wave grid");
   static_assert(NTHR % VPR == 0, "staging");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -146,9 +144,9 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   const int nu1 = NT1 > wn ? (NT1 - wn + WN - 1) / WN : 0;
   const int S = k * KS;                // k-steps per conv
   char* Gs = smem;
-  char* Ts = G::TOG ? smem : smem + (16 * NT1 + 2 * a1) * RS;
+  char* Ts = smem;                     // T overwrites G after conv1
   const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
-  const float slope = p.slope, inv_slope = 1.0f / p.slope;
+  const float slope = p.slope;
   const int ch0 = 32 * wm + 4 * lq;    // + 16*mt: this lane's 4 output channels
 
   // weights: [C/16][k][KS][64][8] -> step s = tap*KS + ks of m-tile mb at (mb*S + s) KiB
@@ -235,7 +233,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
 #pragma unroll
   for (int i = 0; i < PAIR_D; ++i)
     if (i < S) { TTS_PLOAD(w2, i, i) }
-  if constexpr (G::TOG) __syncthreads();  // T overwrites G: every wave is done reading it
+  __syncthreads();  // T overwrites G: every wave is done reading it
   {
     f32x4 bias[MT];
 #pragma unroll
@@ -260,18 +258,8 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   }
   __syncthreads();
 
-  // the MRF sum rows this thread will accumulate into, in flight during conv2
-  constexpr int NIT = BN * VPR / NTHR;
+  constexpr int NIT = BN * VPR / NTHR;  // 16-byte row pieces per thread in the row pass
   T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
-  uint4 sprev[NIT];
-  if (p.accum && !G::TOG) {
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int idx = tid + it * NTHR;
-      const int gr = min(n0 + idx / VPR, len - 1);
-      sprev[it] = *reinterpret_cast<const uint4*>(Y + (long long)gr * C + (idx % VPR) * 8);
-    }
-  }
 
   // ---- conv2 over the BN output rows: output row o reads T rows o .. o + 2*a2 ----
   f32x4 acc2[NU2][MT];
@@ -301,96 +289,24 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     }
   }
 #undef TTS_PLOAD
-  if constexpr (G::TOG) {
-    // residual h (input rows) in flight while the tile is staged (the MRF-sum rows of
-    // accumulating launches are read in the row pass: prefetching both spills)
-    uint4 xin[NIT];
+  // residual h (input rows) in flight while the tile is staged (the MRF-sum rows of
+  // accumulating launches are read in the row pass: prefetching both spills)
+  uint4 xin[NIT];
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int idx = tid + it * NTHR;
-      xin[it] = *reinterpret_cast<const uint4*>(X + (long long)min(n0 + idx / VPR, len - 1) * C + (idx % VPR) * 8);
-    }
-    f32x4 bias[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2 + ch0 + 16 * mt);
-    __syncthreads();  // T no longer read
-#pragma unroll
-    for (int u = 0; u < NU2; ++u) {
-      const int o = 16 * (wn + WN * u) + l15;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        *reinterpret_cast<uint2*>(smem + o * YS16 + (ch0 + 16 * mt) * 2) = pack4<T>(acc2[u][mt] + bias[mt]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int idx = tid + it * NTHR;
-      const int o = idx / VPR, c8 = idx % VPR;
-      const int gr = n0 + o;
-      if (gr >= len) continue;
-      f32x4 v0, v1, a, c;
-      pair_ld8<T>(reinterpret_cast<const T*>(smem + o * YS16 + c8 * 16), v0, v1);
-      pair_ld8<T>(reinterpret_cast<const T*>(&xin[it]), a, c);
-      v0 += a; v1 += c;
-      T* dst = Y + (long long)gr * C + c8 * 8;
-      if (p.accum) {
-        pair_ld8<T>(dst, a, c);
-        v0 += a; v1 += c;
-      }
-      if (p.scale != 1.0f) { v0 *= p.scale; v1 *= p.scale; }
-      pair_st8<T>(dst, v0, v1);
-    }
-    return;
+  for (int it = 0; it < NIT; ++it) {
+    const int idx = tid + it * NTHR;
+    xin[it] = *reinterpret_cast<const uint4*>(X + (long long)min(n0 + idx / VPR, len - 1) * C + (idx % VPR) * 8);
   }
-  // y = acc + b2 + h, h = inverse lrelu of the staged g
-  {
-    f32x4 bias[MT];
+  f32x4 bias[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2 + ch0 + 16 * mt);
-#pragma unroll
-    for (int u = 0; u < NU2; ++u) {
-      const int o = 16 * (wn + WN * u) + l15;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int gr = o + a1 + a2, cb = (ch0 + 16 * mt) * 2;
-        const f32x4 g = Vec4<T>::load(reinterpret_cast<const T*>(Gs + gr * RS + (((cb >> 4) ^ swz(gr)) << 4) + (cb & 15)));
-        f32x4 v = acc2[u][mt] + bias[mt];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += __builtin_fminf(g[e], g[e] * inv_slope);  // h = lrelu^-1(g)
-        acc2[u][mt] = v;
-      }
-    }
-  }
-  __syncthreads();  // G / T no longer read: reuse LDS for the output tile
-  if (!p.accum) {
-    // plain output (the next pair's input): final values in the compute dtype, staged as
-    // such; the row pass is then a 16-byte copy
-#pragma unroll
-    for (int u = 0; u < NU2; ++u) {
-      const int o = 16 * (wn + WN * u) + l15;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        f32x4 v = acc2[u][mt];
-        if (p.scale != 1.0f) v *= p.scale;
-        *reinterpret_cast<uint2*>(smem + o * YS16 + (ch0 + 16 * mt) * 2) = pack4<T>(v);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int idx = tid + it * NTHR;
-      const int o = idx / VPR, c8 = idx % VPR;
-      const int gr = n0 + o;
-      if (gr < len)
-        *reinterpret_cast<uint4*>(Y + (long long)gr * C + c8 * 8) = *reinterpret_cast<const uint4*>(smem + o * YS16 + c8 * 16);
-    }
-    return;
-  }
+  for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2 + ch0 + 16 * mt);
+  __syncthreads();  // T no longer read
 #pragma unroll
   for (int u = 0; u < NU2; ++u) {
     const int o = 16 * (wn + WN * u) + l15;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<f32x4*>(smem + o * YS + (ch0 + 16 * mt) * 4) = acc2[u][mt];
+    for (int mt = 0; mt < MT; ++mt)
+      *reinterpret_cast<uint2*>(smem + o * YS16 + (ch0 + 16 * mt) * 2) = pack4<T>(acc2[u][mt] + bias[mt]);
   }
   __syncthreads();
 #pragma unroll
@@ -399,12 +315,13 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     const int o = idx / VPR, c8 = idx % VPR;
     const int gr = n0 + o;
     if (gr >= len) continue;
-    f32x4 v0 = *reinterpret_cast<const f32x4*>(smem + o * YS + c8 * 32);
-    f32x4 v1 = *reinterpret_cast<const f32x4*>(smem + o * YS + c8 * 32 + 16);
+    f32x4 v0, v1, a, c;
+    pair_ld8<T>(reinterpret_cast<const T*>(smem + o * YS16 + c8 * 16), v0, v1);
+    pair_ld8<T>(reinterpret_cast<const T*>(&xin[it]), a, c);
+    v0 += a; v1 += c;
     T* dst = Y + (long long)gr * C + c8 * 8;
-    {
-      f32x4 a, c;
-      pair_ld8<T>(reinterpret_cast<const T*>(&sprev[it]), a, c);
+    if (p.accum) {
+      pair_ld8<T>(dst, a, c);
       v0 += a; v1 += c;
     }
     if (p.scale != 1.0f) { v0 *= p.scale; v1 *= p.scale; }

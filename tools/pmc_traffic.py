@@ -11,11 +11,12 @@ these kernels is a 16-byte-per-lane load.  WRITE_SIZE is exact for 16-B stores (
 and mrf_fused write 16-B row pieces / 8-B fragments -- the latter uncalibrated, stated).
 
 The last step's launches are mapped onto the step's layer sequence
-  pre, s0.up, 18 x s0 conv, s1.up, 18 x s1 conv, s2.up, s2 MRF (fused), s3.up, s3 MRF, post
+  pre, s0.up, 18 x s0 conv, s1.up, 9 x s1 pair, s2.up, 9 x s2 pair, s3.up, 9 x s3 pair, post
 and each family's traffic is compared with its algorithmic bytes: every conv reads its
 input rows once, its weights once, writes its output once (+ the residual read of a
-ResBlock's second conv); a fused MRF stage reads the stage input once, writes the MRF mean
-once and reads its 18 weight slabs once.
+ResBlock's second conv); a ResBlock pair reads its input once, writes its output once,
+reads both weight tensors once, and the last pair of the 2nd/3rd resblock also reads the
+running MRF sum.
 """
 import csv
 import json
@@ -26,7 +27,7 @@ from collections import defaultdict
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tools.layer_breakdown import vocoder_layers  # noqa: E402
 
-FAMILIES = ("conv_gemm", "conv_xres", "mrf_fused", "conv_post")
+FAMILIES = ("conv_gemm", "conv_xres", "mrf_fused", "mrf_pair", "conv_post")
 
 
 def family(name):
@@ -48,31 +49,25 @@ def per_dispatch(path, counter):
     return [vals[i] for i in ids], [names[i] for i in ids]
 
 
-def fused_step_layers(B, T, elt=2):
-    """[(label, algorithmic bytes)] of one fused-path step, in launch order."""
+def fused_step_layers(B, T, elt=2, pair_channels=(32, 64, 128)):
+    """[(label, algorithmic bytes)] of one default-path step, in launch order: single convs
+    for stages whose width has no pair kernel (C=256), ResBlock-pair launches otherwise."""
     out = []
-    layers = vocoder_layers(T)
-    mrf = defaultdict(list)
-    for name, M, cin, k, n in layers:
+    for name, M, cin, k, n in vocoder_layers(T):
         st = name.split(".")[0]
         if name == "post":
             out.append(("post", B * n * cin * elt + B * n * 4))
-            continue
-        if name == "pre" or name.endswith(".up"):
+        elif name == "pre" or name.endswith(".up"):
             out.append((name, B * n * cin * elt + B * n * M * elt + M * cin * k * elt))
-            if name.endswith(".up") and st in ("s2", "s3"):
-                out.append((f"{st}.mrf", None))  # filled below
-            continue
-        if st in ("s2", "s3"):
-            mrf[st].append((M, cin, k, n))
-            continue
-        r = B * n * M * elt if name.endswith(".c2") else 0
-        out.append((name, B * n * cin * elt + B * n * M * elt + M * cin * k * elt + r))
-    for i, (lab, b) in enumerate(out):
-        if lab.endswith(".mrf"):
-            convs = mrf[lab.split(".")[0]]
-            C, n = convs[0][0], convs[0][3]
-            out[i] = (lab, 2 * B * n * C * elt + sum(M * c * k * elt for M, c, k, _ in convs))
+        elif M in pair_channels:
+            if name.endswith(".c2"):  # one pair launch per (c1, c2)
+                idx = sum(1 for lab, _ in out if lab.startswith(st + ".pair"))
+                accum = idx % 3 == 2 and idx >= 3   # last pair of the 2nd/3rd resblock adds S
+                act = B * n * M * elt
+                out.append((f"{st}.pair{idx}", 2 * act + (act if accum else 0) + 2 * M * cin * k * elt))
+        else:
+            r = B * n * M * elt if name.endswith(".c2") else 0
+            out.append((name, B * n * cin * elt + B * n * M * elt + M * cin * k * elt + r))
     return out
 
 

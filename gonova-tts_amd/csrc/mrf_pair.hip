@@ -86,6 +86,58 @@ __device__ inline void pair_ld8(const T* p, f32x4& a, f32x4& b) {
   a = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
   b = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
 }
+// Epilogue arithmetic.  f16: packed half math after one cvt_pk per pair of accumulators
+// (v_pk_add/mul/max_f16: a fraction of the f32 instruction count; a sum of two f16 values
+// is correctly rounded either way, the bias/slope products differ by <= 1 ulp).  bf16:
+// f32 math, one rounding at the end.
+template <typename T>
+__device__ inline uint2 epi_conv1(f32x4 acc, f32x4 bias, float slope) {  // lrelu(acc + b) -> 4 x T
+  if constexpr (__is_same(T, half_t)) {
+    half4 h = __builtin_convertvector(acc, half4) + __builtin_convertvector(bias, half4);
+    h = __builtin_elementwise_max(h, h * (half_t)slope);
+    return *reinterpret_cast<const uint2*>(&h);
+  } else {
+    f32x4 v = acc + bias;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaxf(v[e], v[e] * slope);  // 0 <= slope <= 1
+    T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
+    return *reinterpret_cast<const uint2*>(o);
+  }
+}
+template <typename T>
+__device__ inline uint2 epi_conv2(f32x4 acc, f32x4 bias) {  // acc + b -> 4 x T
+  if constexpr (__is_same(T, half_t)) {
+    half4 h = __builtin_convertvector(acc, half4) + __builtin_convertvector(bias, half4);
+    return *reinterpret_cast<const uint2*>(&h);
+  } else {
+    const f32x4 v = acc + bias;
+    T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
+    return *reinterpret_cast<const uint2*>(o);
+  }
+}
+// row pass: (y + h (+ s)) * scale on 8 elements
+template <typename T>
+__device__ inline uint4 epi_row(uint4 y, uint4 h, bool acc, uint4 s, float scale) {
+  if constexpr (__is_same(T, half_t)) {
+    half8 v = *reinterpret_cast<const half8*>(&y) + *reinterpret_cast<const half8*>(&h);
+    if (acc) v += *reinterpret_cast<const half8*>(&s);
+    if (scale != 1.0f) v *= (half_t)scale;
+    return *reinterpret_cast<const uint4*>(&v);
+  } else {
+    const T* ye = reinterpret_cast<const T*>(&y);
+    const T* he = reinterpret_cast<const T*>(&h);
+    const T* se = reinterpret_cast<const T*>(&s);
+    T o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = (float)ye[e] + (float)he[e];
+      if (acc) v += (float)se[e];
+      o[e] = (T)(v * scale);
+    }
+    return *reinterpret_cast<const uint4*>(o);
+  }
+}
+
 template <typename T>
 __device__ inline uint2 pack4(f32x4 v) {
   T e[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
@@ -246,10 +298,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
         const bool valid = gr >= 0 && gr < len;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          f32x4 v = acc1[u][mt] + bias[mt];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaxf(v[e], v[e] * slope);  // lrelu, 0 <= slope <= 1
-          uint2 pk = pack4<T>(v);
+          uint2 pk = epi_conv1<T>(acc1[u][mt], bias[mt], slope);
           if (!valid) pk = uint2{0u, 0u};
           const int cb = (ch0 + 16 * mt) * 2;  // byte offset in the row
           *reinterpret_cast<uint2*>(Ts + tr * RS + (((cb >> 4) ^ swz(tr)) << 4) + (cb & 15)) = pk;
@@ -306,7 +355,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     const int o = 16 * (wn + WN * u) + l15;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
-      *reinterpret_cast<uint2*>(smem + o * YS16 + (ch0 + 16 * mt) * 2) = pack4<T>(acc2[u][mt] + bias[mt]);
+      *reinterpret_cast<uint2*>(smem + o * YS16 + (ch0 + 16 * mt) * 2) = epi_conv2<T>(acc2[u][mt], bias[mt]);
   }
   __syncthreads();
 #pragma unroll
@@ -315,17 +364,11 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     const int o = idx / VPR, c8 = idx % VPR;
     const int gr = n0 + o;
     if (gr >= len) continue;
-    f32x4 v0, v1, a, c;
-    pair_ld8<T>(reinterpret_cast<const T*>(smem + o * YS16 + c8 * 16), v0, v1);
-    pair_ld8<T>(reinterpret_cast<const T*>(&xin[it]), a, c);
-    v0 += a; v1 += c;
     T* dst = Y + (long long)gr * C + c8 * 8;
-    if (p.accum) {
-      pair_ld8<T>(dst, a, c);
-      v0 += a; v1 += c;
-    }
-    if (p.scale != 1.0f) { v0 *= p.scale; v1 *= p.scale; }
-    pair_st8<T>(dst, v0, v1);
+    const uint4 y = *reinterpret_cast<const uint4*>(smem + o * YS16 + c8 * 16);
+    uint4 sv = {};
+    if (p.accum) sv = *reinterpret_cast<const uint4*>(dst);
+    *reinterpret_cast<uint4*>(dst) = epi_row<T>(y, xin[it], p.accum, sv, p.scale);
   }
 }
 

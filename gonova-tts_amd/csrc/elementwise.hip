@@ -102,10 +102,99 @@ __global__ __launch_bounds__(256) void conv_post_kernel(const T* __restrict__ x,
   if (tb < T_) wav[b * swb + tb] = tb < len ? tanhf(acc1) : 0.f;
 }
 
+// 16-bit conv_post: the fp32 version above is LDS/VALU-bound (scalar converts into a
+// channel-major fp32 tile, then 224 ds_read_b32 + 224 FMAs per sample: 1.5 TB/s).  Here
+// the tile stays row-major in the compute dtype (lrelu applied packed), 16-byte chunk c of
+// row r at c ^ ((r >> 2) & 3) -- 16 consecutive rows per ds_read_b128 lane group hit 16
+// distinct slots -- and each sample is 4 x 7 row reads + 112 v_dot2_f32_{f16,bf16}
+// against wave-uniform packed weights.  Thread tid produces samples t0+tid, t0+tid+256.
+template <typename T>
+struct Dot2;
+template <>
+struct Dot2<half_t> {
+  typedef _Float16 v2 __attribute__((ext_vector_type(2)));
+  __device__ static inline float dot(unsigned a, unsigned b, float c) {
+    return __builtin_amdgcn_fdot2(*reinterpret_cast<v2*>(&a), *reinterpret_cast<v2*>(&b), c, false);
+  }
+};
+template <>
+struct Dot2<bf16_t> {
+  typedef __bf16 v2 __attribute__((ext_vector_type(2)));
+  __device__ static inline float dot(unsigned a, unsigned b, float c) {
+    return __builtin_amdgcn_fdot2_f32_bf16(*reinterpret_cast<v2*>(&a), *reinterpret_cast<v2*>(&b), c, false);
+  }
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv_post16_kernel(const T* __restrict__ x, const int* __restrict__ x_len,
+                                                          int T_, const unsigned* __restrict__ wpk, float bias,
+                                                          int k, float slope, float* __restrict__ wav,
+                                                          long long swb) {
+  constexpr int C = 32, TB = 512, VPR = 4;  // 4 x 16-byte chunks per 64-byte row
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * TB;
+  const int len = x_len ? min(x_len[b], T_) : T_;
+  const int pad = (k - 1) / 2;
+  const int rows = TB + k - 1;
+  const T* xb = x + (long long)b * T_ * C;
+  auto slot = [](int r, int c) { return r * 64 + ((c ^ ((r >> 2) & 3)) << 4); };
+  for (int i0 = threadIdx.x; i0 < rows * VPR; i0 += 256 * 4) {
+    uint4 u[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = min(i0 + q * 256, rows * VPR - 1);
+      const int t = t0 - pad + i / VPR;
+      u[q] = *reinterpret_cast<const uint4*>(xb + (long long)min(max(t, 0), T_ - 1) * C + (i % VPR) * 8);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = i0 + q * 256;
+      if (i < rows * VPR) {
+        const int r = i / VPR, t = t0 - pad + r;
+        *reinterpret_cast<uint4*>(smem + slot(r, i % VPR)) =
+            (t >= 0 && t < len) ? lrelu_chunk<T>(u[q], slope) : uint4{0u, 0u, 0u, 0u};
+      }
+    }
+  }
+  __syncthreads();
+  float acc0 = bias, acc1 = bias;
+  for (int j = 0; j < k; ++j) {
+    const unsigned* wj = wpk + j * (C / 2);
+#pragma unroll
+    for (int c = 0; c < VPR; ++c) {
+      const uint4 a = *reinterpret_cast<const uint4*>(smem + slot(threadIdx.x + j, c));
+      const uint4 d = *reinterpret_cast<const uint4*>(smem + slot(threadIdx.x + 256 + j, c));
+      acc0 = Dot2<T>::dot(a.x, wj[4 * c + 0], acc0);
+      acc0 = Dot2<T>::dot(a.y, wj[4 * c + 1], acc0);
+      acc0 = Dot2<T>::dot(a.z, wj[4 * c + 2], acc0);
+      acc0 = Dot2<T>::dot(a.w, wj[4 * c + 3], acc0);
+      acc1 = Dot2<T>::dot(d.x, wj[4 * c + 0], acc1);
+      acc1 = Dot2<T>::dot(d.y, wj[4 * c + 1], acc1);
+      acc1 = Dot2<T>::dot(d.z, wj[4 * c + 2], acc1);
+      acc1 = Dot2<T>::dot(d.w, wj[4 * c + 3], acc1);
+    }
+  }
+  const int ta = t0 + threadIdx.x, tb = ta + 256;
+  if (ta < T_) wav[b * swb + ta] = ta < len ? tanhf(acc0) : 0.f;
+  if (tb < T_) wav[b * swb + tb] = tb < len ? tanhf(acc1) : 0.f;
+}
+
 hipError_t launch_conv_post(int dtype, const void* x, const int* x_len, int B, int T_, int C,
-                            const float* w, float bias, int k, float slope, float* wav, long long swb,
-                            hipStream_t s) {
+                            const float* w, const void* wpk, float bias, int k, float slope, float* wav,
+                            long long swb, hipStream_t s) {
   if (C != 32) return hipErrorInvalidValue;
+  if (dtype != DT_F32 && wpk) {
+    dim3 grid((T_ + 511) / 512, B);
+    const size_t lds = (size_t)(512 + k - 1) * 64;
+    if (dtype == DT_F16)
+      hipLaunchKernelGGL((conv_post16_kernel<half_t>), grid, dim3(256), lds, s, (const half_t*)x, x_len, T_,
+                         (const unsigned*)wpk, bias, k, slope, wav, swb);
+    else
+      hipLaunchKernelGGL((conv_post16_kernel<bf16_t>), grid, dim3(256), lds, s, (const bf16_t*)x, x_len, T_,
+                         (const unsigned*)wpk, bias, k, slope, wav, swb);
+    return hipGetLastError();
+  }
   dim3 grid((T_ + 511) / 512, B);
   const size_t lds = (size_t)C * (512 + k - 1) * 4;
   switch (dtype) {

@@ -47,6 +47,7 @@ struct VocoderWeights {
   // mrf[stage][block][pair][0=conv1,1=conv2]
   std::vector<std::vector<std::vector<std::array<ConvLayer, 2>>>> mrf;
   float* post_w = nullptr;  // fp32 [k][C]
+  void* post_wh = nullptr;  // [k][C] in the vocoder dtype (16-bit conv_post kernel), or null
   float post_b = 0.f;
   int post_k = 7, post_c = 32;
   int hop = 256;
@@ -288,6 +289,7 @@ struct tts_engine {
     for (int c = 0; c < v.post_c; ++c)
       for (int j = 0; j < v.post_k; ++j) t[(size_t)j * v.post_c + c] = pw.data[(size_t)c * v.post_k + j];
     v.post_w = (float*)track(upload_f32(t));
+    v.post_wh = dt == DT_F32 ? nullptr : track(upload(t, dt));
     v.post_b = get("conv_post.bias").data[0];
     v.loaded = true;
   }
@@ -465,7 +467,8 @@ struct tts_engine {
       Tin = Tout;
       cin = ch;
     }
-    HIP_CHECK(launch_conv_post(dt, S, Lp(nst), B, Tin, cin, v.post_w, v.post_b, v.post_k, 0.01f, wav, swb, s));
+    HIP_CHECK(launch_conv_post(dt, S, Lp(nst), B, Tin, cin, v.post_w, v.post_wh, v.post_b, v.post_k, 0.01f, wav, swb,
+                               s));
   }
 };
 

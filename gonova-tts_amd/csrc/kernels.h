@@ -89,8 +89,9 @@ hipError_t launch_mel_in(int dtype, const float* mel, long long smb, int smr, co
                          const float* scale, void* out, int B, int T, int C, hipStream_t s);
 hipError_t launch_lens(const int* in, int* out, int B, const int* mult, const int* add, int n,
                        hipStream_t s);
+// wpk (optional, 16-bit dtypes): the same weights [k][C] in the compute dtype -> dot2 kernel
 hipError_t launch_conv_post(int dtype, const void* x, const int* x_len, int B, int T, int C,
-                            const float* w /*[k][C]*/, float bias, int k, float in_slope,
+                            const float* w /*[k][C]*/, const void* wpk, float bias, int k, float in_slope,
                             float* wav, long long swb, hipStream_t s);
 
 }  // namespace tts

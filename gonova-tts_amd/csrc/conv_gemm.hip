@@ -241,7 +241,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
 }
 
 // ---------------------------------------------------------------------------------------
-// X-resident variant for M >= 128, 16-bit dtypes, Cin % 64 == 0, fragment-packed weights
+// X-resident variant for M >= 64, 16-bit dtypes, Cin % 64 == 0, fragment-packed weights
 // (ConvParams::wpk): HiFi-GAN stages 0-1 and upsamplers, acoustic linears/FFN.
 //
 // Why (measured on conv_gemm_kernel at C=128/256: 70-83 % of wave cycles in s_waitcnt,
@@ -260,11 +260,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
 //    residual / scale pass reads and writes whole 16-byte row pieces.
 // The group's X load latency is covered by the other blocks on the CU (LDS <= 53 KB: 3).
 //
-// Block: 4 waves stacked along M (32 output channels each), BN = 32*NT rows.  X tile row
+// Block: 4 waves, WM along M (32 output channels each) x WN = 4/WM along N (32*NT rows
+// each): 128 x 128 tiles for M >= 128, 64 x 256 for M = 64.  X tile row
 // stride CG*2+16 bytes (an odd number of 16-byte slots: conflict-free ds_read_b128 of 32
 // consecutive rows).
-constexpr int XRES_OS = 128 * 4 + 16;  // fp32 output staging row stride (bytes)
-constexpr int XRES_HR = 64;            // output rows staged per half
+constexpr int XRES_HR = 64;            // output rows per N-wave staged per half
 constexpr int XRES_SU = 4;             // X staging loads in flight per thread
 
 template <typename T>
@@ -280,13 +280,18 @@ __device__ inline void st8(T* p, f32x4 a, f32x4 b) {
   *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(e);
 }
 
-template <typename T, int NT>
+template <typename T, int NT, int WM>
 __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG) {
   using MF = Mfma<T>;
   typedef typename MF::frag Frag;
   static_assert(sizeof(T) == 2, "16-bit dtypes only");
   static_assert(NT % 2 == 0, "output staged in 64-row halves");
-  constexpr int BN = 32 * NT;
+  static_assert(WM == 4 || WM == 2, "4 waves: 4 x 1 or 2 x 2");
+  constexpr int WN = 4 / WM;
+  constexpr int BM = 32 * WM;          // output channels per block
+  constexpr int BN = 32 * NT * WN;     // output rows per block
+  constexpr int OS = BM * 4 + 16;      // fp32 output staging row stride (bytes)
+  constexpr int PPR = BM / 8;          // 8-channel pieces per staged row
   constexpr int NTHR = 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -302,12 +307,13 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l31 = lane & 31;
   const int hh = lane >> 5;
+  const int wm = wave % WM, wn = wave / WM;
 
   const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.sxb + (long long)hd * p.sxh;
   // packed weights: [MB][taps][Cin/16][64][8]; a wave past M reads the last block (its
   // results are never stored)
   const int KST = p.Cin / 16;
-  const int mb = min((int)blockIdx.y * 4 + wave, (p.M + 31) / 32 - 1);
+  const int mb = min((int)blockIdx.y * WM + wm, (p.M + 31) / 32 - 1);
   const char* wl = reinterpret_cast<const char*>(p.wpk) + ((long long)mb * p.taps * KST) * 1024 + lane * 16;
   const int R = BN + (p.taps - 1) * p.dil;
   const int RS = CG * 2 + 16;
@@ -317,7 +323,7 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
   const int x_start = n0 - p.pad;
   const int xlast = xlen > 0 ? xlen - 1 : 0;
   const int dstep = p.dil * RS;        // LDS bytes per tap
-  const char* xl = smem + l31 * RS + hh * 16;
+  const char* xl = smem + (wn * 32 * NT + l31) * RS + hh * 16;
 
   f32x16 acc[NT];
 #pragma unroll
@@ -403,8 +409,11 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
   const T* R1 = p.r1 ? reinterpret_cast<const T*>(p.r1) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const T* R2 = p.r2 ? reinterpret_cast<const T*>(p.r2) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const int tlen = p.up_len ? min(p.up_len[b], (p.y_rows - 1) * p.up_s) : 0;
-  const int cl = tid & 15;                    // 8-channel piece of the block's 128 channels
-  const int m8 = blockIdx.y * 128 + cl * 8;
+  // staged half h holds rows wn*32*NT + 64h + [0, 64) of every N-wave, compacted to
+  // staged row wn*64 + r; the row pass maps staged row sr back to its output row
+  const int cl = tid % PPR;                   // 8-channel piece of the block's BM channels
+  const int m8 = blockIdx.y * BM + cl * 8;
+  auto out_row = [&](int half, int sr) { return n0 + (sr >> 6) * (32 * NT) + half * XRES_HR + (sr & 63); };
   const bool mok = m8 < p.M;
   f32x4 bias0 = {}, bias1 = {};
   if (p.bias && mok) {
@@ -416,13 +425,13 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
   // every item's first-residual rows in flight before the staging barriers (the weight
   // ring is dead here, so these registers do not raise the kernel's peak; prefetching r2
   // as well would spill)
-  constexpr int NIT = XRES_HR * 16 / NTHR;
+  constexpr int NIT = XRES_HR * WN * PPR / NTHR;
   uint4 res1[NT / 2][NIT];
 #pragma unroll
   for (int half = 0; half < NT / 2; ++half)
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const int n = n0 + half * XRES_HR + (tid >> 4) + it * (NTHR / 16);
+      const int n = out_row(half, tid / PPR + it * (NTHR / PPR));
       int row = min(n, ylen - 1);
       if (p.up_s) row = min(max(row * p.up_s + q - p.up_p, 0), max(tlen - 1, 0));
       if (R1) res1[half][it] = *reinterpret_cast<const uint4*>(R1 + (long long)row * p.srr + (mok ? col : 0));
@@ -435,22 +444,22 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x16& a = acc[2 * half + k];
-        *reinterpret_cast<f32x4*>(smem + (k * 32 + l31) * XRES_OS + (wave * 32 + 8 * g + 4 * hh) * 4) =
+        *reinterpret_cast<f32x4*>(smem + (wn * 64 + k * 32 + l31) * OS + (wm * 32 + 8 * g + 4 * hh) * 4) =
             f32x4{a[4 * g + 0], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]};
       }
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const int rl = (tid >> 4) + it * (NTHR / 16);
-      const int n = n0 + half * XRES_HR + rl;
+      const int rl = tid / PPR + it * (NTHR / PPR);
+      const int n = out_row(half, rl);
       if (n >= ylen || !mok) continue;
       int row = n;
       if (p.up_s) {
         row = n * p.up_s + q - p.up_p;
         if (row < 0 || row >= tlen) continue;
       }
-      f32x4 v0 = *reinterpret_cast<const f32x4*>(smem + rl * XRES_OS + cl * 32);
-      f32x4 v1 = *reinterpret_cast<const f32x4*>(smem + rl * XRES_OS + cl * 32 + 16);
+      f32x4 v0 = *reinterpret_cast<const f32x4*>(smem + rl * OS + cl * 32);
+      f32x4 v1 = *reinterpret_cast<const f32x4*>(smem + rl * OS + cl * 32 + 16);
       v0 += bias0; v1 += bias1;
       if (p.alpha != 1.0f) { v0 *= p.alpha; v1 *= p.alpha; }
       if (p.act_out) {
@@ -473,7 +482,7 @@ constexpr int XRES_LDS_MAX = 53 * 1024;  // 3 blocks per CU
 // channel group for the X-resident kernel: largest power-of-two CG | Cin, CG >= 64, tile within
 // XRES_LDS_MAX; 0 = not eligible
 static int xres_group(const ConvParams& p, int BN) {
-  if (!p.wpk || p.M < 128 || p.Cin % 64 || p.M % 8 || p.nh != 1) return 0;
+  if (!p.wpk || p.M < 64 || p.Cin % 64 || p.M % 8 || p.nh != 1) return 0;
   if (p.syr % 8 || p.syb % 8 || ((p.r1 || p.r2) && (p.srr % 8 || p.srb % 8))) return 0;
   if (p.up_s && p.up_cout % 8) return 0;
   const int R = BN + (p.taps - 1) * p.dil;
@@ -492,16 +501,27 @@ static int xres_mode() {  // TTS_CONV_XRES=0 disables the X-resident kernel (A/B
   return m;
 }
 
+// 128-channel blocks (4 x 1 waves, BN = 128) for M >= 128; 64-channel blocks (2 x 2 waves,
+// BN = 256) for M = 64 (the last upsampler)
+static int xres_wm(const ConvParams& p) { return p.M >= 128 ? 4 : 2; }
+
+template <typename T, int WM>
+static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s) {
+  constexpr int NT = 4, BM = 32 * WM, BN = 32 * NT * (4 / WM);
+  const size_t lds = std::max((size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16),
+                              (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
+  dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
+  hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM>), grid, dim3(256), lds, s, p, cg);
+  return hipGetLastError();
+}
+
 template <typename T>
 static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err) {
-  constexpr int NT = 4, BN = 32 * NT;
   if (!xres_mode()) return false;
-  const int cg = xres_group(p, BN);
+  const int wm = xres_wm(p);
+  const int cg = xres_group(p, 32 * 4 * (4 / wm));
   if (!cg) return false;
-  const size_t lds = std::max((size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16), (size_t)XRES_HR * XRES_OS);
-  dim3 grid((p.y_rows + BN - 1) / BN, (p.M + 127) / 128, p.B * p.nh);
-  hipLaunchKernelGGL((conv_xres_kernel<T, NT>), grid, dim3(256), lds, s, p, cg);
-  *err = hipGetLastError();
+  *err = wm == 4 ? launch_xres_wm<T, 4>(p, cg, s) : launch_xres_wm<T, 2>(p, cg, s);
   return true;
 }
 
@@ -565,7 +585,7 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why) {
 }
 
 int conv_gemm_kind(int dtype, const ConvParams& p) {
-  return (dtype != DT_F32 && xres_mode() && xres_group(p, 128)) ? PK_CONV_XRES : PK_CONV_GEMM;
+  return (dtype != DT_F32 && xres_mode() && xres_group(p, 32 * 4 * (4 / xres_wm(p)))) ? PK_CONV_XRES : PK_CONV_GEMM;
 }
 
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s) {

@@ -74,9 +74,9 @@ struct ConvLayer {
 //   P[M/32][taps][Cin/16][lane 0..63][8],  lane l holding row 32*mb + (l & 31),
 //   channels 16*ks + 8*(l >> 5) + [0, 8)   (the A operand of v_mfma_f32_32x32x16_*),
 // so one wave's fragment for (32-row block, tap, k-step) is 1 KiB contiguous.  Rows past
-// M are zero.  Only for 16-bit dtypes with Cin % 64 == 0 and M >= 128 (else null).
+// M are zero.  Only for 16-bit dtypes with Cin % 64 == 0 and M >= 64 (else null).
 inline void* frag_pack(const std::vector<float>& w, int M, int taps, int ci, int dt, std::vector<void*>& allocs) {
-  if (dt == DT_F32 || ci % 64 || M < 128) return nullptr;
+  if (dt == DT_F32 || ci % 64 || M < 64) return nullptr;
   const int MB = (M + 31) / 32, KS = ci / 16;
   std::vector<float> p((size_t)MB * 32 * taps * ci, 0.f);
   size_t o = 0;

@@ -19,7 +19,7 @@ the max time over ranks is used.  value = samples of all ranks / max time.
 `roofline` is for the dominant kernel family (largest summed time per step: today the
 X-resident implicit-GEMM conv of stages 0-1), timed live with hipEvents around every
 launch on the stream it runs on; `roofline.kernels` lists every family the same way
-(conv_gemm_kernel, conv_xres_kernel, mrf_fused_kernel).  `cpu_baseline` is the NumPy
+(conv_gemm_kernel, conv_xres_kernel, mrf_fused_kernel, mrf_pair_kernel).  `cpu_baseline` is the NumPy
 oracle on the host cores (bounded sample, rank 0 only).
 """
 from __future__ import annotations
@@ -328,7 +328,7 @@ def main():
                "per_gpu_samples_per_s": round(per_gpu, 1), "x_realtime_per_gpu": round(per_gpu / SR, 2),
                "rtf": round(SR / per_gpu, 7), "acoustic_ms_per_step": f["acoustic_ms_per_step"],
                "roofline": f["roofline"]}
-    if ctx.rank == 0 and not args.no_cpu_baseline:
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:  # rank 0 at N=1 only
         out["cpu_baseline"] = cpu_baseline(args.cpu_frames)
     if ctx.rank == 0:
         print(json.dumps(out), flush=True)

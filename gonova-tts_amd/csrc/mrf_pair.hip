@@ -77,7 +77,6 @@ struct Mfma16<bf16_t> {
 };
 
 constexpr int PAIR_SU = 8;       // input-tile loads in flight per thread (one round for every shape)
-constexpr int PAIR_KMAX = 17;    // 2*a2 <= 16 keeps conv1 within NU2 + 1 tiles per wave
 
 template <typename T>
 __device__ inline void pair_ld8(const T* p, f32x4& a, f32x4& b) {
@@ -160,23 +159,76 @@ static size_t pair_lds_bytes(int k, int d) {
   return std::max(std::max(g, t), (size_t)G::BN * (C * 2 + 16));
 }
 
-template <typename T, int C>
-__global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
+// One conv of the pair over NU 16-row tiles per wave: acc[u][mt] += W[mt] x tile u.
+// S = k * KS k-steps, weights streamed through the D-slot register ring (ring[i] holds step
+// i on entry).  The step sequence is compile-time: full groups of D steps in a counted loop
+// (every step reloads its slot D steps ahead), then a peeled last group whose reloads stop
+// at S, then the S % D tail.  Straight-line bodies let the waitcnt pass keep the ring's
+// 2*(D-1) younger loads in flight (a conditional reload made it drain vmcnt to 0 every step).
+// lb: this lane's LDS base (row l15 of the wave's first tile); tstep: LDS bytes per tap;
+// trow: rows per tap (swizzle); tile[u]: byte offset of tile u.
+template <typename T, int C, int S, int NU, int D>
+__device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][2], typename Mfma<T>::frag (&ring)[D][2],
+                                          const char* __restrict__ wp, const char* lb, int tstep, int trow,
+                                          const int (&tile)[NU], int l15, int lq) {
   using G = PairGeom<C>;
   using MF = Mfma16<T>;
   typedef typename Mfma<T>::frag Frag;
+  constexpr int KS = C / 32;
+  constexpr int NG = S / D, REM = S % D;
+  auto step = [&](const int s, const int slot, const bool reload) __attribute__((always_inline)) {
+    const int tap = KS == 1 ? s : s / KS, ks = KS == 1 ? 0 : s % KS;
+    const int r = l15 + tap * trow;
+    const char* bp = lb + tap * tstep + (((lq + 4 * ks) ^ (((r * G::SW_MUL) >> G::SW_S) & G::SW_M)) << 4);
+    Frag bf[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) bf[u] = *reinterpret_cast<const Frag*>(bp + tile[u]);
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) acc[u][mt] = MF::mma(ring[slot][mt], bf[u], acc[u][mt]);
+    if (reload) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        ring[slot][mt] = *reinterpret_cast<const Frag*>(wp + ((long long)mt * S + s + D) * 1024);
+    }
+  };
+  if constexpr (NG >= 2) {
+#pragma nounroll
+    for (int g = 0; g < NG - 1; ++g) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) step(g * D + i, i, true);
+    }
+  }
+  if constexpr (NG >= 1) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) step((NG - 1) * D + i, i, i < REM);
+  }
+#pragma unroll
+  for (int i = 0; i < REM; ++i) step(NG * D + i, i, false);
+}
+
+template <typename T, int C, int K>
+__global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
+  using G = PairGeom<C>;
+  typedef typename Mfma<T>::frag Frag;
   constexpr int BN = G::BN, WM = G::WM, WN = G::WN, RS = G::RS;
-  constexpr int PAIR_D = G::D;         // weight ring depth (k-steps)
+  constexpr int D = G::D;              // weight ring depth (k-steps)
   auto swz = [](int r) { return ((r * G::SW_MUL) >> G::SW_S) & G::SW_M; };  // chunk XOR of row r
   constexpr int NTHR = 256;
   constexpr int KS = C / 32;           // k-steps (of 32 channels) per tap
   constexpr int MT = 2;                // 16-channel M tiles per wave
+  constexpr int S = K * KS;            // k-steps per conv
+  constexpr int A2 = (K - 1) / 2;
+  constexpr int RT = BN + 2 * A2;      // conv1 rows conv2 needs
+  constexpr int NT1 = (RT + 15) / 16;  // conv1 tiles (block)
+  constexpr int NU1 = (NT1 + WN - 1) / WN;  // conv1 tiles per wave (the last may be a repeat)
   constexpr int NU2 = BN / 16 / WN;    // conv2 tiles per wave
-  constexpr int NU1 = NU2 + 1;         // conv1 tiles per wave (upper bound)
   constexpr int VPR = C / 8;           // 16-byte pieces per row
   constexpr int YS16 = C * 2 + 16;     // output tile staging row stride
   static_assert(WM * WN * 64 == NTHR && WM * 32 == C, "wave grid");
   static_assert(NTHR % VPR == 0, "staging");
+  static_assert(2 * A2 <= 16, "conv1 overrun within one tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int b = blockIdx.y;
@@ -186,37 +238,32 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave % WM, wn = wave / WM;
+  const int wm = WM == 1 ? 0 : wave % WM, wn = WN == 1 ? 0 : wave / WM;
   const int l15 = lane & 15, lq = lane >> 4;
-  const int k = p.k, d = p.d;
-  const int a2 = (k - 1) / 2, a1 = a2 * d;
-  const int RG = BN + 2 * (a1 + a2);
-  const int RT = BN + 2 * a2;
-  const int NT1 = (RT + 15) / 16;
-  const int nu1 = NT1 > wn ? (NT1 - wn + WN - 1) / WN : 0;
-  const int S = k * KS;                // k-steps per conv
+  const int d = p.d;
+  const int a1 = A2 * d;
+  const int RG = BN + 2 * (a1 + A2);
   char* Gs = smem;
   char* Ts = smem;                     // T overwrites G after conv1
   const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
   const float slope = p.slope;
   const int ch0 = 32 * wm + 4 * lq;    // + 16*mt: this lane's 4 output channels
 
-  // weights: [C/16][k][KS][64][8] -> step s = tap*KS + ks of m-tile mb at (mb*S + s) KiB
+  // weights: [C/16][k][KS][64][8] -> step s of m-tile mb at (mb*S + s) KiB
   const char* w1 = reinterpret_cast<const char*>(p.w1) + (long long)(2 * wm) * S * 1024 + lane * 16;
   const char* w2 = reinterpret_cast<const char*>(p.w2) + (long long)(2 * wm) * S * 1024 + lane * 16;
-  Frag ring[PAIR_D][MT];
-#define TTS_PLOAD(W_, SLOT_, S_)                                                          \
-  _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_)                                    \
-    ring[SLOT_][mt_] = *reinterpret_cast<const Frag*>((W_) + ((long long)mt_ * S + (S_)) * 1024);
+  Frag ring[D][MT];
 #pragma unroll
-  for (int i = 0; i < PAIR_D; ++i)
-    if (i < S) { TTS_PLOAD(w1, i, i) }
+  for (int i = 0; i < D; ++i)
+    if (i < S)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) ring[i][mt] = *reinterpret_cast<const Frag*>(w1 + ((long long)mt * S + i) * 1024);
 
   // ---- stage g = lrelu(h) (zero outside the utterance) ----
   {
     const int cc = tid % VPR, r0 = tid / VPR;
     constexpr int rstep = NTHR / VPR;
-    const int gs = n0 - a1 - a2;
+    const int gs = n0 - a1 - A2;
     const T* xc = X + cc * 8;
     if (gs >= 0 && gs + RG <= len) {  // interior tile: no clamps, no masks
       for (int rb = r0; rb < RG; rb += PAIR_SU * rstep) {
@@ -252,39 +299,26 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   __syncthreads();
 
   // ---- conv1 over T rows [0, 16*NT1): T row t <-> global row n0 - a2 + t ----
+  // Tiles are dealt round-robin to the WN waves of an M slice; a wave whose share is one
+  // short repeats the block's last tile (straight-line loop, result not stored).
   f32x4 acc1[NU1][MT];
 #pragma unroll
   for (int u = 0; u < NU1; ++u)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = f32x4{};
   {
-    const char* gb = Gs + (16 * wn + l15) * RS;
-    for (int s0 = 0; s0 < S; s0 += PAIR_D) {
+    int tile[NU1];
 #pragma unroll
-      for (int i = 0; i < PAIR_D; ++i) {
-        const int s = s0 + i;
-        if (s < S) {
-          const int tap = KS == 1 ? s : s / KS, ks = KS == 1 ? 0 : s % KS;
-          const char* bp = gb + tap * d * RS + ((lq + 4 * ks) ^ swz(l15 + tap * d)) * 16;
-          Frag bf[NU1];
-#pragma unroll
-          for (int u = 0; u < NU1; ++u)
-            if (u < nu1) bf[u] = *reinterpret_cast<const Frag*>(bp + u * (16 * WN) * RS);
-#pragma unroll
-          for (int u = 0; u < NU1; ++u)
-            if (u < nu1) {
-#pragma unroll
-              for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = MF::mma(ring[i][mt], bf[u], acc1[u][mt]);
-            }
-          if (s + PAIR_D < S) { TTS_PLOAD(w1, i, s + PAIR_D) }
-        }
-      }
-    }
+    for (int u = 0; u < NU1; ++u) tile[u] = 16 * min(wn + WN * u, NT1 - 1) * RS;
+    pair_conv<T, C, S, NU1, D>(acc1, ring, w1, Gs + l15 * RS, d * RS, d, tile, l15, lq);
   }
+  __builtin_amdgcn_sched_barrier(0);
   // conv2's first weight steps in flight during the conv1 epilogue
 #pragma unroll
-  for (int i = 0; i < PAIR_D; ++i)
-    if (i < S) { TTS_PLOAD(w2, i, i) }
+  for (int i = 0; i < D; ++i)
+    if (i < S)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) ring[i][mt] = *reinterpret_cast<const Frag*>(w2 + ((long long)mt * S + i) * 1024);
   __syncthreads();  // T overwrites G: every wave is done reading it
   {
     f32x4 bias[MT];
@@ -292,9 +326,9 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b1 + ch0 + 16 * mt);
 #pragma unroll
     for (int u = 0; u < NU1; ++u)
-      if (u < nu1) {
+      if (NT1 % WN == 0 || wn + WN * u < NT1) {
         const int tr = 16 * (wn + WN * u) + l15;
-        const int gr = n0 - a2 + tr;
+        const int gr = n0 - A2 + tr;
         const bool valid = gr >= 0 && gr < len;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
@@ -317,27 +351,12 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = f32x4{};
   {
-    const char* tb = Ts + (16 * wn + l15) * RS;
-    for (int s0 = 0; s0 < S; s0 += PAIR_D) {
+    int tile[NU2];
 #pragma unroll
-      for (int i = 0; i < PAIR_D; ++i) {
-        const int s = s0 + i;
-        if (s < S) {
-          const int tap = KS == 1 ? s : s / KS, ks = KS == 1 ? 0 : s % KS;
-          const char* bp = tb + tap * RS + ((lq + 4 * ks) ^ swz(l15 + tap)) * 16;
-          Frag bf[NU2];
-#pragma unroll
-          for (int u = 0; u < NU2; ++u) bf[u] = *reinterpret_cast<const Frag*>(bp + u * (16 * WN) * RS);
-#pragma unroll
-          for (int u = 0; u < NU2; ++u)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = MF::mma(ring[i][mt], bf[u], acc2[u][mt]);
-          if (s + PAIR_D < S) { TTS_PLOAD(w2, i, s + PAIR_D) }
-        }
-      }
-    }
+    for (int u = 0; u < NU2; ++u) tile[u] = 16 * (wn + WN * u) * RS;
+    pair_conv<T, C, S, NU2, D>(acc2, ring, w2, Ts + l15 * RS, RS, 1, tile, l15, lq);
   }
-#undef TTS_PLOAD
+  __builtin_amdgcn_sched_barrier(0);  // keep the epilogue's loads out of the MFMA tail
   // residual h (input rows) in flight while the tile is staged (the MRF-sum rows of
   // accumulating launches are read in the row pass: prefetching both spills)
   uint4 xin[NIT];
@@ -372,31 +391,44 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   }
 }
 
-template <typename T, int C>
+template <typename T, int C, int K>
 static hipError_t launch_pair_t(const MrfPairParams& p, hipStream_t s) {
   using G = PairGeom<C>;
-  const size_t lds = pair_lds_bytes<C>(p.k, p.d);
+  const size_t lds = pair_lds_bytes<C>(K, p.d);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   dim3 grid((p.T + G::BN - 1) / G::BN, p.B);
-  hipLaunchKernelGGL((mrf_pair_kernel<T, C>), grid, dim3(256), lds, s, p);
+  hipLaunchKernelGGL((mrf_pair_kernel<T, C, K>), grid, dim3(256), lds, s, p);
   return hipGetLastError();
 }
 
+template <typename T, int C>
+static hipError_t launch_pair_k(const MrfPairParams& p, hipStream_t s) {
+  switch (p.k) {
+    case 3: return launch_pair_t<T, C, 3>(p, s);
+    case 5: return launch_pair_t<T, C, 5>(p, s);
+    case 7: return launch_pair_t<T, C, 7>(p, s);
+    case 11: return launch_pair_t<T, C, 11>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// kernel sizes with a compiled pair kernel: HiFi-GAN V1/V2 (3, 7, 11) and V3 (3, 5, 7);
+// other sizes run the per-conv path
 bool mrf_pair_supported(int dtype, int C, int k) {
-  return (dtype == DT_F16 || dtype == DT_BF16) && (C == 32 || C == 64 || C == 128) && k >= 1 && k % 2 == 1 &&
-         k <= PAIR_KMAX;
+  return (dtype == DT_F16 || dtype == DT_BF16) && (C == 32 || C == 64 || C == 128) &&
+         (k == 3 || k == 5 || k == 7 || k == 11);
 }
 
 hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s) {
   if (!mrf_pair_supported(dtype, C, p.k) || p.d < 1) return hipErrorInvalidValue;
   if (dtype == DT_F16) {
-    if (C == 32) return launch_pair_t<half_t, 32>(p, s);
-    if (C == 64) return launch_pair_t<half_t, 64>(p, s);
-    return launch_pair_t<half_t, 128>(p, s);
+    if (C == 32) return launch_pair_k<half_t, 32>(p, s);
+    if (C == 64) return launch_pair_k<half_t, 64>(p, s);
+    return launch_pair_k<half_t, 128>(p, s);
   }
-  if (C == 32) return launch_pair_t<bf16_t, 32>(p, s);
-  if (C == 64) return launch_pair_t<bf16_t, 64>(p, s);
-  return launch_pair_t<bf16_t, 128>(p, s);
+  if (C == 32) return launch_pair_k<bf16_t, 32>(p, s);
+  if (C == 64) return launch_pair_k<bf16_t, 64>(p, s);
+  return launch_pair_k<bf16_t, 128>(p, s);
 }
 
 }  // namespace tts

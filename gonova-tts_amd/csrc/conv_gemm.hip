@@ -314,11 +314,20 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
   // results are never stored)
   const int KST = p.Cin / 16;
   const int mb = min((int)blockIdx.y * WM + wm, (p.M + 31) / 32 - 1);
-  const char* wl = reinterpret_cast<const char*>(p.wpk) + ((long long)mb * p.taps * KST) * 1024 + lane * 16;
+  // Weight quads stream through a bounds-checked buffer descriptor over this wave's block:
+  // a reload past the group's last quad gets an out-of-range offset and fetches nothing, so
+  // every ring slot is reloaded unconditionally (a branch around the reloads made the
+  // waitcnt pass drain vmcnt to 0-2 every quad instead of keeping the ring's 8 younger
+  // loads in flight).
+  const int wbytes = __builtin_amdgcn_readfirstlane(p.taps * KST * 1024);
+  const char* wblk = reinterpret_cast<const char*>(p.wpk) + (long long)mb * wbytes;
+  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wblk), 0, wbytes, 0x00020000);
+  const int lofs = lane * 16;          // voffset: loop-invariant (the quad offset is soffset)
   const int R = BN + (p.taps - 1) * p.dil;
   const int RS = CG * 2 + 16;
   const int VPR = CG / 8;
   const int NQ = CG / 64;              // weight quads (4 k-steps of 16) per tap
+  const int lnq = __builtin_ctz(NQ);
   const int QT = p.taps * NQ;          // quads per channel group
   const int x_start = n0 - p.pad;
   const int xlast = xlen > 0 ? xlen - 1 : 0;
@@ -329,15 +338,20 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
 #pragma unroll
   for (int j = 0; j < NT; ++j) acc[j] = f32x16{};
 
-  // quad (tap, kq) of channel group g0: 4 contiguous 1 KiB fragments
-#define TTS_LOADQ(A_, TAP_, KQ_)                                                          \
+  // quad qq of channel group g0: 4 contiguous 1 KiB fragments (nothing past the group's QT)
+#define TTS_LOADQ(A_, QQ_)                                                                \
   do {                                                                                    \
-    const char* q_ = wl + (long long)((TAP_) * KST + g0 / 16 + (KQ_) * 4) * 1024;          \
-    _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) A_[j_] = *reinterpret_cast<const Frag*>(q_ + j_ * 1024); \
+    const int qq_ = (QQ_);                                                                \
+    const int o_ = ((qq_ >> lnq) * KST + g0 / 16 + (qq_ & (NQ - 1)) * 4) * 1024 +         \
+                   (((QT - 1 - qq_) >> 31) & 0x40000000); /* uniform; out of range past QT */ \
+    _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) A_[j_] =                             \
+        __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lofs + j_ * 1024, o_, 0)); \
+    __builtin_amdgcn_sched_barrier(0); /* issue here: the scheduler would sink reloads */  \
   } while (0)
-#define TTS_MMAQ(A_, TAP_, KQ_)                                                           \
+#define TTS_MMAQ(A_, QQ_)                                                                 \
   do {                                                                                    \
-    const char* bq_ = xl + (TAP_) * dstep + (KQ_) * 128;                                  \
+    const int qq_ = (QQ_);                                                                \
+    const char* bq_ = xl + (qq_ >> lnq) * dstep + (qq_ & (NQ - 1)) * 128;                 \
     _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                    \
       Frag bf_[NT];                                                                       \
       _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_)                                \
@@ -354,26 +368,13 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
   const int r0 = tid >> lvpr;
   const int rstep = NTHR >> lvpr;
   // quad ring, 3 deep: quad q's weights are issued while quads q-2 and q-1 compute
-#define TTS_STEP(A_, QQ_)                                                                 \
-  if ((QQ_) < QT) {                                                                       \
-    TTS_MMAQ(A_, ctap, ckq);                                                              \
-    if (++ckq == NQ) { ckq = 0; ++ctap; }                                                 \
-    if ((QQ_) + 3 < QT) {                                                                 \
-      TTS_LOADQ(A_, ptap, pkq);                                                           \
-      if (++pkq == NQ) { pkq = 0; ++ptap; }                                               \
-    }                                                                                     \
-  }
   for (int g0 = 0; g0 < p.Cin; g0 += CG) {
     Frag a0[4], a1[4], a2[4];
     // first quads of the group in flight before the X loads (in-order vmcnt: they
     // complete first and are ready when the MFMA loop starts)
-    int ptap = 0, pkq = 0;
-    TTS_LOADQ(a0, ptap, pkq);
-    if (++pkq == NQ) { pkq = 0; ++ptap; }
-    if (QT > 1) TTS_LOADQ(a1, ptap, pkq);
-    if (++pkq == NQ) { pkq = 0; ++ptap; }
-    if (QT > 2) TTS_LOADQ(a2, ptap, pkq);
-    if (++pkq == NQ) { pkq = 0; ++ptap; }
+    TTS_LOADQ(a0, 0);
+    TTS_LOADQ(a1, 1);
+    TTS_LOADQ(a2, 2);
     if (g0) __syncthreads();  // previous group's B reads are done
     const T* xg = X + g0 + cc * 8;
     for (int rb = r0; rb < R; rb += XRES_SU * rstep) {
@@ -386,21 +387,26 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
 #pragma unroll
       for (int i = 0; i < XRES_SU; ++i) {
         const int rr = rb + i * rstep;
-        if (rr < R) {
-          const int xr = x_start + rr;
-          *reinterpret_cast<uint4*>(smem + rr * RS + cc * 16) = act16<T>(r[i], xr >= 0 && xr < xlen, p.in_slope);
-        }
+        const int xr = x_start + rr;
+        // consumed unconditionally: a load consumed only under the row mask stays "pending"
+        // for the waitcnt pass, whose WAW check then drains vmcnt at the MFMA loop head
+        const uint4 v = act16<T>(r[i], xr >= 0 && xr < xlen, p.in_slope);
+        if (rr < R) *reinterpret_cast<uint4*>(smem + rr * RS + cc * 16) = v;
       }
     }
     __syncthreads();
-    int ctap = 0, ckq = 0;
-    for (int q = 0; q < QT; q += 3) {
-      TTS_STEP(a0, q)
-      TTS_STEP(a1, q + 1)
-      TTS_STEP(a2, q + 2)
+    int q = 0;
+    for (; q + 3 <= QT; q += 3) {  // straight-line body
+      TTS_MMAQ(a0, q);
+      TTS_LOADQ(a0, q + 3);
+      TTS_MMAQ(a1, q + 1);
+      TTS_LOADQ(a1, q + 4);
+      TTS_MMAQ(a2, q + 2);
+      TTS_LOADQ(a2, q + 5);
     }
+    if (q < QT) TTS_MMAQ(a0, q);
+    if (q + 1 < QT) TTS_MMAQ(a1, q + 1);
   }
-#undef TTS_STEP
 #undef TTS_LOADQ
 #undef TTS_MMAQ
 

@@ -191,6 +191,7 @@ __device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][2], typename Mfma<T>:
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
         ring[slot][mt] = *reinterpret_cast<const Frag*>(wp + ((long long)mt * S + s + D) * 1024);
+      __builtin_amdgcn_sched_barrier(0);  // issue the reload here, D steps ahead of its use
     }
   };
   if constexpr (NG >= 2) {
@@ -274,7 +275,8 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
 #pragma unroll
         for (int i = 0; i < PAIR_SU; ++i) {
           const int r = rb + i * rstep;
-          if (r < RG) *reinterpret_cast<uint4*>(Gs + r * RS + (cc ^ swz(r)) * 16) = lrelu_chunk<T>(v[i], slope);
+          const uint4 g = lrelu_chunk<T>(v[i], slope);  // consumed unconditionally (waitcnt)
+          if (r < RG) *reinterpret_cast<uint4*>(Gs + r * RS + (cc ^ swz(r)) * 16) = g;
         }
       }
     } else
@@ -288,11 +290,10 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
 #pragma unroll
       for (int i = 0; i < PAIR_SU; ++i) {
         const int r = rb + i * rstep;
-        if (r < RG) {
-          const int gr = gs + r;
-          *reinterpret_cast<uint4*>(Gs + r * RS + (cc ^ swz(r)) * 16) =
-              (gr >= 0 && gr < len) ? lrelu_chunk<T>(v[i], slope) : uint4{0u, 0u, 0u, 0u};
-        }
+        const int gr = gs + r;
+        const uint4 g = lrelu_chunk<T>(v[i], slope);
+        if (r < RG)
+          *reinterpret_cast<uint4*>(Gs + r * RS + (cc ^ swz(r)) * 16) = (gr >= 0 && gr < len) ? g : uint4{0u, 0u, 0u, 0u};
       }
     }
   }

@@ -33,35 +33,41 @@ def _headers():
     return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.h"))
 
 
-def _compile(src, force):
-    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+def _compile(src, force, build_dir=BUILD, defines=()):
+    obj = os.path.join(build_dir, os.path.basename(src) + ".o")
     newest_dep = max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _headers()])
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj, False
-    cmd = [HIPCC] + CFLAGS + ["-x", "hip", "-c", src, "-o", obj]
+    cmd = [HIPCC] + CFLAGS + list(defines) + ["-x", "hip", "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-8000:]}")
     return obj, True
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(force: bool = False, verbose: bool = True, variant: str = "", defines=()) -> str:
+    """variant/defines: an A/B build (-D tunables) into build_<variant>/ and
+    libtts_hip_<variant>.so, loaded with TTS_LIB=<path> (tools/ab.sh); the product is LIB."""
+    build_dir = BUILD + ("_" + variant if variant else "")
+    lib = LIB if not variant else os.path.join(PKG, f"libtts_hip_{variant}.so")
+    os.makedirs(build_dir, exist_ok=True)
     srcs = _sources()
     jobs = min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(jobs) as ex:
-        results = list(ex.map(lambda s: _compile(s, force), srcs))
+        results = list(ex.map(lambda s: _compile(s, force, build_dir, defines), srcs))
     objs = [o for o, _ in results]
     rebuilt = any(r for _, r in results)
-    if rebuilt or not os.path.exists(LIB) or force:
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
+    if rebuilt or not os.path.exists(lib) or force:
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")
         if verbose:
-            print(f"[gonova_tts_amd] built {LIB}")
-    return LIB
+            print(f"[gonova_tts_amd] built {lib}")
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    a = sys.argv[1:]
+    var = a[a.index("--variant") + 1] if "--variant" in a else ""
+    build(force="--force" in a or bool(var), variant=var, defines=[x for x in a if x.startswith("-D")])

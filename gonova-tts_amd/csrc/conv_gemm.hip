@@ -265,7 +265,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
 // stride CG*2+16 bytes (an odd number of 16-byte slots: conflict-free ds_read_b128 of 32
 // consecutive rows).
 constexpr int XRES_HR = 64;            // output rows per N-wave staged per half
-constexpr int XRES_SU = 4;             // X staging loads in flight per thread
+constexpr int XRES_SU = 4;             // X staging loads in flight per thread (more spills: acc + ring are live)
 
 template <typename T>
 __device__ inline void ld8(const T* p, f32x4& a, f32x4& b) {

@@ -62,6 +62,14 @@ static bool mrf_fused_enabled() {
   const char* e = getenv("TTS_MRF_FUSED");
   return e ? atoi(e) != 0 : true;
 }
+// resblock chain kernel for the HBM-bound resblocks (default on; TTS_MRF_CHAIN=0: pairs only)
+#ifndef TTS_MRF_CHAIN_DEFAULT
+#define TTS_MRF_CHAIN_DEFAULT 1
+#endif
+static bool mrf_chain_enabled() {
+  const char* e = getenv("TTS_MRF_CHAIN");
+  return e ? atoi(e) != 0 : TTS_MRF_CHAIN_DEFAULT != 0;
+}
 // fused MRF flavour: pair kernels (default) or the whole-stage kernel (TTS_MRF_PAIR=0)
 static bool mrf_pair_enabled() {
   const char* e = getenv("TTS_MRF_PAIR");
@@ -397,6 +405,31 @@ struct tts_engine {
         for (int j = 0; j < nk; ++j) {
           const auto& blk = v.mrf[i][j];
           const int np = (int)blk.size();
+          int dil[4] = {0, 0, 0, 0};
+          for (int q = 0; q < np && q < 4; ++q) dil[q] = blk[q][0].dil;
+          if (mrf_chain_enabled() && mrf_chain_supported(dt, ch, blk[0][0].taps, dil, np)) {
+            // the whole resblock in one launch (HBM-bound resblocks: k = 3 at C <= 64, k = 7 at C = 32)
+            MrfChainParams cp{};
+            cp.x = XS; cp.y = S; cp.len = Lp(i + 1);
+            for (int q = 0; q < 3; ++q) {
+              cp.w1[q] = blk[q][0].wpk16; cp.w2[q] = blk[q][1].wpk16;
+              cp.b1[q] = blk[q][0].bias; cp.b2[q] = blk[q][1].bias;
+            }
+            cp.T = Tout; cp.B = B; cp.slope = slope;
+            cp.accum = j > 0 ? 1 : 0;
+            cp.scale = j == nk - 1 ? 1.0f / (float)nk : 1.f;
+            const double fl = 2.0 * 2.0 * ch * (double)ch * blk[0][0].taps * (double)B * Tout * np;
+            if (prof.on) {
+              Profiler::Rec r{prof.get(), prof.get(), fl, PK_MRF_CHAIN};
+              HIP_CHECK(hipEventRecord(r.a, s));
+              HIP_CHECK(mrf_chain_launch(dt, ch, blk[0][0].taps, cp, s));
+              HIP_CHECK(hipEventRecord(r.b, s));
+              prof.recs.push_back(r);
+            } else {
+              HIP_CHECK(mrf_chain_launch(dt, ch, blk[0][0].taps, cp, s));
+            }
+            continue;
+          }
           const void* h = XS;
           for (int q = 0; q < np; ++q) {
             const bool last = q == np - 1;

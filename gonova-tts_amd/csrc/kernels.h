@@ -38,7 +38,7 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why);
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s);
 
 // kernel family a launch runs as (live profiling buckets; tts_engine_profile_read_kinds)
-enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_MRF_FUSED = 2, PK_MRF_PAIR = 3, PK_N = 4 };
+enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_MRF_FUSED = 2, PK_MRF_PAIR = 3, PK_MRF_CHAIN = 4, PK_N = 5 };
 int conv_gemm_kind(int dtype, const ConvParams& p);
 
 // Fused MRF stage (mrf_fused.hip): all resblocks of one HiFi-GAN stage in one launch.
@@ -79,6 +79,23 @@ struct MrfPairParams {
 };
 bool mrf_pair_supported(int dtype, int C, int k);
 hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s);
+
+// Fused resblock (mrf_chain.hip): the three pairs of one resblock (dilations 1, 3, 5) in one
+// launch; y = ((accum ? y : 0) + resblock(x)) * scale.  Bit-identical to three pair launches.
+struct MrfChainParams {
+  const void* x;          // [B][T][C] resblock input, compute dtype
+  void* y;                // [B][T][C] MRF sum S; never aliases x
+  const int* len;
+  const void* w1[3];      // per pair: conv1 / conv2 weights, frag_pack16
+  const void* w2[3];
+  const float* b1[3];
+  const float* b2[3];
+  int T, B;
+  float slope, scale;
+  int accum;
+};
+bool mrf_chain_supported(int dtype, int C, int k, const int* dil, int npair);
+hipError_t mrf_chain_launch(int dtype, int C, int k, const MrfChainParams& p, hipStream_t s);
 
 int mrf_fused_taps_per_group(int C);
 int mrf_fused_bn(int C);

@@ -1,0 +1,306 @@
+// Fused HiFi-GAN resblock: the three ResBlock pairs of one resblock (dilations 1, 3, 5) in
+// one launch, for the resblocks whose pair kernels are HBM-bound (k = 3 at C = 32 / 64,
+// k = 7 at C = 32):
+//
+//   h0 = x;  for p in 0..2:  t = lrelu(conv_{k,d_p}(lrelu(h_p)) + b1_p)
+//                            h_{p+1} = conv_{k,1}(t) + b2_p + h_p
+//   y = ((accum ? y : 0) + h_3) * scale                       (oracle: vocoder.resblock)
+//
+// Three pair launches move [rows][C] through HBM six times (read h, write h' per pair, the
+// first pair's halo from L2); here a block reads its x tile once (with the resblock's whole
+// receptive-field halo H0 = a2 * sum(d_p + 1) rows per side) and writes its BN output rows
+// once.  At C = 32 a row is 64 bytes and a k = 3 pair only 12 kFLOP per row, so the pair
+// kernels ran near the HBM rate; the chain trades that traffic for the halo recompute
+// (every conv computes only the rows its successor needs, in 16-row tiles).
+//
+// LDS: two [NRA][C] tiles in the pair kernel's swizzled layout (mrf_tile.h):
+//   Hs: h_p, the residual (raw, in place: each h_{p+1} row is written by the thread that
+//       read h_p there);
+//   GT: G = lrelu(h_p) (conv1's operand), overwritten by T after conv1, overwritten by the
+//       next G after conv2 (barriers between), and by the last conv2's output for the
+//       row pass.
+// Rows are in block coordinates: LDS row r <-> utterance row n0 - H0 + r; rows outside the
+// utterance are zero in G and T after every conv (the unfused convs' zero padding).
+// Arithmetic and rounding order match the pair path (mrf_pair.hip) exactly, so the chain's
+// output is bit-identical to three pair launches.
+#include <type_traits>
+
+#include "common.h"
+#include "kernels.h"
+#include "mrf_tile.h"
+
+namespace tts {
+
+template <int C, int K>
+struct ChainGeom;
+#ifndef TTS_CHAIN_BN32_3
+#define TTS_CHAIN_BN32_3 512
+#endif
+#ifndef TTS_CHAIN_BN32_7
+#define TTS_CHAIN_BN32_7 512
+#endif
+#ifndef TTS_CHAIN_BN64_3
+#define TTS_CHAIN_BN64_3 256
+#endif
+#ifndef TTS_CHAIN_OCC
+#define TTS_CHAIN_OCC 2           // blocks per CU the register budget is sized for
+#endif
+template <>
+struct ChainGeom<32, 3> { static constexpr int BN = TTS_CHAIN_BN32_3; };
+template <>
+struct ChainGeom<32, 7> { static constexpr int BN = TTS_CHAIN_BN32_7; };
+template <>
+struct ChainGeom<64, 3> { static constexpr int BN = TTS_CHAIN_BN64_3; };
+
+constexpr int CHAIN_D0 = 1, CHAIN_D1 = 3, CHAIN_D2 = 5;  // HiFi-GAN V1/V2 dilations
+
+template <int C, int K>
+struct ChainPlan {
+  static constexpr int BN = ChainGeom<C, K>::BN;
+  static constexpr int A = (K - 1) / 2;
+  static constexpr int DIL[3] = {CHAIN_D0, CHAIN_D1, CHAIN_D2};
+  // first row each pair's output must cover (s[3] = H0)
+  static constexpr int s(int p) { return p == 0 ? 0 : s(p - 1) + A * (DIL[p - 1] + 1); }
+  static constexpr int H0 = s(3);
+  static constexpr int NR = BN + 2 * H0;
+  static constexpr int lo1(int p) { return s(p) + A * DIL[p]; }
+  static constexpr int nt1(int p) { return (NR - 2 * lo1(p) + 15) / 16; }
+  static constexpr int lo2(int p) { return s(p + 1); }
+  static constexpr int nt2(int p) { return (NR - 2 * lo2(p) + 15) / 16; }
+  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  // rows touched: staging [0, NR); conv1 reads up to lo1 + 16*nt1 + A*d, conv2 up to lo2 + 16*nt2 + A
+  static constexpr int top(int p) {
+    return cmax(lo1(p) + 16 * nt1(p) + A * DIL[p], lo2(p) + 16 * nt2(p) + A);
+  }
+  static constexpr int NRA = cmax(NR, cmax(top(0), cmax(top(1), top(2))));
+};
+
+template <int C, int K>
+static size_t chain_lds_bytes() {
+  return (size_t)2 * ChainPlan<C, K>::NRA * PairGeom<C>::RS;
+}
+
+// 4 x T: (y + h), rounded as epi_row does for the intermediate h' (scale 1, no accumulate)
+template <typename T>
+__device__ inline uint2 epi_add4(uint2 y, uint2 h) {
+  if constexpr (__is_same(T, half_t)) {
+    const half4 v = *reinterpret_cast<const half4*>(&y) + *reinterpret_cast<const half4*>(&h);
+    return *reinterpret_cast<const uint2*>(&v);
+  } else {
+    const T* ye = reinterpret_cast<const T*>(&y);
+    const T* he = reinterpret_cast<const T*>(&h);
+    T o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (T)((float)ye[e] + (float)he[e]);
+    return *reinterpret_cast<const uint2*>(o);
+  }
+}
+template <typename T>
+__device__ inline uint2 lrelu4(uint2 v, float slope) {
+  const uint4 w = lrelu_chunk<T>(uint4{v.x, v.y, 0u, 0u}, slope);
+  return uint2{w.x, w.y};
+}
+
+template <typename T, int C, int K>
+__global__ __launch_bounds__(256, TTS_CHAIN_OCC) void mrf_chain_kernel(MrfChainParams p) {
+  using G = PairGeom<C>;
+  using P = ChainPlan<C, K>;
+  typedef typename Mfma<T>::frag Frag;
+  constexpr int BN = P::BN, WM = G::WM, WN = G::WN, RS = G::RS, D = G::D, A = P::A;
+  constexpr int NTHR = 256, MT = 2, KS = C / 32, S = K * KS, VPR = C / 8;
+  constexpr int H0 = P::H0, NR = P::NR, NRA = P::NRA;
+  static_assert(WM * WN * 64 == NTHR && WM * 32 == C, "wave grid");
+  static_assert(BN % 16 == 0 && (NR - 2 * P::lo2(2)) == BN, "last conv covers exactly the output rows");
+  auto swz = [](int r) { return ((r * G::SW_MUL) >> G::SW_S) & G::SW_M; };
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Hs = smem;
+  char* GT = smem + NRA * RS;
+
+  const int b = blockIdx.y;
+  const int n0 = blockIdx.x * BN;
+  const int len = min(p.len[b], p.T);
+  if (n0 >= len) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = WM == 1 ? 0 : wave % WM, wn = WN == 1 ? 0 : wave / WM;
+  const int l15 = lane & 15, lq = lane >> 4;
+  const int r0g = n0 - H0;             // utterance row of LDS row 0
+  const float slope = p.slope;
+  const int ch0 = 32 * wm + 4 * lq;    // + 16*mt: this lane's 4 output channels
+  const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
+  auto lds4 = [&](int r, int mt) {     // byte offset of this lane's 4 channels (ch0 + 16 mt) in row r
+    const int cb = (ch0 + 16 * mt) * 2;
+    return r * RS + (((cb >> 4) ^ swz(r)) << 4) + (cb & 15);
+  };
+
+  Frag ring[D][MT];
+  auto preload = [&](const void* w) __attribute__((always_inline)) {
+    const char* wp = reinterpret_cast<const char*>(w) + (long long)(2 * wm) * S * 1024 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+      if (i < S)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) ring[i][mt] = *reinterpret_cast<const Frag*>(wp + ((long long)mt * S + i) * 1024);
+  };
+  preload(p.w1[0]);
+
+  // ---- stage h (Hs) and g = lrelu(h) (GT), zero outside the utterance ----
+  {
+    const int cc = tid % VPR, rr0 = tid / VPR;
+    constexpr int rstep = NTHR / VPR;
+    const T* xc = X + cc * 8;
+    for (int rb = rr0; rb < NR; rb += PAIR_SU * rstep) {
+      uint4 v[PAIR_SU];
+#pragma unroll
+      for (int i = 0; i < PAIR_SU; ++i) {
+        const int gr = min(max(r0g + min(rb + i * rstep, NR - 1), 0), len - 1);
+        v[i] = *reinterpret_cast<const uint4*>(xc + (long long)gr * C);
+      }
+#pragma unroll
+      for (int i = 0; i < PAIR_SU; ++i) {
+        const int r = rb + i * rstep;
+        const int gr = r0g + r;
+        const bool in = gr >= 0 && gr < len;
+        const uint4 h = in ? v[i] : uint4{0u, 0u, 0u, 0u};
+        const uint4 g = lrelu_chunk<T>(h, slope);  // consumed unconditionally (waitcnt)
+        if (r < NR) {
+          const int o = r * RS + ((cc ^ swz(r)) << 4);
+          *reinterpret_cast<uint4*>(Hs + o) = h;
+          *reinterpret_cast<uint4*>(GT + o) = g;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  auto pair = [&](auto PI) __attribute__((always_inline)) {
+    constexpr int Q = decltype(PI)::value;
+    constexpr int DQ = P::DIL[Q];
+    constexpr int LO1 = P::lo1(Q), NT1 = P::nt1(Q), NU1 = (NT1 + WN - 1) / WN;
+    constexpr int LO2 = P::lo2(Q), NT2 = P::nt2(Q), NU2 = (NT2 + WN - 1) / WN;
+    const char* w1 = reinterpret_cast<const char*>(p.w1[Q]) + (long long)(2 * wm) * S * 1024 + lane * 16;
+    const char* w2 = reinterpret_cast<const char*>(p.w2[Q]) + (long long)(2 * wm) * S * 1024 + lane * 16;
+
+    // conv1: T rows [LO1, LO1 + 16 NT1) read G rows (row - A*DQ) + tap*DQ
+    {
+      f32x4 acc1[NU1][MT];
+#pragma unroll
+      for (int u = 0; u < NU1; ++u)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = f32x4{};
+      int tile[NU1];
+#pragma unroll
+      for (int u = 0; u < NU1; ++u) tile[u] = 16 * min(wn + WN * u, NT1 - 1) * RS;
+      const int rb = LO1 - A * DQ + l15;
+      pair_conv<T, C, S, NU1, D>(acc1, ring, w1, GT + rb * RS, DQ * RS, DQ, tile, rb, lq);
+      __builtin_amdgcn_sched_barrier(0);
+      preload(p.w2[Q]);  // conv2's first steps in flight during the epilogue
+      f32x4 bias[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b1[Q] + ch0 + 16 * mt);
+      __syncthreads();  // T overwrites G
+#pragma unroll
+      for (int u = 0; u < NU1; ++u)
+        if (NT1 % WN == 0 || wn + WN * u < NT1) {
+          const int tr = LO1 + 16 * (wn + WN * u) + l15;
+          const int gr = r0g + tr;
+          const bool valid = gr >= 0 && gr < len;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            uint2 pk = epi_conv1<T>(acc1[u][mt], bias[mt], slope);
+            if (!valid) pk = uint2{0u, 0u};
+            *reinterpret_cast<uint2*>(GT + lds4(tr, mt)) = pk;
+          }
+        }
+      __syncthreads();
+    }
+    // conv2: output rows [LO2, LO2 + 16 NT2) read T rows (row - A) + tap
+    {
+      f32x4 acc2[NU2][MT];
+#pragma unroll
+      for (int u = 0; u < NU2; ++u)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = f32x4{};
+      int tile[NU2];
+#pragma unroll
+      for (int u = 0; u < NU2; ++u) tile[u] = 16 * min(wn + WN * u, NT2 - 1) * RS;
+      const int rb = LO2 - A + l15;
+      pair_conv<T, C, S, NU2, D>(acc2, ring, w2, GT + rb * RS, RS, 1, tile, rb, lq);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (Q < 2) preload(p.w1[Q + 1]);
+      f32x4 bias[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2[Q] + ch0 + 16 * mt);
+      __syncthreads();  // T no longer read
+#pragma unroll
+      for (int u = 0; u < NU2; ++u)
+        if (NT2 % WN == 0 || wn + WN * u < NT2) {
+          const int tr = LO2 + 16 * (wn + WN * u) + l15;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const int o = lds4(tr, mt);
+            const uint2 y = epi_conv2<T>(acc2[u][mt], bias[mt]);
+            if constexpr (Q < 2) {
+              const int gr = r0g + tr;
+              const bool valid = gr >= 0 && gr < len;
+              const uint2 h = epi_add4<T>(y, *reinterpret_cast<const uint2*>(Hs + o));
+              *reinterpret_cast<uint2*>(Hs + o) = h;
+              *reinterpret_cast<uint2*>(GT + o) = valid ? lrelu4<T>(h, slope) : uint2{0u, 0u};
+            } else {
+              *reinterpret_cast<uint2*>(GT + o) = y;  // row pass: epi_row(y, h, S)
+            }
+          }
+        }
+      __syncthreads();
+    }
+  };
+  pair(std::integral_constant<int, 0>{});
+  pair(std::integral_constant<int, 1>{});
+  pair(std::integral_constant<int, 2>{});
+
+  // ---- row pass: y = ((accum ? S : 0) + (y2 + h2)) * scale over rows [n0, n0 + BN) ----
+  T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
+  constexpr int NIT = BN * VPR / NTHR;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int idx = tid + it * NTHR;
+    const int o = idx / VPR, c8 = idx % VPR;
+    const int gr = n0 + o;
+    if (gr >= len) continue;
+    const int r = H0 + o;
+    const int off = r * RS + ((c8 ^ swz(r)) << 4);
+    T* dst = Y + (long long)gr * C + c8 * 8;
+    uint4 sv = {};
+    if (p.accum) sv = *reinterpret_cast<const uint4*>(dst);
+    const uint4 y = *reinterpret_cast<const uint4*>(GT + off);
+    const uint4 h = *reinterpret_cast<const uint4*>(Hs + off);
+    *reinterpret_cast<uint4*>(dst) = epi_row<T>(y, h, p.accum, sv, p.scale);
+  }
+}
+
+template <typename T, int C, int K>
+static hipError_t launch_chain_t(const MrfChainParams& p, hipStream_t s) {
+  constexpr int BN = ChainGeom<C, K>::BN;
+  const size_t lds = chain_lds_bytes<C, K>();
+  static_assert(2 * ChainPlan<C, K>::NRA * PairGeom<C>::RS * TTS_CHAIN_OCC <= 160 * 1024, "LDS for TTS_CHAIN_OCC blocks per CU");
+  dim3 grid((p.T + BN - 1) / BN, p.B);
+  hipLaunchKernelGGL((mrf_chain_kernel<T, C, K>), grid, dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+bool mrf_chain_supported(int dtype, int C, int k, const int* dil, int npair) {
+  if (!(dtype == DT_F16 || dtype == DT_BF16) || npair != 3) return false;
+  if (dil[0] != CHAIN_D0 || dil[1] != CHAIN_D1 || dil[2] != CHAIN_D2) return false;
+  return (C == 32 && (k == 3 || k == 7)) || (C == 64 && k == 3);
+}
+
+hipError_t mrf_chain_launch(int dtype, int C, int k, const MrfChainParams& p, hipStream_t s) {
+  const bool f16 = dtype == DT_F16;
+  if (C == 32 && k == 3) return f16 ? launch_chain_t<half_t, 32, 3>(p, s) : launch_chain_t<bf16_t, 32, 3>(p, s);
+  if (C == 32 && k == 7) return f16 ? launch_chain_t<half_t, 32, 7>(p, s) : launch_chain_t<bf16_t, 32, 7>(p, s);
+  if (C == 64 && k == 3) return f16 ? launch_chain_t<half_t, 64, 3>(p, s) : launch_chain_t<bf16_t, 64, 3>(p, s);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace tts

@@ -32,121 +32,11 @@
 // (no barriers inside a conv).  Activation tiles are XOR-swizzled (PairGeom).
 #include "common.h"
 #include "kernels.h"
+#include "mrf_tile.h"
 
 #include <algorithm>
 
 namespace tts {
-
-template <int C>
-struct PairGeom;
-// Activation tiles in LDS: unpadded rows (RS = C*2 bytes), 16-byte chunk c of row r stored
-// at chunk c ^ (((r * SW_MUL) >> SW_S) & SW_M).  Chosen with an LDS bank model of every access
-// (MI355X_MICROARCH.md §LDS lane groups): the MFMA B-fragment ds_read_b128 (16 rows x 4
-// chunks per lane group) and the staging ds_write_b128 are conflict-free; the once-per-tile
-// 8-byte epilogue accesses are 2-way.  (Padded rows of 80/144 B made the B reads 2-way:
-// measured 43-47 % of LDS cycles were bank conflicts.)  The swizzle depends on r mod 8
-// only, so it is shared by every 16-row tile and computed once per tap.  At C = 128 the
-// 256-byte rows are one LDS bank row each; chunk ^ ((2r) & 15) keeps the B reads
-// conflict-free for every tap offset (exhaustive check over r mod 16).
-template <>
-struct PairGeom<32> {
-  static constexpr int BN = 512, WM = 1, WN = 4, RS = 64, SW_MUL = 1, SW_S = 1, SW_M = 3, D = 4;
-};
-template <>
-struct PairGeom<64> {
-  static constexpr int BN = 256, WM = 2, WN = 2, RS = 128, SW_MUL = 1, SW_S = 0, SW_M = 7, D = 4;
-};
-template <>
-struct PairGeom<128> {
-  static constexpr int BN = 128, WM = 4, WN = 1, RS = 256, SW_MUL = 2, SW_S = 0, SW_M = 15, D = 4;
-};
-
-template <typename T>
-struct Mfma16;
-template <>
-struct Mfma16<half_t> {
-  __device__ static inline f32x4 mma(half8 a, half8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-  }
-};
-template <>
-struct Mfma16<bf16_t> {
-  __device__ static inline f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-  }
-};
-
-constexpr int PAIR_SU = 8;       // input-tile loads in flight per thread (one round for every shape)
-
-template <typename T>
-__device__ inline void pair_ld8(const T* p, f32x4& a, f32x4& b) {
-  const uint4 u = *reinterpret_cast<const uint4*>(p);
-  const T* e = reinterpret_cast<const T*>(&u);
-  a = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
-  b = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
-}
-// Epilogue arithmetic.  f16: packed half math after one cvt_pk per pair of accumulators
-// (v_pk_add/mul/max_f16: a fraction of the f32 instruction count; a sum of two f16 values
-// is correctly rounded either way, the bias/slope products differ by <= 1 ulp).  bf16:
-// f32 math, one rounding at the end.
-template <typename T>
-__device__ inline uint2 epi_conv1(f32x4 acc, f32x4 bias, float slope) {  // lrelu(acc + b) -> 4 x T
-  if constexpr (__is_same(T, half_t)) {
-    half4 h = __builtin_convertvector(acc, half4) + __builtin_convertvector(bias, half4);
-    h = __builtin_elementwise_max(h, h * (half_t)slope);
-    return *reinterpret_cast<const uint2*>(&h);
-  } else {
-    f32x4 v = acc + bias;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaxf(v[e], v[e] * slope);  // 0 <= slope <= 1
-    T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
-    return *reinterpret_cast<const uint2*>(o);
-  }
-}
-template <typename T>
-__device__ inline uint2 epi_conv2(f32x4 acc, f32x4 bias) {  // acc + b -> 4 x T
-  if constexpr (__is_same(T, half_t)) {
-    half4 h = __builtin_convertvector(acc, half4) + __builtin_convertvector(bias, half4);
-    return *reinterpret_cast<const uint2*>(&h);
-  } else {
-    const f32x4 v = acc + bias;
-    T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
-    return *reinterpret_cast<const uint2*>(o);
-  }
-}
-// row pass: (y + h (+ s)) * scale on 8 elements
-template <typename T>
-__device__ inline uint4 epi_row(uint4 y, uint4 h, bool acc, uint4 s, float scale) {
-  if constexpr (__is_same(T, half_t)) {
-    half8 v = *reinterpret_cast<const half8*>(&y) + *reinterpret_cast<const half8*>(&h);
-    if (acc) v += *reinterpret_cast<const half8*>(&s);
-    if (scale != 1.0f) v *= (half_t)scale;
-    return *reinterpret_cast<const uint4*>(&v);
-  } else {
-    const T* ye = reinterpret_cast<const T*>(&y);
-    const T* he = reinterpret_cast<const T*>(&h);
-    const T* se = reinterpret_cast<const T*>(&s);
-    T o[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float v = (float)ye[e] + (float)he[e];
-      if (acc) v += (float)se[e];
-      o[e] = (T)(v * scale);
-    }
-    return *reinterpret_cast<const uint4*>(o);
-  }
-}
-
-template <typename T>
-__device__ inline uint2 pack4(f32x4 v) {
-  T e[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
-  return *reinterpret_cast<const uint2*>(e);
-}
-template <typename T>
-__device__ inline void pair_st8(T* p, f32x4 a, f32x4 b) {
-  T e[8] = {(T)a[0], (T)a[1], (T)a[2], (T)a[3], (T)b[0], (T)b[1], (T)b[2], (T)b[3]};
-  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(e);
-}
 
 // LDS bytes of one launch (G tile incl. conv1 overrun rows, T tile; >= fp32 output tile)
 template <int C>
@@ -157,56 +47,6 @@ static size_t pair_lds_bytes(int k, int d) {
   const size_t g = (size_t)(16 * nt1 + 2 * a1) * G::RS;
   const size_t t = (size_t)16 * nt1 * G::RS;
   return std::max(std::max(g, t), (size_t)G::BN * (C * 2 + 16));
-}
-
-// One conv of the pair over NU 16-row tiles per wave: acc[u][mt] += W[mt] x tile u.
-// S = k * KS k-steps, weights streamed through the D-slot register ring (ring[i] holds step
-// i on entry).  The step sequence is compile-time: full groups of D steps in a counted loop
-// (every step reloads its slot D steps ahead), then a peeled last group whose reloads stop
-// at S, then the S % D tail.  Straight-line bodies let the waitcnt pass keep the ring's
-// 2*(D-1) younger loads in flight (a conditional reload made it drain vmcnt to 0 every step).
-// lb: this lane's LDS base (row l15 of the wave's first tile); tstep: LDS bytes per tap;
-// trow: rows per tap (swizzle); tile[u]: byte offset of tile u.
-template <typename T, int C, int S, int NU, int D>
-__device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][2], typename Mfma<T>::frag (&ring)[D][2],
-                                          const char* __restrict__ wp, const char* lb, int tstep, int trow,
-                                          const int (&tile)[NU], int l15, int lq) {
-  using G = PairGeom<C>;
-  using MF = Mfma16<T>;
-  typedef typename Mfma<T>::frag Frag;
-  constexpr int KS = C / 32;
-  constexpr int NG = S / D, REM = S % D;
-  auto step = [&](const int s, const int slot, const bool reload) __attribute__((always_inline)) {
-    const int tap = KS == 1 ? s : s / KS, ks = KS == 1 ? 0 : s % KS;
-    const int r = l15 + tap * trow;
-    const char* bp = lb + tap * tstep + (((lq + 4 * ks) ^ (((r * G::SW_MUL) >> G::SW_S) & G::SW_M)) << 4);
-    Frag bf[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) bf[u] = *reinterpret_cast<const Frag*>(bp + tile[u]);
-#pragma unroll
-    for (int u = 0; u < NU; ++u)
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) acc[u][mt] = MF::mma(ring[slot][mt], bf[u], acc[u][mt]);
-    if (reload) {
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-        ring[slot][mt] = *reinterpret_cast<const Frag*>(wp + ((long long)mt * S + s + D) * 1024);
-      __builtin_amdgcn_sched_barrier(0);  // issue the reload here, D steps ahead of its use
-    }
-  };
-  if constexpr (NG >= 2) {
-#pragma nounroll
-    for (int g = 0; g < NG - 1; ++g) {
-#pragma unroll
-      for (int i = 0; i < D; ++i) step(g * D + i, i, true);
-    }
-  }
-  if constexpr (NG >= 1) {
-#pragma unroll
-    for (int i = 0; i < D; ++i) step((NG - 1) * D + i, i, i < REM);
-  }
-#pragma unroll
-  for (int i = 0; i < REM; ++i) step(NG * D + i, i, false);
 }
 
 template <typename T, int C, int K>

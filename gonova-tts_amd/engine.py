@@ -19,7 +19,8 @@ from typing import Dict, Optional
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libtts_hip.so")
+# TTS_LIB: load an A/B variant build (build.py --variant, tools/ab.sh) instead of the product library
+LIB_PATH = os.environ.get("TTS_LIB") or os.path.join(_PKG, "libtts_hip.so")
 
 DTYPES = {"f32": 0, "fp32": 0, "float32": 0, "f16": 1, "fp16": 1, "float16": 1, "bf16": 2, "bfloat16": 2}
 
@@ -234,7 +235,7 @@ class HipEngine:
               "profile_read")
         return ms.value, fl.value, n.value
 
-    PROFILE_KINDS = ("conv_gemm_kernel", "conv_xres_kernel", "mrf_fused_kernel", "mrf_pair_kernel")
+    PROFILE_KINDS = ("conv_gemm_kernel", "conv_xres_kernel", "mrf_fused_kernel", "mrf_pair_kernel", "mrf_chain_kernel")
 
     def profile_read_kinds(self):
         """-> {kernel name: (summed ms, algorithmic FLOPs, launch count)}; resets."""

@@ -103,7 +103,8 @@ int tts_acoustic_forward(tts_engine* eng, const int32_t* d_tokens, const int32_t
 int tts_engine_profile(tts_engine* eng, int enable);
 int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops, int* n_launches);
 /* The same, split by kernel family into arrays of nkinds entries:
- * 0 = conv_gemm_kernel, 1 = conv_xres_kernel, 2 = mrf_fused_kernel, 3 = mrf_pair_kernel. */
+ * 0 = conv_gemm_kernel, 1 = conv_xres_kernel, 2 = mrf_fused_kernel, 3 = mrf_pair_kernel,
+ * 4 = mrf_chain_kernel. */
 int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, double* flops, int* n_launches);
 
 /* Thread-local message describing the last failure on this thread. */

@@ -172,3 +172,24 @@ def test_fused_mrf_matches_unfused_path(vw, dtype, pair, monkeypatch):
         e = rel_rms(fused[b, :L * 256], unfused[b, :L * 256])
         assert e <= (2e-3 if dtype == "f16" else 1.5e-2), (b, e)
         assert np.all(fused[b, L * 256:] == 0)
+
+
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_resblock_chain_bit_identical_to_pairs(vw, dtype, monkeypatch):
+    """The resblock chain kernel (three pairs in one launch: k=3 at C=32/64, k=7 at C=32)
+    reproduces the three pair launches bit for bit, ragged utterances and tile edges included
+    (first / last blocks of an utterance, one block shorter than the halo)."""
+    eng = engine_for(dtype, vw)
+    rng = np.random.default_rng(22)
+    lens = [70, 1, 33, 64, 5]
+    mel = torch.from_numpy(rng.standard_normal((5, 70, 80)).astype(np.float32)).to(DEV)
+    ln = torch.tensor(lens, dtype=torch.int32)
+    monkeypatch.setenv("TTS_MRF_FUSED", "1")
+    monkeypatch.setenv("TTS_MRF_PAIR", "1")
+    monkeypatch.setenv("TTS_MRF_CHAIN", "1")
+    chain = eng.vocoder(mel, ln).cpu().numpy()
+    monkeypatch.setenv("TTS_MRF_CHAIN", "0")
+    pairs = eng.vocoder(mel, ln).cpu().numpy()
+    for b, L in enumerate(lens):
+        assert np.array_equal(chain[b], pairs[b]), (b, float(np.abs(chain[b] - pairs[b]).max()))
+        assert np.all(chain[b, L * 256:] == 0)

@@ -10,8 +10,9 @@ bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled; every HB
 these kernels is a 16-byte-per-lane load.  WRITE_SIZE is exact for 16-B stores (conv_xres
 and mrf_fused write 16-B row pieces / 8-B fragments -- the latter uncalibrated, stated).
 
-The last step's launches are mapped onto the step's layer sequence
-  pre, s0.up, 18 x s0 conv, s1.up, 9 x s1 pair, s2.up, 9 x s2 pair, s3.up, 9 x s3 pair, post
+The last step's launches are mapped onto the step's launch sequence (step_launches):
+  pre, s0.up, 18 x s0 conv, then per stage: up, one chain launch per chained resblock
+  (k=3 at C=32/64, k=7 at C=32) or three pair launches, and post
 and each family's traffic is compared with its algorithmic bytes: every conv reads its
 input rows once, its weights once, writes its output once (+ the residual read of a
 ResBlock's second conv); a ResBlock pair reads its input once, writes its output once,
@@ -27,7 +28,7 @@ from collections import defaultdict
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tools.layer_breakdown import vocoder_layers  # noqa: E402
 
-FAMILIES = ("conv_gemm", "conv_xres", "mrf_fused", "mrf_pair", "conv_post")
+FAMILIES = ("conv_gemm", "conv_xres", "mrf_fused", "mrf_pair", "mrf_chain", "conv_post")
 
 
 def family(name):
@@ -49,26 +50,45 @@ def per_dispatch(path, counter):
     return [vals[i] for i in ids], [names[i] for i in ids]
 
 
-def fused_step_layers(B, T, elt=2, pair_channels=(32, 64, 128)):
-    """[(label, algorithmic bytes)] of one default-path step, in launch order: single convs
-    for stages whose width has no pair kernel (C=256), ResBlock-pair launches otherwise."""
+CHAIN = {(32, 3), (32, 7), (64, 3)}   # (C, k) resblocks run as one chain launch (mrf_chain.hip)
+
+
+def step_launches(B, T, elt=2, pair_channels=(32, 64, 128), chain=CHAIN):
+    """[(label, algorithmic bytes, algorithmic FLOPs)] of one default-path step, in launch
+    order: single convs for stages whose width has no pair kernel (C=256), one chain launch
+    per resblock in `chain`, ResBlock-pair launches otherwise."""
     out = []
+    npairs = {}
     for name, M, cin, k, n in vocoder_layers(T):
         st = name.split(".")[0]
+        f = 2.0 * M * cin * k * n * B
         if name == "post":
-            out.append(("post", B * n * cin * elt + B * n * 4))
+            out.append(("post", B * n * cin * elt + B * n * 4, f))
         elif name == "pre" or name.endswith(".up"):
-            out.append((name, B * n * cin * elt + B * n * M * elt + M * cin * k * elt))
+            out.append((name, B * n * cin * elt + B * n * M * elt + M * cin * k * elt, f))
         elif M in pair_channels:
-            if name.endswith(".c2"):  # one pair launch per (c1, c2)
-                idx = sum(1 for lab, _ in out if lab.startswith(st + ".pair"))
-                accum = idx % 3 == 2 and idx >= 3   # last pair of the 2nd/3rd resblock adds S
-                act = B * n * M * elt
-                out.append((f"{st}.pair{idx}", 2 * act + (act if accum else 0) + 2 * M * cin * k * elt))
+            if not name.endswith(".c2"):
+                continue
+            idx = npairs.get(st, 0)   # pair index within the stage (3 per resblock)
+            npairs[st] = idx + 1
+            accum = idx >= 3          # the 2nd/3rd resblock's output adds the running MRF sum
+            act = B * n * M * elt
+            if (M, k) in chain:
+                if idx % 3 == 2:      # the chain launch, counted at its resblock's last pair
+                    out.append((f"{st}.k{k}.chain", 2 * act + (act if accum else 0) + 6 * M * cin * k * elt,
+                                3 * 2 * f))
+            else:
+                out.append((f"{st}.pair{idx}", 2 * act + (act if accum and idx % 3 == 2 else 0)
+                            + 2 * M * cin * k * elt, 2 * f))
         else:
             r = B * n * M * elt if name.endswith(".c2") else 0
-            out.append((name, B * n * cin * elt + B * n * M * elt + M * cin * k * elt + r))
+            out.append((name, B * n * cin * elt + B * n * M * elt + M * cin * k * elt + r, f))
     return out
+
+
+def fused_step_layers(B, T, elt=2, pair_channels=(32, 64, 128)):
+    """[(label, algorithmic bytes)] of one default-path step, in launch order."""
+    return [(lab, by) for lab, by, _ in step_launches(B, T, elt, pair_channels)]
 
 
 def main():

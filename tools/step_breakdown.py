@@ -11,24 +11,7 @@ import sys
 from collections import OrderedDict
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from tools.layer_breakdown import vocoder_layers  # noqa: E402
-from tools.pmc_traffic import family, fused_step_layers  # noqa: E402
-
-
-def launch_flops(B, T, pair_channels=(32, 64, 128)):
-    """Algorithmic FLOPs of each launch of one default-path step, in launch order."""
-    out = []
-    pairs = {}
-    for name, M, cin, k, n in vocoder_layers(T):
-        st = name.split(".")[0]
-        f = 2.0 * M * cin * k * n * B
-        if M in pair_channels and name.endswith((".c1", ".c2")):
-            if name.endswith(".c2"):  # one launch per (c1, c2)
-                pairs[st] = pairs.get(st, 0) + 1
-                out.append(2 * f)
-        else:
-            out.append(f)
-    return out
+from tools.pmc_traffic import family, step_launches  # noqa: E402
 
 
 def main():
@@ -37,13 +20,12 @@ def main():
     T = int(sys.argv[3]) if len(sys.argv) > 3 else 862
     rows = [r for r in csv.DictReader(open(path)) if family(r["Kernel_Name"])]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    step = fused_step_layers(B, T)
+    step = step_launches(B, T)
     rows = rows[-len(step):]
-    fl = launch_flops(B, T)
     stage = OrderedDict()
     total = 0.0
     print(f"{'launch':12s} {'kernel':10s} {'us':>9s} {'TF/s':>8s}")
-    for (lab, _), r, f in zip(step, rows, fl):
+    for (lab, _, f), r in zip(step, rows):
         us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         total += us
         s = stage.setdefault(lab.split(".")[0], [0.0, 0.0])

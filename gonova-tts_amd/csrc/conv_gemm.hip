@@ -265,7 +265,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
 // stride CG*2+16 bytes (an odd number of 16-byte slots: conflict-free ds_read_b128 of 32
 // consecutive rows).
 constexpr int XRES_HR = 64;            // output rows per N-wave staged per half
-constexpr int XRES_SU = 4;             // X staging loads in flight per thread (more spills: acc + ring are live)
+#ifndef TTS_XRES_OCC
+#define TTS_XRES_OCC 3                 // blocks per CU (register budget; LDS tile cap below)
+#endif
+#ifndef TTS_XRES_SU
+#define TTS_XRES_SU 4                  // more spills at 3 blocks/CU: acc + ring are live
+#endif
+constexpr int XRES_SU = TTS_XRES_SU;   // X staging loads in flight per thread
 
 template <typename T>
 __device__ inline void ld8(const T* p, f32x4& a, f32x4& b) {
@@ -281,7 +287,7 @@ __device__ inline void st8(T* p, f32x4 a, f32x4 b) {
 }
 
 template <typename T, int NT, int WM>
-__global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG) {
+__global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams p, int CG) {
   using MF = Mfma<T>;
   typedef typename MF::frag Frag;
   static_assert(sizeof(T) == 2, "16-bit dtypes only");
@@ -483,7 +489,7 @@ __global__ __launch_bounds__(256, 3) void conv_xres_kernel(ConvParams p, int CG)
   }
 }
 
-constexpr int XRES_LDS_MAX = 53 * 1024;  // 3 blocks per CU
+constexpr int XRES_LDS_MAX = (160 / TTS_XRES_OCC - 1) * 1024;  // TTS_XRES_OCC blocks per CU (53 KB at 3)
 
 // channel group for the X-resident kernel: largest power-of-two CG | Cin, CG >= 64, tile within
 // XRES_LDS_MAX; 0 = not eligible

@@ -33,24 +33,34 @@ namespace tts {
 
 template <int C, int K>
 struct ChainGeom;
+// Rows per block and blocks per CU (LDS 2 * NRA * C * 2 bytes per block, registers sized for
+// OCC blocks) per (C, k); tuned by same-box A/B (tools/ab.sh).
 #ifndef TTS_CHAIN_BN32_3
-#define TTS_CHAIN_BN32_3 512
+#define TTS_CHAIN_BN32_3 256
 #endif
 #ifndef TTS_CHAIN_BN32_7
-#define TTS_CHAIN_BN32_7 512
+#define TTS_CHAIN_BN32_7 320
 #endif
 #ifndef TTS_CHAIN_BN64_3
-#define TTS_CHAIN_BN64_3 256
+#define TTS_CHAIN_BN64_3 128
 #endif
-#ifndef TTS_CHAIN_OCC
-#define TTS_CHAIN_OCC 2           // blocks per CU the register budget is sized for
+#ifndef TTS_CHAIN_BN64_7
+#define TTS_CHAIN_BN64_7 128
+#endif
+#ifndef TTS_CHAIN_OCC64_7
+#define TTS_CHAIN_OCC64_7 2
+#endif
+#ifndef TTS_CHAIN_C64K7
+#define TTS_CHAIN_C64K7 0          // chain the k = 7 resblock at C = 64 too
 #endif
 template <>
-struct ChainGeom<32, 3> { static constexpr int BN = TTS_CHAIN_BN32_3; };
+struct ChainGeom<32, 3> { static constexpr int BN = TTS_CHAIN_BN32_3, OCC = 3; };
 template <>
-struct ChainGeom<32, 7> { static constexpr int BN = TTS_CHAIN_BN32_7; };
+struct ChainGeom<32, 7> { static constexpr int BN = TTS_CHAIN_BN32_7, OCC = 3; };
 template <>
-struct ChainGeom<64, 3> { static constexpr int BN = TTS_CHAIN_BN64_3; };
+struct ChainGeom<64, 3> { static constexpr int BN = TTS_CHAIN_BN64_3, OCC = 3; };
+template <>
+struct ChainGeom<64, 7> { static constexpr int BN = TTS_CHAIN_BN64_7, OCC = TTS_CHAIN_OCC64_7; };
 
 constexpr int CHAIN_D0 = 1, CHAIN_D1 = 3, CHAIN_D2 = 5;  // HiFi-GAN V1/V2 dilations
 
@@ -102,7 +112,7 @@ __device__ inline uint2 lrelu4(uint2 v, float slope) {
 }
 
 template <typename T, int C, int K>
-__global__ __launch_bounds__(256, TTS_CHAIN_OCC) void mrf_chain_kernel(MrfChainParams p) {
+__global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(MrfChainParams p) {
   using G = PairGeom<C>;
   using P = ChainPlan<C, K>;
   typedef typename Mfma<T>::frag Frag;
@@ -283,7 +293,7 @@ template <typename T, int C, int K>
 static hipError_t launch_chain_t(const MrfChainParams& p, hipStream_t s) {
   constexpr int BN = ChainGeom<C, K>::BN;
   const size_t lds = chain_lds_bytes<C, K>();
-  static_assert(2 * ChainPlan<C, K>::NRA * PairGeom<C>::RS * TTS_CHAIN_OCC <= 160 * 1024, "LDS for TTS_CHAIN_OCC blocks per CU");
+  static_assert(2 * ChainPlan<C, K>::NRA * PairGeom<C>::RS * ChainGeom<C, K>::OCC <= 160 * 1024, "LDS for OCC blocks per CU");
   dim3 grid((p.T + BN - 1) / BN, p.B);
   hipLaunchKernelGGL((mrf_chain_kernel<T, C, K>), grid, dim3(256), lds, s, p);
   return hipGetLastError();
@@ -292,7 +302,7 @@ static hipError_t launch_chain_t(const MrfChainParams& p, hipStream_t s) {
 bool mrf_chain_supported(int dtype, int C, int k, const int* dil, int npair) {
   if (!(dtype == DT_F16 || dtype == DT_BF16) || npair != 3) return false;
   if (dil[0] != CHAIN_D0 || dil[1] != CHAIN_D1 || dil[2] != CHAIN_D2) return false;
-  return (C == 32 && (k == 3 || k == 7)) || (C == 64 && k == 3);
+  return (C == 32 && (k == 3 || k == 7)) || (C == 64 && (k == 3 || (TTS_CHAIN_C64K7 && k == 7)));
 }
 
 hipError_t mrf_chain_launch(int dtype, int C, int k, const MrfChainParams& p, hipStream_t s) {
@@ -300,6 +310,9 @@ hipError_t mrf_chain_launch(int dtype, int C, int k, const MrfChainParams& p, hi
   if (C == 32 && k == 3) return f16 ? launch_chain_t<half_t, 32, 3>(p, s) : launch_chain_t<bf16_t, 32, 3>(p, s);
   if (C == 32 && k == 7) return f16 ? launch_chain_t<half_t, 32, 7>(p, s) : launch_chain_t<bf16_t, 32, 7>(p, s);
   if (C == 64 && k == 3) return f16 ? launch_chain_t<half_t, 64, 3>(p, s) : launch_chain_t<bf16_t, 64, 3>(p, s);
+#if TTS_CHAIN_C64K7
+  if (C == 64 && k == 7) return f16 ? launch_chain_t<half_t, 64, 7>(p, s) : launch_chain_t<bf16_t, 64, 7>(p, s);
+#endif
   return hipErrorInvalidValue;
 }
 

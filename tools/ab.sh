@@ -5,7 +5,8 @@
 # trace + per-launch breakdown per build.  Box-to-box clock differences (~5 %) exceed most
 # single-change effects, so compare only within one call.
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/$1; shift; mkdir -p $O
-LIBS="$R/gonova-tts_amd/libtts_hip.so $*"
+LIBS="$R/gonova-tts_amd/libtts_hip.so"
+for L in "$@"; do case $L in /*) LIBS="$LIBS $L";; *) LIBS="$LIBS $R/$L";; esac; done
 for rep in 1 2; do
   for L in $LIBS; do
     n=$(basename $L .so)

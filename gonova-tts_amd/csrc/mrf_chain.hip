@@ -184,6 +184,10 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
   }
   __syncthreads();
 
+  T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
+  constexpr int NIT = BN * VPR / NTHR;
+  static_assert(BN * VPR % NTHR == 0, "row pass");
+  uint4 sin[NIT];
   auto pair = [&](auto PI) __attribute__((always_inline)) {
     constexpr int Q = decltype(PI)::value;
     constexpr int DQ = P::DIL[Q];
@@ -238,7 +242,17 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
       const int rb = LO2 - A + l15;
       pair_conv<T, C, S, NU2, D>(acc2, ring, w2, GT + rb * RS, RS, 1, tile, rb, lq);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (Q < 2) preload(p.w1[Q + 1]);
+      if constexpr (Q < 2) {
+        preload(p.w1[Q + 1]);
+      } else {  // MRF-sum rows in flight during the last epilogue (no records: not accumulating)
+        const auto yrsrc = __builtin_amdgcn_make_buffer_rsrc(Y, 0, p.accum ? len * C * (int)sizeof(T) : 0, 0x00020000);
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          const int idx = tid + it * NTHR;
+          const int e = min(n0 + idx / VPR, len - 1) * C + (idx % VPR) * 8;
+          sin[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrsrc, e * (int)sizeof(T), 0, 0));
+        }
+      }
       f32x4 bias[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2[Q] + ch0 + 16 * mt);
@@ -270,8 +284,6 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
   pair(std::integral_constant<int, 2>{});
 
   // ---- row pass: y = ((accum ? S : 0) + (y2 + h2)) * scale over rows [n0, n0 + BN) ----
-  T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
-  constexpr int NIT = BN * VPR / NTHR;
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int idx = tid + it * NTHR;
@@ -281,11 +293,9 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
     const int r = H0 + o;
     const int off = r * RS + ((c8 ^ swz(r)) << 4);
     T* dst = Y + (long long)gr * C + c8 * 8;
-    uint4 sv = {};
-    if (p.accum) sv = *reinterpret_cast<const uint4*>(dst);
     const uint4 y = *reinterpret_cast<const uint4*>(GT + off);
     const uint4 h = *reinterpret_cast<const uint4*>(Hs + off);
-    *reinterpret_cast<uint4*>(dst) = epi_row<T>(y, h, p.accum, sv, p.scale);
+    *reinterpret_cast<uint4*>(dst) = epi_row<T>(y, h, p.accum, sin[it], p.scale);
   }
 }
 

@@ -34,6 +34,10 @@
 #include "kernels.h"
 #include "mrf_tile.h"
 
+#ifndef TTS_PAIR_PROBE
+#define TTS_PAIR_PROBE 0  // timing-only probes for A/B builds (results invalid): 1 no staging loads, 2 no weight reloads
+#endif
+
 #include <algorithm>
 
 namespace tts {
@@ -111,7 +115,12 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
         uint4 v[PAIR_SU];
 #pragma unroll
         for (int i = 0; i < PAIR_SU; ++i)
+#if TTS_PAIR_PROBE & 1  // timing-only probe: no staging loads (pseudo-random f16 payload)
+          { const unsigned z = (unsigned)(rb + i * rstep + cc * 977 + n0) * 2654435761u;
+            v[i] = uint4{z & 0xB7FF37FFu, (z >> 3) & 0x37FFB7FFu, (z >> 5) & 0xB7FF37FFu, (z >> 7) & 0x37FFB7FFu}; }
+#else
           v[i] = *reinterpret_cast<const uint4*>(xc + (long long)(gs + min(rb + i * rstep, RG - 1)) * C);
+#endif
 #pragma unroll
         for (int i = 0; i < PAIR_SU; ++i) {
           const int r = rb + i * rstep;
@@ -183,7 +192,6 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   __syncthreads();
 
   constexpr int NIT = BN * VPR / NTHR;  // 16-byte row pieces per thread in the row pass
-  T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
 
   // ---- conv2 over the BN output rows: output row o reads T rows o .. o + 2*a2 ----
   f32x4 acc2[NU2][MT];
@@ -198,13 +206,19 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     pair_conv<T, C, S, NU2, D>(acc2, ring, w2, Ts + l15 * RS, RS, 1, tile, l15, lq);
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the epilogue's loads out of the MFMA tail
-  // residual h (input rows) in flight while the tile is staged (the MRF-sum rows of
-  // accumulating launches are read in the row pass: prefetching both spills)
-  uint4 xin[NIT];
+  // residual h (input rows) and, for accumulating launches, the MRF-sum rows in flight while
+  // the tile is staged.  The sum is read through a buffer descriptor with no records when the
+  // launch does not accumulate: the load is issued unconditionally (no branch for the waitcnt
+  // pass) and fetches nothing.
+  T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
+  const auto yrsrc = __builtin_amdgcn_make_buffer_rsrc(Y, 0, p.accum ? len * C * (int)sizeof(T) : 0, 0x00020000);
+  uint4 xin[NIT], sin[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int idx = tid + it * NTHR;
-    xin[it] = *reinterpret_cast<const uint4*>(X + (long long)min(n0 + idx / VPR, len - 1) * C + (idx % VPR) * 8);
+    const int e = min(n0 + idx / VPR, len - 1) * C + (idx % VPR) * 8;
+    xin[it] = *reinterpret_cast<const uint4*>(X + e);
+    sin[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrsrc, e * (int)sizeof(T), 0, 0));
   }
   f32x4 bias[MT];
 #pragma unroll
@@ -226,9 +240,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     if (gr >= len) continue;
     T* dst = Y + (long long)gr * C + c8 * 8;
     const uint4 y = *reinterpret_cast<const uint4*>(smem + o * YS16 + c8 * 16);
-    uint4 sv = {};
-    if (p.accum) sv = *reinterpret_cast<const uint4*>(dst);
-    *reinterpret_cast<uint4*>(dst) = epi_row<T>(y, xin[it], p.accum, sv, p.scale);
+    *reinterpret_cast<uint4*>(dst) = epi_row<T>(y, xin[it], p.accum, sin[it], p.scale);
   }
 }
 

@@ -148,7 +148,11 @@ __device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][2], typename Mfma<T>:
     for (int u = 0; u < NU; ++u)
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) acc[u][mt] = MF::mma(ring[slot][mt], bf[u], acc[u][mt]);
+#if defined(TTS_PAIR_PROBE) && (TTS_PAIR_PROBE & 2)
+    if (false) {
+#else
     if (reload) {
+#endif
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
         ring[slot][mt] = *reinterpret_cast<const Frag*>(wp + ((long long)mt * S + s + D) * 1024);

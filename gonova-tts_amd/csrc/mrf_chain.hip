@@ -126,8 +126,9 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
   char* Hs = smem;
   char* GT = smem + NRA * RS;
 
-  const int b = blockIdx.y;
-  const int n0 = blockIdx.x * BN;
+  int b, tile0;
+  if (!xcd_tile((p.T + BN - 1) / BN, p.B, b, tile0)) return;
+  const int n0 = tile0 * BN;
   const int len = min(p.len[b], p.T);
   if (n0 >= len) return;
   const int tid = threadIdx.x;
@@ -304,7 +305,7 @@ static hipError_t launch_chain_t(const MrfChainParams& p, hipStream_t s) {
   constexpr int BN = ChainGeom<C, K>::BN;
   const size_t lds = chain_lds_bytes<C, K>();
   static_assert(2 * ChainPlan<C, K>::NRA * PairGeom<C>::RS * ChainGeom<C, K>::OCC <= 160 * 1024, "LDS for OCC blocks per CU");
-  dim3 grid((p.T + BN - 1) / BN, p.B);
+  dim3 grid(xcd_grid((p.T + BN - 1) / BN, p.B));
   hipLaunchKernelGGL((mrf_chain_kernel<T, C, K>), grid, dim3(256), lds, s, p);
   return hipGetLastError();
 }

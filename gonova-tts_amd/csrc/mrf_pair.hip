@@ -76,8 +76,9 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   static_assert(2 * A2 <= 16, "conv1 overrun within one tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int b = blockIdx.y;
-  const int n0 = blockIdx.x * BN;
+  int b, tile0;
+  if (!xcd_tile((p.T + BN - 1) / BN, p.B, b, tile0)) return;
+  const int n0 = tile0 * BN;
   const int len = min(p.len[b], p.T);
   if (n0 >= len) return;
   const int tid = threadIdx.x;
@@ -249,7 +250,7 @@ static hipError_t launch_pair_t(const MrfPairParams& p, hipStream_t s) {
   using G = PairGeom<C>;
   const size_t lds = pair_lds_bytes<C>(K, p.d);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  dim3 grid((p.T + G::BN - 1) / G::BN, p.B);
+  dim3 grid(xcd_grid((p.T + G::BN - 1) / G::BN, p.B));
   hipLaunchKernelGGL((mrf_pair_kernel<T, C, K>), grid, dim3(256), lds, s, p);
   return hipGetLastError();
 }

@@ -48,6 +48,34 @@ struct Mfma16<bf16_t> {
 #ifndef TTS_PAIR_SU
 #define TTS_PAIR_SU 12
 #endif
+#ifndef TTS_XCD_REMAP
+#define TTS_XCD_REMAP 1
+#endif
+// XCD-aware tile order for a 1-D grid of nx row tiles x B utterances.  Workgroups are dealt to
+// the 8 XCDs round robin in dispatch order, so adjacent row tiles (which share halo rows)
+// would land on 8 different L2s; here XCD x gets the contiguous tile range
+// [x * per, (x + 1) * per) of the (utterance, tile) sequence.  Returns false for the padding
+// workgroups of the last range.
+__device__ inline bool xcd_tile(int nx, int B, int& b, int& tile) {
+  const int total = nx * B;
+  int v = blockIdx.x;
+#if TTS_XCD_REMAP
+  const int per = (total + 7) / 8;
+  v = (v & 7) * per + (v >> 3);
+#endif
+  if (v >= total) return false;
+  b = v / nx;
+  tile = v - b * nx;
+  return true;
+}
+inline int xcd_grid(int nx, int B) {
+#if TTS_XCD_REMAP
+  return 8 * ((nx * B + 7) / 8);
+#else
+  return nx * B;
+#endif
+}
+
 constexpr int PAIR_SU = TTS_PAIR_SU;  // input-tile loads in flight per thread (one round for every pair shape up to k = 11)
 
 template <typename T>

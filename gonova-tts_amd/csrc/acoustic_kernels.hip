@@ -211,6 +211,68 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const T* __restrict__ a
   }
 }
 
+// The same with a compile-time kernel size (the conformer's 7 / 31): 16-byte GLU loads
+// (8 x 16-bit or 4 x f32 channels of x and of the gate per load), and a register sliding
+// window per thread: one channel x RPT consecutive rows reads RPT + K - 1 LDS values for
+// RPT * K FMAs (the generic kernel above reads K LDS values per output).  HBM-bound: reads
+// the [rows][2D] GLU input once (+ halo), writes [rows][D] once.
+template <typename T, int K>
+__global__ __launch_bounds__(256) void glu_dwconv_k_kernel(const T* __restrict__ a, const int* __restrict__ lens,
+                                                          int Tm, int D, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, T* __restrict__ out) {
+  constexpr int TR = 128, CB = 64, RPT = TR / 4, PAD = (K - 1) / 2, ROWS = TR + K - 1;
+  constexpr int EPP = 16 / (int)sizeof(T);   // channels per 16-byte piece
+  constexpr int PPR = CB / EPP;              // pieces per staged row
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* g = reinterpret_cast<float*>(smem);  // [ROWS][CB] GLU output, fp32
+  const int b = blockIdx.z;
+  const int t0 = blockIdx.x * TR;
+  const int c0 = blockIdx.y * CB;
+  const int L = min(lens[b], Tm);
+  if (t0 >= L) return;
+  const T* ab = a + (long long)b * Tm * 2 * D;
+  for (int i = threadIdx.x; i < ROWS * PPR; i += 256) {
+    const int r = i / PPR, pc = i - r * PPR;
+    const int t = t0 - PAD + r;
+    const int c = c0 + pc * EPP;
+    float v[EPP];
+    if (t >= 0 && t < L && c < D) {
+      const uint4 xu = *reinterpret_cast<const uint4*>(ab + (long long)t * 2 * D + c);
+      const uint4 gu = *reinterpret_cast<const uint4*>(ab + (long long)t * 2 * D + D + c);
+      const T* xe = reinterpret_cast<const T*>(&xu);
+      const T* ge = reinterpret_cast<const T*>(&gu);
+#pragma unroll
+      for (int e = 0; e < EPP; ++e) v[e] = to_f32(xe[e]) * (1.f / (1.f + __expf(-to_f32(ge[e]))));
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPP; ++e) v[e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < EPP; e += 4)
+      *reinterpret_cast<f32x4*>(g + r * CB + pc * EPP + e) = f32x4{v[e], v[e + 1], v[e + 2], v[e + 3]};
+  }
+  __syncthreads();
+  const int c = threadIdx.x & (CB - 1);
+  const int r0 = (threadIdx.x / CB) * RPT;
+  if (c0 + c >= D || t0 + r0 >= L) return;
+  float wk[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) wk[j] = w[(long long)(c0 + c) * K + j];
+  const float bc = bias[c0 + c];
+  float win[RPT + K - 1];
+#pragma unroll
+  for (int i = 0; i < RPT + K - 1; ++i) win[i] = g[(r0 + i) * CB + c];
+  T* ob = out + (long long)b * Tm * D + c0 + c;
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    float acc = bc;
+#pragma unroll
+    for (int j = 0; j < K; ++j) acc = fmaf(wk[j], win[r + j], acc);
+    const int t = t0 + r0 + r;
+    if (t < L) ob[(long long)t * D] = from_f32<T>(acc / (1.f + __expf(-acc)));  // SiLU
+  }
+}
+
 // ---------------------------------------------------------------------------
 // variance-predictor head: LayerNorm(C) then Linear(C -> 1) (HF:261-271, 318)
 // ---------------------------------------------------------------------------
@@ -410,6 +472,16 @@ hipError_t launch_rel_softmax(int dt, const void* ac, const void* bd, const int*
 hipError_t launch_glu_dwconv(int dt, const void* a, const int* lens, int B, int Tm, int D, const float* w, int k,
                              const float* bias, void* out, hipStream_t s) {
   dim3 grid((Tm + 127) / 128, (D + 63) / 64, B);
+  const int epp = dt == DT_F32 ? 4 : 8;
+  if ((k == 7 || k == 31) && D % epp == 0) {
+    const size_t ldsk = (size_t)(128 + k - 1) * 64 * 4;
+    if (k == 7) {  // (TTS_DISPATCH returns)
+      TTS_DISPATCH(dt, hipLaunchKernelGGL((glu_dwconv_k_kernel<TT, 7>), grid, dim3(256), ldsk, s, (const TT*)a, lens,
+                                          Tm, D, w, bias, (TT*)out));
+    }
+    TTS_DISPATCH(dt, hipLaunchKernelGGL((glu_dwconv_k_kernel<TT, 31>), grid, dim3(256), ldsk, s, (const TT*)a, lens,
+                                        Tm, D, w, bias, (TT*)out));
+  }
   const size_t lds = (size_t)(128 + k - 1) * 64 * 4;
   TTS_DISPATCH(dt, hipLaunchKernelGGL(glu_dwconv_kernel<TT>, grid, dim3(256), lds, s, (const TT*)a, lens, Tm, D, w, k,
                                       bias, (TT*)out));

@@ -265,6 +265,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
 // stride CG*2+16 bytes (an odd number of 16-byte slots: conflict-free ds_read_b128 of 32
 // consecutive rows).
 constexpr int XRES_HR = 64;            // output rows per N-wave staged per half
+#ifndef TTS_XRES_PROBE
+#define TTS_XRES_PROBE 0               // timing-only probes for A/B builds (results invalid)
+#endif
 #ifndef TTS_XRES_OCC
 #define TTS_XRES_OCC 3                 // blocks per CU (register budget; LDS tile cap below)
 #endif
@@ -388,7 +391,12 @@ __global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams
 #pragma unroll
       for (int i = 0; i < XRES_SU; ++i) {
         const int xr = min(max(x_start + min(rb + i * rstep, R - 1), 0), xlast);
+#if TTS_XRES_PROBE & 1  // timing-only: no X staging loads
+        { const unsigned z = (unsigned)(xr * 977 + cc + g0) * 2654435761u;
+          r[i] = uint4{z & 0xB7FF37FFu, (z >> 3) & 0x37FFB7FFu, (z >> 5) & 0xB7FF37FFu, (z >> 7) & 0x37FFB7FFu}; }
+#else
         r[i] = *reinterpret_cast<const uint4*>(xg + xr * p.sxr);
+#endif
       }
 #pragma unroll
       for (int i = 0; i < XRES_SU; ++i) {

@@ -13,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <numeric>
 #include <string>
 #include <vector>
 
@@ -97,6 +98,9 @@ struct tts_engine {
   int vlens_batch = 0;
   float* vchunk_wav = nullptr;
   size_t vchunk_elems = 0;
+  // polyphase resampler tables, keyed by the reduced (up, down): [up][nq] fp32 on the device
+  struct Resampler { int up, down, nq, n_pre_remove; float* hp; };
+  std::vector<Resampler> resamplers;
 
   ~tts_engine() {
     hipSetDevice(device);
@@ -105,6 +109,7 @@ struct tts_engine {
     if (vmel) hipFree(vmel);
     if (vlens) hipFree(vlens);
     if (vchunk_wav) hipFree(vchunk_wav);
+    for (auto& r : resamplers) hipFree(r.hp);
     ac.free_all();
   }
 
@@ -670,6 +675,49 @@ int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, doubl
   return guarded(eng, [&] {
     if (nkinds < 1 || !ms || !flops || !n_launches) throw TtsError(TTS_ERR_INVALID, "profile_read_kinds: bad arguments");
     eng->prof.read_kinds(nkinds, ms, flops, n_launches);
+  });
+}
+
+int tts_resample_filter(int up, int down, double* h, int cap, int* n_pre_remove) {
+  try {
+    if (up <= 0 || down <= 0) throw TtsError(TTS_ERR_INVALID, "resample: up/down must be positive");
+    const int g = std::gcd(up, down);
+    std::vector<double> hv;
+    int npr = 0;
+    const int n = resample_design(up / g, down / g, hv, npr);
+    if (n_pre_remove) *n_pre_remove = npr;
+    if (h && cap >= n) std::copy(hv.begin(), hv.end(), h);
+    return n;
+  } catch (const TtsError& e) {
+    g_last_error = e.what();
+    return e.code;
+  }
+}
+
+int tts_resample_poly(tts_engine* eng, const float* d_in, int64_t in_stride, const int32_t* d_in_lens, int B,
+                      int up, int down, float* d_out, int64_t out_stride, int out_cap, int32_t* d_out_lens,
+                      void* stream) {
+  return guarded(eng, [&] {
+    if (!d_in || !d_in_lens || !d_out || B <= 0 || up <= 0 || down <= 0 || out_cap <= 0 || out_stride < out_cap)
+      throw TtsError(TTS_ERR_INVALID, "bad resample args");
+    const int g = std::gcd(up, down);
+    up /= g; down /= g;
+    tts_engine::Resampler* rs = nullptr;
+    for (auto& r : eng->resamplers)
+      if (r.up == up && r.down == down) rs = &r;
+    if (!rs) {
+      std::vector<double> h;
+      int npr = 0;
+      const int n = resample_design(up, down, h, npr);
+      const int nq = (n + up - 1) / up;
+      std::vector<float> hp((size_t)up * nq, 0.f);
+      for (int k = 0; k < n; ++k) hp[(size_t)(k % up) * nq + k / up] = (float)h[k];
+      float* d = upload_f32(hp);
+      eng->resamplers.push_back({up, down, nq, npr, d});
+      rs = &eng->resamplers.back();
+    }
+    HIP_CHECK(launch_resample_poly(d_in, in_stride, d_in_lens, B, up, down, rs->nq, rs->n_pre_remove, rs->hp, d_out,
+                                   out_stride, out_cap, d_out_lens, (hipStream_t)stream));
   });
 }
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace tts {
 
 // Implicit-GEMM conv (conv_gemm.hip).  All strides are in elements of the compute dtype.
@@ -100,6 +102,12 @@ hipError_t mrf_chain_launch(int dtype, int C, int k, const MrfChainParams& p, hi
 int mrf_fused_taps_per_group(int C);
 int mrf_fused_bn(int C);
 hipError_t mrf_fused_launch(int dtype, int C, const MrfParams& p, hipStream_t s);
+
+// resample.hip: scipy.signal.resample_poly's default filter (padded taps, n_pre_remove)
+int resample_design(int up, int down, std::vector<double>& h, int& n_pre_remove);
+hipError_t launch_resample_poly(const float* x, long long sxb, const int* in_lens, int B, int up, int down, int nq,
+                                int n_pre_remove, const float* hp, float* y, long long syb, int y_cap,
+                                int* out_lens, hipStream_t s);
 
 // elementwise.hip
 hipError_t launch_mel_in(int dtype, const float* mel, long long smb, int smr, const float* mean,

@@ -68,6 +68,8 @@ C_API = [
                                      ctypes.POINTER(ctypes.c_int)]),
     ("tts_engine_profile_read_kinds", _I, [_VP, _I, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
+    ("tts_resample_poly", _I, [_VP, _VP, ctypes.c_int64, _VP, _I, _I, _I, _VP, ctypes.c_int64, _I, _VP, _VP]),
+    ("tts_resample_filter", _I, [_I, _I, ctypes.POINTER(ctypes.c_double), _I, ctypes.POINTER(ctypes.c_int)]),
     ("tts_last_error", ctypes.c_char_p, []),
     ("tts_op_conv1d", _I, [_I, ctypes.POINTER(TtsConvDesc), _VP]),
 ]
@@ -92,6 +94,19 @@ def load_library(path: str = LIB_PATH):
             fn.argtypes = args
         _lib = lib
         return lib
+
+
+def resample_filter(up: int, down: int):
+    """Host-side filter design of tts_resample_poly (no GPU): (taps float64, n_pre_remove)."""
+    lib = load_library()
+    npr = ctypes.c_int()
+    n = lib.tts_resample_filter(up, down, None, 0, ctypes.byref(npr))
+    if n < 0:
+        check(n, "tts_resample_filter")
+    h = (ctypes.c_double * n)()
+    lib.tts_resample_filter(up, down, h, n, ctypes.byref(npr))
+    import numpy as _np
+    return _np.frombuffer(h, dtype=_np.float64).copy(), npr.value
 
 
 def check(rc: int, what: str = ""):
@@ -202,6 +217,26 @@ class HipEngine:
                                                  ctypes.c_void_p(out.data_ptr()), _stream_ptr(stream)),
               "tts_vocoder_forward_chunk")
         return out
+
+    def resample(self, wav, lens, up: int, down: int, out=None, stream=None):
+        """Per-utterance rational resampling on the device (scipy.signal.resample_poly(x, up,
+        down) semantics): wav cuda float32 [B, S], lens (valid samples) [B] ->
+        (out cuda float32 [B, ceil(S*up/down)], out_lens cuda int32 [B])."""
+        import torch
+        assert wav.is_cuda and wav.dtype == torch.float32 and wav.dim() == 2
+        wav = wav.contiguous()
+        B, S = wav.shape
+        lens = torch.as_tensor(lens).to(device=wav.device, dtype=torch.int32).contiguous()
+        cap = max(1, -(-S * up // down))
+        if out is None:
+            out = torch.empty((B, cap), dtype=torch.float32, device=wav.device)
+        out_lens = torch.empty((B,), dtype=torch.int32, device=wav.device)
+        check(self.lib.tts_resample_poly(self.handle, ctypes.c_void_p(wav.data_ptr()), S,
+                                         ctypes.c_void_p(lens.data_ptr()), B, up, down,
+                                         ctypes.c_void_p(out.data_ptr()), out.shape[1], cap,
+                                         ctypes.c_void_p(out_lens.data_ptr()), _stream_ptr(stream)),
+              "tts_resample_poly")
+        return out, out_lens
 
     def acoustic(self, tokens, tok_lens, t_cap: int, durations=None, stream=None, return_durations=False):
         """tokens: cuda int32 [B, N]; returns (mel [B, t_cap, 80] f32, mel_lens int32 [B])."""

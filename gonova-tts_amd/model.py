@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import os
 import threading
+from math import gcd
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -28,14 +29,43 @@ from .text import tokenize_batch
 from .weights import make_acoustic_weights, make_vocoder_weights
 
 
+def fold_weight_norm(sd: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
+    """Fold weight-normalised convolutions into plain weights.
+
+    HiFi-GAN checkpoints are often saved with torch weight norm on (HF's
+    `apply_weight_norm`): `<name>.weight_g` / `<name>.weight_v` (torch.nn.utils.weight_norm)
+    or `<name>.parametrizations.weight.original0` / `.original1` (the parametrization API).
+    Both store w = g * v / ||v|| with the norm over every dim but 0 (torch's default
+    dim=0, which HF uses for Conv1d and ConvTranspose1d alike); the result is written
+    as `<name>.weight` and the g/v entries are dropped."""
+    out = dict(sd)
+    pairs = []
+    for k in sd:
+        if k.endswith(".weight_g"):
+            pairs.append((k[: -len(".weight_g")], k, k[:-1] + "v"))
+        elif k.endswith(".parametrizations.weight.original0"):
+            base = k[: -len(".parametrizations.weight.original0")]
+            pairs.append((base, k, k[:-1] + "1"))
+    for base, kg, kv in pairs:
+        if kv not in sd:
+            raise ValueError(f"weight norm: {kg} without {kv}")
+        g = np.asarray(sd[kg], np.float64)
+        v = np.asarray(sd[kv], np.float64)
+        norm = np.sqrt((v.reshape(v.shape[0], -1) ** 2).sum(axis=1)).reshape((-1,) + (1,) * (v.ndim - 1))
+        out[base + ".weight"] = (g.reshape(norm.shape) * v / norm).astype(np.float32)
+        del out[kg], out[kv]
+    return out
+
+
 def load_state_dict(path: str) -> Dict[str, np.ndarray]:
-    """Load a local checkpoint without executing code from it (safetensors / npz)."""
+    """Load a local checkpoint without executing code from it (safetensors / npz); weight-norm
+    pairs are folded (fold_weight_norm)."""
     if path.endswith(".safetensors"):
         from safetensors.numpy import load_file
-        return {k: np.asarray(v, np.float32) for k, v in load_file(path).items()}
+        return fold_weight_norm({k: np.asarray(v, np.float32) for k, v in load_file(path).items()})
     if path.endswith(".npz"):
         with np.load(path, allow_pickle=False) as z:
-            return {k: z[k].astype(np.float32) for k in z.files}
+            return fold_weight_norm({k: z[k].astype(np.float32) for k in z.files})
     raise ValueError(f"unsupported checkpoint format: {path}")
 
 
@@ -44,23 +74,30 @@ class GonovaTTS:
 
     FRAMES_PER_TOKEN_CAP = 12  # first-pass frame budget per token; exact retry if exceeded
 
-    def __init__(self, engine: HipEngine, acoustic_cfg: AcousticConfig, vocoder_cfg: VocoderConfig):
+    def __init__(self, engine: HipEngine, acoustic_cfg: AcousticConfig, vocoder_cfg: VocoderConfig,
+                 sample_rate: Optional[int] = None):
         self.engine = engine
         self.acoustic_cfg = acoustic_cfg
         self.vocoder_cfg = vocoder_cfg
-        self.sr = SAMPLE_RATE
+        # output rate: the vocoder's 22,050 Hz, or e.g. 24,000 for clients that assume the
+        # reference's hard-coded rate (synthesizer.py:119); converted on the device
+        # (tts_resample_poly, scipy.signal.resample_poly semantics)
+        self.native_sr = SAMPLE_RATE
+        self.sr = int(sample_rate) if sample_rate else SAMPLE_RATE
         self.device = f"cuda:{engine.device_index}"
         self._lock = threading.Lock()
 
     @classmethod
     def from_pretrained(cls, device: str = "cuda", ckpt_dir: Optional[str] = None, seed: int = 0,
                         vocoder_dtype: str = "f16", acoustic_dtype: str = "bf16", fixed_duration: Optional[int] = None,
-                        max_batch: int = 0, max_frames: int = 0, max_tokens: int = 0):
+                        max_batch: int = 0, max_frames: int = 0, max_tokens: int = 0,
+                        sample_rate: Optional[int] = None):
         """Mirror of `ChatterboxTTS.from_pretrained(device=...)` (synthesizer.py:185).
 
         ckpt_dir: optional directory with `acoustic.safetensors` and `vocoder.safetensors`
         (HF state_dict names); without it the deterministic seeded weights are used
-        (no checkpoint is reachable offline)."""
+        (no checkpoint is reachable offline).  sample_rate: output rate (default 22,050 Hz;
+        24,000 reproduces the rate the reference's clients assume)."""
         acfg, vcfg = AcousticConfig(), VocoderConfig()
         if ckpt_dir:
             aw = load_state_dict(os.path.join(ckpt_dir, "acoustic.safetensors"))
@@ -71,7 +108,7 @@ class GonovaTTS:
         eng = HipEngine(device, vocoder_dtype=vocoder_dtype, acoustic_dtype=acoustic_dtype,
                         max_batch=max_batch, max_frames=max_frames, max_tokens=max_tokens)
         eng.load_weights(vocoder=vw, acoustic=aw, vocoder_cfg=vcfg)
-        return cls(eng, acfg, vcfg)
+        return cls(eng, acfg, vcfg, sample_rate=sample_rate)
 
     # -------------------------------------------------------------- synthesis
     def synthesize_tokens(self, tokens: np.ndarray, lens: np.ndarray, durations: Optional[np.ndarray] = None,
@@ -93,6 +130,11 @@ class GonovaTTS:
                 mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
                                                           return_durations=True)
         wav = self.engine.vocoder(mel, mel_lens, stream=stream)
+        if self.sr != self.native_sr:
+            g = gcd(self.sr, self.native_sr)
+            wav, out_lens = self.engine.resample(wav, mel_lens * self.vocoder_cfg.hop, self.sr // g,
+                                                 self.native_sr // g, stream=stream)
+            return wav, out_lens.to(torch.int64).cpu().numpy()
         wav_lens = mel_lens.to(torch.int64).cpu().numpy() * self.vocoder_cfg.hop
         return wav, wav_lens
 
@@ -106,7 +148,9 @@ class GonovaTTS:
         With ctx >= the receptive field every kept sample is computed from the same inputs
         in the same order as the full-utterance pass, so the concatenated chunks equal it.
 
-        Yields (c0, wav_chunk cuda float32 [B, chunk*256], valid samples per utterance np [B])."""
+        Yields (c0, wav_chunk cuda float32 [B, chunk*256], valid samples per utterance np [B]).
+        Chunks are at the vocoder's native 22,050 Hz whatever `sr` is (a resampled stream would
+        need the resampler's own filter context across chunk edges)."""
         import torch
         ctx = self.STREAM_CONTEXT if context is None else context
         dev = self.engine.torch_device

@@ -107,6 +107,19 @@ int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops
  * 4 = mrf_chain_kernel. */
 int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, double* flops, int* n_launches);
 
+/* Rational-rate resampling of waveforms (22,050 -> 24,000 Hz for
+ * clients that assume the reference's hard-coded 24 kHz, synthesizer.py:119 /
+ * queue_manager.py:40).  Restates scipy.signal.resample_poly(x, up, down) with its default
+ * Kaiser(5.0) FIR and zero padding, per utterance: d_in [B][in_stride] fp32 with d_in_lens[b]
+ * valid samples -> d_out [B][out_stride], d_out_lens[b] = min(ceil(len*up/down), out_cap);
+ * samples past each length (up to out_cap) are written as 0.  up/down are reduced by their gcd. */
+int tts_resample_poly(tts_engine* eng, const float* d_in, int64_t in_stride, const int32_t* d_in_lens, int B,
+                      int up, int down, float* d_out, int64_t out_stride, int out_cap, int32_t* d_out_lens,
+                      void* stream);
+/* Host only: the padded filter taps tts_resample_poly uses (float64, scaled by up); returns the
+ * tap count (h filled only when cap >= it), *n_pre_remove = leading outputs scipy discards. */
+int tts_resample_filter(int up, int down, double* h, int cap, int* n_pre_remove);
+
 /* Thread-local message describing the last failure on this thread. */
 const char* tts_last_error(void);
 

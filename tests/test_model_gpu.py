@@ -99,3 +99,20 @@ def test_streaming_chunks_equal_full_utterance(dtype):
         got = np.concatenate(pieces[b])
         assert got.shape[0] == full_lens[b]
         np.testing.assert_array_equal(got, full[b, :full_lens[b]])
+
+
+def test_generate_at_24khz_is_resampled_native_output(model32):
+    """sample_rate=24000 (the rate the reference's clients assume, synthesizer.py:119): the
+    22,050 Hz waveform converted on the device == scipy.signal.resample_poly of it."""
+    import scipy.signal as ss
+    m24 = GonovaTTS(model32.engine, model32.acoustic_cfg, model32.vocoder_cfg, sample_rate=24000)
+    assert m24.sr == 24000
+    texts = ["Hello world.", "The quick brown fox jumps over the lazy dog."]
+    native = model32.generate_batch(texts)
+    at24 = m24.generate_batch(texts)
+    for a, b in zip(native, at24):
+        ref = ss.resample_poly(a.astype(np.float64), 160, 147)
+        assert b.shape == ref.shape
+        assert np.abs(b - ref).max() <= 2e-6
+    one = m24.generate(texts[0]).squeeze().cpu().numpy()
+    np.testing.assert_array_equal(one, at24[0])

@@ -181,7 +181,9 @@ def create_app(model_factory: Optional[Callable] = None, **service_kwargs):
     if model_factory is None:
         def model_factory():
             from ..model import GonovaTTS
-            return GonovaTTS.from_pretrained(device="cuda:0", ckpt_dir=os.environ.get("TTS_CKPT_DIR"))
+            sr = os.environ.get("TTS_SAMPLE_RATE")  # e.g. 24000: the rate the reference's clients assume
+            return GonovaTTS.from_pretrained(device="cuda:0", ckpt_dir=os.environ.get("TTS_CKPT_DIR"),
+                                             sample_rate=int(sr) if sr else None)
 
     app = FastAPI(title="TTS Service (MI355X)", version="0.1.0")
     svc = TTSService(model_factory, **service_kwargs)

@@ -56,9 +56,12 @@ class StreamingSynthesizer:
         start_time = time.time()
         try:
             from .model import GonovaTTS
+            # sample_rate is the output rate, as in the reference (synthesizer.py:119); 24000 gets
+            # the reference's rate through the on-device resampler
             self.model = GonovaTTS.from_pretrained(device=self.device, ckpt_dir=self.model_path,
                                                    vocoder_dtype=self.vocoder_dtype,
-                                                   acoustic_dtype=self.acoustic_dtype)
+                                                   acoustic_dtype=self.acoustic_dtype,
+                                                   sample_rate=self.sample_rate)
             self.sample_rate = self.model.sr
             loop = asyncio.get_event_loop()
             warmup_texts = [

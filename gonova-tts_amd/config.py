@@ -12,7 +12,7 @@ SURVEY.md §8c) so that a checkpoint in that naming can be loaded unchanged.
 from __future__ import annotations
 
 from dataclasses import dataclass, field, asdict
-from typing import List, Tuple
+from typing import Optional, List, Tuple
 
 SAMPLE_RATE = 22050
 HOP_LENGTH = 256  # prod(upsample_rates): one mel frame -> 256 samples
@@ -45,6 +45,10 @@ class AcousticConfig:
     layer_norm_eps: float = 1e-5
     batch_norm_eps: float = 1e-5
     speaking_speed: float = 1.0
+    # HF FastSpeech2ConformerConfig.speaker_embed_dim (HF:1051-1053, 1192-1196): when set, an
+    # external speaker embedding is L2-normalised, concatenated to every encoder frame and
+    # projected back to hidden_size (Linear(hidden + E -> hidden)); None = single speaker
+    speaker_embed_dim: Optional[int] = None
 
     @property
     def head_dim(self) -> int:

@@ -64,6 +64,12 @@ struct AcousticModel::Impl {
   float *pe_w = nullptr, *pe_b = nullptr, *ee_w = nullptr, *ee_b = nullptr;
   ConvLayer feat_out;
   std::vector<ConvLayer> postnet;
+  // speaker-embedding projection (HF:1051-1053, 1192-1196): hidden part as a k=1 conv,
+  // embedding part (fp32 [D][E]) + bias folded per utterance by spk_bias_kernel
+  int E = 0;
+  ConvLayer proj_h;
+  float *proj_we = nullptr, *proj_b = nullptr;
+  void* SPK = nullptr;  // [B][D] per-utterance term, compute dtype
   std::vector<void*> allocs;
   int rmax = 0;
   float* pe_host_table_dummy = nullptr;
@@ -233,6 +239,7 @@ struct AcousticModel::Impl {
     P = alloc_ws((size_t)B * H * Tm * Sk, e);
     const size_t nrows = (size_t)B * rup(N, 32);
     ENC = alloc_ws(nrows * D, e);
+    SPK = alloc_ws((size_t)B * D, e);
     PB1 = alloc_ws(nrows * PRED, e); PB2 = alloc_ws(nrows * PRED, e);
     const size_t trows = (size_t)B * rup(T, 32);
     BEF = alloc_ws(trows * NMEL, e); MELT = alloc_ws(trows * NMEL, e);
@@ -317,7 +324,7 @@ struct AcousticModel::Impl {
   }
 
   void forward(const int* tokens, const int* tok_lens, int B, int N, const int* dur_override, float* mel,
-               int* mel_lens, int Tcap, int* durations, hipStream_t s) {
+               int* mel_lens, int Tcap, int* durations, const float* spk, hipStream_t s) {
     reserve(B, N, Tcap);
     const int Tm = std::max(N, Tcap);
     if (Tm > rmax) build_ptabs(rup(Tm, 256), s);
@@ -326,6 +333,18 @@ struct AcousticModel::Impl {
     // encoder
     HIP_CHECK(launch_embed(dt, tokens, tok_lens, B, N, Np, embed, V, D, xscale, ENC, s));
     stack(enc, ENC, tok_lens, B, N, s);
+    if (spk && E) {  // speaker embedding (HF:1192-1196); without one HF skips the projection
+      HIP_CHECK(launch_spk_bias(dt, spk, B, E, proj_we, proj_b, D, SPK, s));
+      ConvParams p = conv_params_default();
+      p.x = ENC; p.sxb = (long long)Np * D; p.sxr = D; p.x_len = tok_lens; p.x_rows = Np;
+      p.w = proj_h.w; p.w_ld = D; p.bias = nullptr; p.wpk = proj_h.wpk;
+      p.y = Y; p.syb = (long long)Np * D; p.syr = D;
+      p.r1 = SPK; p.srb = D; p.srr = 0;  // the utterance's term broadcast over its frames
+      p.y_len = tok_lens; p.y_rows = Np;
+      p.M = D; p.Cin = D; p.B = B;
+      launch_conv_checked(p, dt, s, prof, 2.0 * D * (double)D * B * Np);
+      HIP_CHECK(hipMemcpyAsync(ENC, Y, (size_t)B * Np * D * dtype_size(dt), hipMemcpyDeviceToDevice, s));
+    }
     // variance adaptor (HF:1198-1218)
     predict(pitch, ENC, tok_lens, B, Np, f_pitch, s);
     predict(energy, ENC, tok_lens, B, Np, f_energy, s);
@@ -403,6 +422,21 @@ void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtyp
   m->pitch = m->predictor(get, shape, "pitch_predictor.");
   m->energy = m->predictor(get, shape, "energy_predictor.");
   m->duration = m->predictor(get, shape, "duration_predictor.");
+  if (get("projection.weight")) {
+    const auto ps = shape("projection.weight");  // [D][D + E]
+    const int din = (int)ps.at(1);
+    if ((int)ps.at(0) != m->D || din <= m->D) throw TtsError(TTS_ERR_INVALID, "bad projection.weight shape");
+    m->E = din - m->D;
+    const auto& pw = m->need(get, "projection.weight");
+    std::vector<float> wh((size_t)m->D * m->D), we((size_t)m->D * m->E);
+    for (int o = 0; o < m->D; ++o) {
+      for (int i = 0; i < m->D; ++i) wh[(size_t)o * m->D + i] = pw[(size_t)o * din + i];
+      for (int i = 0; i < m->E; ++i) we[(size_t)o * m->E + i] = pw[(size_t)o * din + m->D + i];
+    }
+    m->proj_h = make_conv(wh, m->D, m->D, 1, {}, 1, 0, dtype, m->allocs);
+    m->proj_we = m->upf(we);
+    m->proj_b = m->upf(m->need(get, "projection.bias"));
+  }
   m->pe_w = m->upf(m->need(get, "pitch_embed.conv.weight"));
   m->pe_b = m->upf(m->need(get, "pitch_embed.conv.bias"));
   m->ee_w = m->upf(m->need(get, "energy_embed.conv.weight"));
@@ -434,10 +468,13 @@ void AcousticModel::reserve(int B, int N, int T) {
 }
 
 void AcousticModel::forward(const int32_t* tokens, const int32_t* tok_lens, int B, int N, const int32_t* dur_override,
-                            float* mel, int32_t* mel_lens, int Tcap, int32_t* durations, hipStream_t s) {
+                            float* mel, int32_t* mel_lens, int Tcap, int32_t* durations, const float* spk,
+                            hipStream_t s) {
   if (!impl) throw TtsError(TTS_ERR_STATE, "acoustic model not loaded");
-  impl->forward(tokens, tok_lens, B, N, dur_override, mel, mel_lens, Tcap, durations, s);
+  impl->forward(tokens, tok_lens, B, N, dur_override, mel, mel_lens, Tcap, durations, spk, s);
 }
+
+int AcousticModel::speaker_dim() const { return impl ? impl->E : 0; }
 
 void AcousticModel::free_all() {
   delete impl;

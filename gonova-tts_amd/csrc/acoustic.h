@@ -17,8 +17,10 @@ struct AcousticModel {
   typedef std::function<std::vector<int64_t>(const std::string&)> GetShape;
   void finalize(const GetData& get, const GetShape& shape, int dtype, Profiler* prof);
   void reserve(int B, int N, int T);
+  // spk: optional [B][speaker_dim()] fp32 speaker embeddings (ignored when the model has none)
   void forward(const int32_t* tokens, const int32_t* tok_lens, int B, int N, const int32_t* dur_override,
-               float* mel, int32_t* mel_lens, int Tcap, int32_t* durations, hipStream_t s);
+               float* mel, int32_t* mel_lens, int Tcap, int32_t* durations, const float* spk, hipStream_t s);
+  int speaker_dim() const;
   void free_all();
   struct Impl;
   Impl* impl = nullptr;

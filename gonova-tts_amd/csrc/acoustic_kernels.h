@@ -27,4 +27,7 @@ hipError_t launch_regulate(int dt, const void* enc, int B, int N, int D, const i
 hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, int Tcap, int C, float* out,
                           hipStream_t s);
 
+hipError_t launch_spk_bias(int dt, const float* e, int B, int E, const float* We, const float* bias, int D, void* out,
+                           hipStream_t s);
+
 }  // namespace tts

@@ -274,6 +274,37 @@ __global__ __launch_bounds__(256) void glu_dwconv_k_kernel(const T* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// Speaker-embedding term of the projection after the encoder (HF:1192-1196):
+//   c[b][o] = bias[o] + sum_i We[o][i] * e[b][i] / max(||e[b]||, 1e-12)
+// (F.normalize), the part of Linear(concat(h, e)) that is constant over an utterance's
+// frames; the hidden part runs as a k=1 conv with c broadcast as its residual.  One block
+// per utterance: a block reduction for the norm, then one output channel per thread.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void spk_bias_kernel(const float* __restrict__ e, int E,
+                                                      const float* __restrict__ We, const float* __restrict__ bias,
+                                                      int D, T* __restrict__ out) {
+  __shared__ float red[256];
+  const int b = blockIdx.x;
+  const float* eb = e + (long long)b * E;
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < E; i += 256) ss = fmaf(eb[i], eb[i], ss);
+  red[threadIdx.x] = ss;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const float inv = 1.f / fmaxf(sqrtf(red[0]), 1e-12f);
+  for (int o = threadIdx.x; o < D; o += 256) {
+    const float* wr = We + (long long)o * E;
+    float acc = 0.f;
+    for (int i = 0; i < E; ++i) acc = fmaf(wr[i], eb[i], acc);
+    out[(long long)b * D + o] = from_f32<T>(bias[o] + acc * inv);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // variance-predictor head: LayerNorm(C) then Linear(C -> 1) (HF:261-271, 318)
 // ---------------------------------------------------------------------------
 template <typename T, int PER>
@@ -518,6 +549,11 @@ hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, in
   dim3 grid(grid1((long long)Tcap * C), B);
   TTS_DISPATCH(dt, hipLaunchKernelGGL(mel_out_kernel<TT>, grid, dim3(256), 0, s, (const TT*)in, mel_lens, Tcap, C,
                                       out));
+}
+
+hipError_t launch_spk_bias(int dt, const float* e, int B, int E, const float* We, const float* bias, int D, void* out,
+                           hipStream_t s) {
+  TTS_DISPATCH(dt, hipLaunchKernelGGL(spk_bias_kernel<TT>, dim3(B), dim3(256), 0, s, e, E, We, bias, D, (TT*)out));
 }
 
 }  // namespace tts

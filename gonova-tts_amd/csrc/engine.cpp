@@ -650,16 +650,32 @@ int tts_vocoder_forward_chunk(tts_engine* eng, const float* d_mel, const int32_t
   });
 }
 
-int tts_acoustic_forward(tts_engine* eng, const int32_t* d_tokens, const int32_t* d_tok_lens, int B, int N,
-                         const int32_t* d_dur_override, float* d_mel, int32_t* d_mel_lens, int Tcap,
-                         int32_t* d_durations, void* stream) {
+int tts_acoustic_forward_spk(tts_engine* eng, const int32_t* d_tokens, const int32_t* d_tok_lens, int B, int N,
+                             const int32_t* d_dur_override, const float* d_spk_emb, int spk_dim, float* d_mel,
+                             int32_t* d_mel_lens, int Tcap, int32_t* d_durations, void* stream) {
   return guarded(eng, [&] {
     if (!eng->finalized) throw TtsError(TTS_ERR_STATE, "finalize first");
     if (!eng->ac.loaded) throw TtsError(TTS_ERR_STATE, "acoustic weights not loaded");
     if (!d_tokens || !d_tok_lens || !d_mel || !d_mel_lens || B <= 0 || N <= 0 || Tcap <= 0)
       throw TtsError(TTS_ERR_INVALID, "bad acoustic args");
-    eng->ac.forward(d_tokens, d_tok_lens, B, N, d_dur_override, d_mel, d_mel_lens, Tcap, d_durations,
+    if (d_spk_emb && eng->ac.speaker_dim() && spk_dim != eng->ac.speaker_dim())
+      throw TtsError(TTS_ERR_INVALID, "speaker embedding size does not match the model's projection");
+    eng->ac.forward(d_tokens, d_tok_lens, B, N, d_dur_override, d_mel, d_mel_lens, Tcap, d_durations, d_spk_emb,
                     (hipStream_t)stream);
+  });
+}
+
+int tts_acoustic_forward(tts_engine* eng, const int32_t* d_tokens, const int32_t* d_tok_lens, int B, int N,
+                         const int32_t* d_dur_override, float* d_mel, int32_t* d_mel_lens, int Tcap,
+                         int32_t* d_durations, void* stream) {
+  return tts_acoustic_forward_spk(eng, d_tokens, d_tok_lens, B, N, d_dur_override, nullptr, 0, d_mel, d_mel_lens,
+                                  Tcap, d_durations, stream);
+}
+
+int tts_acoustic_speaker_dim(tts_engine* eng, int* dim) {
+  return guarded(eng, [&] {
+    if (!dim) throw TtsError(TTS_ERR_INVALID, "null dim");
+    *dim = eng->ac.loaded ? eng->ac.speaker_dim() : 0;
   });
 }
 

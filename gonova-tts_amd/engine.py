@@ -63,6 +63,8 @@ C_API = [
     ("tts_vocoder_forward", _I, [_VP, _VP, _VP, _I, _I, _VP, _VP]),
     ("tts_vocoder_forward_chunk", _I, [_VP, _VP, _VP, _I, _I, _I, _I, _VP, _VP]),
     ("tts_acoustic_forward", _I, [_VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _I, _VP, _VP]),
+    ("tts_acoustic_forward_spk", _I, [_VP, _VP, _VP, _I, _I, _VP, _VP, _I, _VP, _VP, _I, _VP, _VP]),
+    ("tts_acoustic_speaker_dim", _I, [_VP, ctypes.POINTER(ctypes.c_int)]),
     ("tts_engine_profile", _I, [_VP, _I]),
     ("tts_engine_profile_read", _I, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_int)]),
@@ -238,8 +240,17 @@ class HipEngine:
               "tts_resample_poly")
         return out, out_lens
 
-    def acoustic(self, tokens, tok_lens, t_cap: int, durations=None, stream=None, return_durations=False):
-        """tokens: cuda int32 [B, N]; returns (mel [B, t_cap, 80] f32, mel_lens int32 [B])."""
+    @property
+    def speaker_dim(self) -> int:
+        """Speaker-embedding size of the loaded acoustic model (0: single speaker)."""
+        d = ctypes.c_int()
+        check(self.lib.tts_acoustic_speaker_dim(self.handle, ctypes.byref(d)), "tts_acoustic_speaker_dim")
+        return d.value
+
+    def acoustic(self, tokens, tok_lens, t_cap: int, durations=None, stream=None, return_durations=False,
+                 speaker_embedding=None):
+        """tokens: cuda int32 [B, N]; returns (mel [B, t_cap, 80] f32, mel_lens int32 [B]).
+        speaker_embedding: optional float32 [B, E] (HF:1192-1196), E = speaker_dim."""
         import torch
         tokens = tokens.to(dtype=torch.int32).contiguous()
         tok_lens = tok_lens.to(device=tokens.device, dtype=torch.int32).contiguous()
@@ -251,10 +262,15 @@ class HipEngine:
         if durations is not None:
             durations = durations.to(device=tokens.device, dtype=torch.int32).contiguous()
             dptr = ctypes.c_void_p(durations.data_ptr())
-        check(self.lib.tts_acoustic_forward(self.handle, ctypes.c_void_p(tokens.data_ptr()),
-                                            ctypes.c_void_p(tok_lens.data_ptr()), B, N, dptr,
-                                            ctypes.c_void_p(mel.data_ptr()), ctypes.c_void_p(mel_lens.data_ptr()),
-                                            t_cap, ctypes.c_void_p(dur_out.data_ptr()), _stream_ptr(stream)),
+        sptr, sdim = ctypes.c_void_p(0), 0
+        if speaker_embedding is not None:
+            speaker_embedding = torch.as_tensor(speaker_embedding, dtype=torch.float32).to(tokens.device)
+            speaker_embedding = speaker_embedding.reshape(B, -1).contiguous()
+            sptr, sdim = ctypes.c_void_p(speaker_embedding.data_ptr()), speaker_embedding.shape[1]
+        check(self.lib.tts_acoustic_forward_spk(self.handle, ctypes.c_void_p(tokens.data_ptr()),
+                                                ctypes.c_void_p(tok_lens.data_ptr()), B, N, dptr, sptr, sdim,
+                                                ctypes.c_void_p(mel.data_ptr()), ctypes.c_void_p(mel_lens.data_ptr()),
+                                                t_cap, ctypes.c_void_p(dur_out.data_ptr()), _stream_ptr(stream)),
               "tts_acoustic_forward")
         if return_durations:
             return mel, mel_lens, dur_out

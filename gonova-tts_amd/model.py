@@ -91,17 +91,21 @@ class GonovaTTS:
     def from_pretrained(cls, device: str = "cuda", ckpt_dir: Optional[str] = None, seed: int = 0,
                         vocoder_dtype: str = "f16", acoustic_dtype: str = "bf16", fixed_duration: Optional[int] = None,
                         max_batch: int = 0, max_frames: int = 0, max_tokens: int = 0,
-                        sample_rate: Optional[int] = None):
+                        sample_rate: Optional[int] = None, speaker_embed_dim: Optional[int] = None):
         """Mirror of `ChatterboxTTS.from_pretrained(device=...)` (synthesizer.py:185).
 
         ckpt_dir: optional directory with `acoustic.safetensors` and `vocoder.safetensors`
         (HF state_dict names); without it the deterministic seeded weights are used
         (no checkpoint is reachable offline).  sample_rate: output rate (default 22,050 Hz;
-        24,000 reproduces the rate the reference's clients assume)."""
-        acfg, vcfg = AcousticConfig(), VocoderConfig()
+        24,000 reproduces the rate the reference's clients assume).  speaker_embed_dim: seeded
+        multi-speaker weights with a speaker-embedding projection of that size (a checkpoint
+        carrying `projection.weight` sets it by itself)."""
+        acfg, vcfg = AcousticConfig(speaker_embed_dim=speaker_embed_dim), VocoderConfig()
         if ckpt_dir:
             aw = load_state_dict(os.path.join(ckpt_dir, "acoustic.safetensors"))
             vw = load_state_dict(os.path.join(ckpt_dir, "vocoder.safetensors"))
+            if "projection.weight" in aw:  # multi-speaker checkpoint (HF speaker_embed_dim)
+                acfg.speaker_embed_dim = aw["projection.weight"].shape[1] - aw["projection.weight"].shape[0]
         else:
             aw = make_acoustic_weights(seed, acfg, fixed_duration=fixed_duration)
             vw = make_vocoder_weights(seed, vcfg)
@@ -112,7 +116,7 @@ class GonovaTTS:
 
     # -------------------------------------------------------------- synthesis
     def synthesize_tokens(self, tokens: np.ndarray, lens: np.ndarray, durations: Optional[np.ndarray] = None,
-                          stream=None):
+                          stream=None, speaker_embedding: Optional[np.ndarray] = None):
         """tokens int32 [B, N], lens [B] -> (wav cuda float32 [B, T*256], wav_lens np.int64 [B])."""
         import torch
         dev = self.engine.torch_device
@@ -123,12 +127,14 @@ class GonovaTTS:
         t_cap = max(64, int(self.FRAMES_PER_TOKEN_CAP * N))
         if durations is not None:
             t_cap = max(1, int(np.asarray(durations).sum(axis=1).max()))
-        mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True)
+        spk = speaker_embedding
+        mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True,
+                                                  speaker_embedding=spk)
         if durations is None:
             need = int(dur.sum(dim=1).max().item())
             if need > t_cap:  # exact second pass with the predicted durations and a fitting cap
                 mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
-                                                          return_durations=True)
+                                                          return_durations=True, speaker_embedding=spk)
         wav = self.engine.vocoder(mel, mel_lens, stream=stream)
         if self.sr != self.native_sr:
             g = gcd(self.sr, self.native_sr)
@@ -189,17 +195,47 @@ class GonovaTTS:
             host = wav.cpu().numpy()
         return [host[i, : int(wav_lens[i])].astype(np.float32, copy=False) for i in range(len(texts))]
 
+    def speaker_embedding(self, audio_prompt_path: Optional[str]) -> Optional[np.ndarray]:
+        """The voice for `audio_prompt_path` (the reference's voice_id -> path,
+        server.py:127-138): a stored speaker embedding (.npy / .npz / .safetensors, one vector of
+        speaker_embed_dim values, loaded without executing anything from the file) when the
+        model has a speaker projection; None otherwise.  Audio prompts (.wav) carry no
+        embedding here -- the speaker encoder that would compute one is not part of this
+        engine -- and are ignored, as before."""
+        if not audio_prompt_path or not self.acoustic_cfg.speaker_embed_dim:
+            return None
+        path = str(audio_prompt_path)
+        if path.endswith(".npy"):
+            v = np.load(path, allow_pickle=False)
+        elif path.endswith(".npz"):
+            with np.load(path, allow_pickle=False) as z:
+                v = z["embedding"] if "embedding" in z.files else z[z.files[0]]
+        elif path.endswith(".safetensors"):
+            from safetensors.numpy import load_file
+            d = load_file(path)
+            v = d["embedding"] if "embedding" in d else next(iter(d.values()))
+        else:
+            return None
+        v = np.asarray(v, np.float32).reshape(-1)
+        if v.size != self.acoustic_cfg.speaker_embed_dim:
+            raise ValueError(f"speaker embedding {path}: {v.size} values, model expects "
+                             f"{self.acoustic_cfg.speaker_embed_dim}")
+        return v
+
     def generate(self, text: str, audio_prompt_path: Optional[str] = None, exaggeration: float = 0.5,
                  cfg_weight: float = 0.5, temperature: float = 0.8, **kwargs):
         """Same call shape as the reference's `model.generate` (synthesizer.py:344-350).
 
         Returns a float32 torch tensor of shape (1, N) on the engine device; the
-        reference's `audio.squeeze().cpu().numpy()` applies unchanged."""
+        reference's `audio.squeeze().cpu().numpy()` applies unchanged.  audio_prompt_path
+        selects a stored speaker embedding on a multi-speaker model (speaker_embedding())."""
         import torch
-        del audio_prompt_path, exaggeration, cfg_weight, temperature, kwargs
+        del exaggeration, cfg_weight, temperature, kwargs
+        spk = self.speaker_embedding(audio_prompt_path)
         with self._lock:
             tokens, lens = tokenize_batch([text])
-            wav, wav_lens = self.synthesize_tokens(tokens, lens)
+            wav, wav_lens = self.synthesize_tokens(tokens, lens,
+                                                   speaker_embedding=None if spk is None else spk[None])
         return wav[:, : int(wav_lens[0])].contiguous().to(torch.float32)
 
 

@@ -119,6 +119,10 @@ def _acoustic_spec(cfg: AcousticConfig):
     s.update(_predictor_spec("duration_predictor.", cfg, cfg.duration_predictor_layers,
                              cfg.duration_predictor_channels, cfg.duration_predictor_kernel_size,
                              0.5 / math.sqrt(cfg.duration_predictor_channels), ("const", math.log(4.0))))
+    if cfg.speaker_embed_dim:  # speaker-embedding projection (HF:1051-1053)
+        e = cfg.speaker_embed_dim
+        s["projection.weight"] = ((h, h + e), ("normal", 1.0 / math.sqrt(h + e)))
+        s["projection.bias"] = ((h,), ("normal", 0.02))
     s.update(_predictor_spec("pitch_predictor.", cfg, cfg.pitch_predictor_layers,
                              cfg.pitch_predictor_channels, cfg.pitch_predictor_kernel_size,
                              1.0 / math.sqrt(cfg.pitch_predictor_channels), ("normal", 0.02)))

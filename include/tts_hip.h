@@ -97,6 +97,17 @@ int tts_acoustic_forward(tts_engine* eng, const int32_t* d_tokens, const int32_t
                          int B, int N, const int32_t* d_dur_override, float* d_mel,
                          int32_t* d_mel_lens, int Tcap, int32_t* d_durations, void* stream);
 
+/* The same with per-utterance speaker embeddings (HF:1192-1196):
+ * d_spk_emb [B][spk_dim] fp32 on the device, spk_dim == tts_acoustic_speaker_dim(); each is
+ * L2-normalised, concatenated to every encoder frame and projected back to the hidden size.
+ * NULL (or a model without a speaker projection) = tts_acoustic_forward. */
+int tts_acoustic_forward_spk(tts_engine* eng, const int32_t* d_tokens, const int32_t* d_tok_lens,
+                             int B, int N, const int32_t* d_dur_override, const float* d_spk_emb,
+                             int spk_dim, float* d_mel, int32_t* d_mel_lens, int Tcap,
+                             int32_t* d_durations, void* stream);
+/* Speaker-embedding size E of the loaded acoustic model (0: single speaker). */
+int tts_acoustic_speaker_dim(tts_engine* eng, int* dim);
+
 /* Live kernel timing for bench.py: with profiling on, every implicit-GEMM launch is
  * bracketed by hipEvents on its own stream; _read() waits for them and returns the summed
  * kernel time (ms), the algorithmic FLOPs of those launches and their count, then resets. */

@@ -176,10 +176,12 @@ def postnet(x, w, n_layers=5, eps=1e-5):
     return before + h
 
 
-def acoustic_forward(token_ids, w, cfg=None, durations=None, dtype=np.float32):
+def acoustic_forward(token_ids, w, cfg=None, durations=None, dtype=np.float32, speaker_embedding=None):
     """FastSpeech2ConformerModel.forward inference path (HF:1099-1288) for one utterance.
 
     token_ids: int [L].  durations: optional int [L] override (otherwise predicted).
+    speaker_embedding: optional [E] vector, used when the weights carry `projection.*`
+    (HF:1192-1196: normalize, concat to every encoder frame, Linear back to hidden).
     Returns dict(mel [T, 80], durations [L], pitch [L], energy [L], log_durations [L]).
     """
     from gonova_tts_amd.config import AcousticConfig  # config only
@@ -188,6 +190,11 @@ def acoustic_forward(token_ids, w, cfg=None, durations=None, dtype=np.float32):
     ids = np.asarray(token_ids, np.int64)
     x = w["encoder.embed.weight"][ids]
     x = conformer_stack(x, w, "encoder.", cfg.encoder_layers, cfg.num_attention_heads)
+    if speaker_embedding is not None and "projection.weight" in w:  # HF:1192-1196
+        e = np.asarray(speaker_embedding, dtype)
+        e = e / max(float(np.sqrt((e.astype(np.float64) ** 2).sum())), 1e-12)  # F.normalize, eps 1e-12
+        xe = np.concatenate([x, np.broadcast_to(e, (x.shape[0], e.shape[0]))], axis=1)
+        x = xe @ w["projection.weight"].T + w["projection.bias"]
     pitch = variance_predictor(x, w, "pitch_predictor.", cfg.pitch_predictor_layers)
     energy = variance_predictor(x, w, "energy_predictor.", cfg.energy_predictor_layers)
     logd = variance_predictor(x, w, "duration_predictor.", cfg.duration_predictor_layers)

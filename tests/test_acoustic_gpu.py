@@ -138,3 +138,62 @@ def test_end_to_end_fp32_matches_golden(aw):
     L = int(mel_lens[0])
     wav = eng.vocoder(torch.from_numpy(mel[:, :L].copy()).to(DEV)).cpu().numpy()[0]
     np.testing.assert_allclose(wav, G["e2e_wav"], atol=2e-4, rtol=2e-3)
+
+
+GS = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_spk.npz"))
+
+
+@pytest.fixture(scope="module")
+def spk_engine():
+    from gonova_tts_amd.config import AcousticConfig
+    w = make_acoustic_weights(seed=0, cfg=AcousticConfig(speaker_embed_dim=64))
+    e = HipEngine(DEV, vocoder_dtype="f32", acoustic_dtype="f32")
+    e.load_weights(acoustic=w, vocoder=make_vocoder_weights(seed=0))
+    return e, w
+
+
+def test_speaker_embedding_matches_golden_batched(spk_engine):
+    """Speaker-embedding conditioning (HF:1192-1196): two utterances
+    with different embeddings in one ragged batch against the transformers goldens
+    (tests/golden/make_spk_golden.py); without embeddings the projection is skipped (HF)."""
+    eng, w = spk_engine
+    assert eng.speaker_dim == 64
+    tags = ["spk_a", "spk_b"]
+    ids_list = [GS[f"{t}_ids"] for t in tags]
+    B, N = len(tags), max(len(x) for x in ids_list)
+    tok = np.zeros((B, N), np.int32)
+    for b, x in enumerate(ids_list):
+        tok[b, :len(x)] = x
+    lens = torch.tensor([len(x) for x in ids_list], dtype=torch.int32)
+    emb = np.stack([GS[f"{t}_emb"] for t in tags])
+    mel, mel_lens, dur = eng.acoustic(torch.from_numpy(tok).to(DEV), lens, 160, return_durations=True,
+                                      speaker_embedding=torch.from_numpy(emb))
+    mel0, mel_lens0 = eng.acoustic(torch.from_numpy(tok).to(DEV), lens, 160)
+    for b, t in enumerate(tags):
+        np.testing.assert_array_equal(dur[b, :len(ids_list[b])].cpu().numpy(), GS[f"{t}_dur"])
+        L = int(mel_lens[b])
+        assert L == GS[f"{t}_mel"].shape[0]
+        np.testing.assert_allclose(mel[b, :L].cpu().numpy(), GS[f"{t}_mel"], atol=2e-4, rtol=2e-3)
+        L0 = int(mel_lens0[b])
+        assert L0 == GS[f"{t}_mel_nospk"].shape[0]
+        np.testing.assert_allclose(mel0[b, :L0].cpu().numpy(), GS[f"{t}_mel_nospk"], atol=2e-4, rtol=2e-3)
+
+
+def test_speaker_embedding_file_through_generate(spk_engine, tmp_path):
+    """model.generate(text, audio_prompt_path=<stored embedding>) honours the voice (the
+    reference's voice_id -> audio_prompt_path, server.py:127-138); scaling the embedding does
+    not change the output (it is L2-normalised), a different voice does."""
+    from gonova_tts_amd.config import AcousticConfig, VocoderConfig
+    from gonova_tts_amd.model import GonovaTTS
+    eng, w = spk_engine
+    m = GonovaTTS(eng, AcousticConfig(speaker_embed_dim=64), VocoderConfig())
+    np.save(tmp_path / "v1.npy", GS["spk_a_emb"])
+    np.save(tmp_path / "v1x3.npy", 3.0 * GS["spk_a_emb"])
+    np.save(tmp_path / "v2.npy", GS["spk_b_emb"])
+    a = m.generate("Hello there.", audio_prompt_path=str(tmp_path / "v1.npy")).cpu().numpy()
+    a3 = m.generate("Hello there.", audio_prompt_path=str(tmp_path / "v1x3.npy")).cpu().numpy()
+    b = m.generate("Hello there.", audio_prompt_path=str(tmp_path / "v2.npy")).cpu().numpy()
+    n = m.generate("Hello there.", audio_prompt_path="/nonexistent/voice.wav").cpu().numpy()
+    assert a.shape == a3.shape and np.abs(a - a3).max() <= 1e-5 * max(1.0, np.abs(a).max())
+    assert a.shape != b.shape or not np.allclose(a, b)
+    assert n.size > 0

@@ -43,3 +43,19 @@ def test_end_to_end_oracle_matches_golden():
     o = acoustic_forward(G["ac_a_ids"], make_acoustic_weights(seed=0))
     wav = vocoder_forward(o["mel"], make_vocoder_weights(seed=0))
     np.testing.assert_allclose(wav, G["e2e_wav"], atol=1e-5, rtol=1e-4)
+
+
+GS = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_spk.npz"))
+
+
+@pytest.mark.parametrize("tag", ["spk_a", "spk_b"])
+def test_speaker_embedding_oracle_matches_golden(tag):
+    """Speaker-embedding conditioning (HF:1192-1196; tests/golden/make_spk_golden.py)."""
+    from gonova_tts_amd.config import AcousticConfig
+    from gonova_tts_amd.weights import make_acoustic_weights
+    w = make_acoustic_weights(0, AcousticConfig(speaker_embed_dim=64))
+    o = acoustic_forward(GS[f"{tag}_ids"], w, speaker_embedding=GS[f"{tag}_emb"])
+    np.testing.assert_array_equal(o["durations"], GS[f"{tag}_dur"])
+    np.testing.assert_allclose(o["mel"], GS[f"{tag}_mel"], atol=1e-4, rtol=1e-4)
+    o0 = acoustic_forward(GS[f"{tag}_ids"], w)  # no embedding: HF skips the projection
+    np.testing.assert_allclose(o0["mel"], GS[f"{tag}_mel_nospk"], atol=1e-4, rtol=1e-4)

@@ -185,15 +185,33 @@ class GonovaTTS:
             valid = np.clip(lens_h - c0, 0, tc) * hop
             yield c0, wav, valid
 
-    def generate_batch(self, texts: List[str], **_ignored) -> List[np.ndarray]:
-        """Synthesize many sentences in one batched pass -> list of float32 waveforms."""
+    def generate_batch(self, texts: List[str], speaker_embeddings: Optional[List[Optional[np.ndarray]]] = None,
+                       **_ignored) -> List[np.ndarray]:
+        """Synthesize many sentences in one batched pass -> list of float32 waveforms.
+        speaker_embeddings: optional per-sentence voice vectors (None entries: no voice); on a
+        multi-speaker model the sentences with and without a voice run as two batches (HF
+        skips the projection when no embedding is given, HF:1192)."""
         if not texts:
             return []
+        if not self.acoustic_cfg.speaker_embed_dim or speaker_embeddings is None or \
+                all(e is None for e in speaker_embeddings):
+            groups = [(list(range(len(texts))), None)]
+        else:
+            with_v = [i for i, e in enumerate(speaker_embeddings) if e is not None]
+            without = [i for i, e in enumerate(speaker_embeddings) if e is None]
+            groups = [(with_v, np.stack([np.asarray(speaker_embeddings[i], np.float32).reshape(-1)
+                                         for i in with_v]))]
+            if without:
+                groups.append((without, None))
+        out: List[Optional[np.ndarray]] = [None] * len(texts)
         with self._lock:
-            tokens, lens = tokenize_batch(texts)
-            wav, wav_lens = self.synthesize_tokens(tokens, lens)
-            host = wav.cpu().numpy()
-        return [host[i, : int(wav_lens[i])].astype(np.float32, copy=False) for i in range(len(texts))]
+            for idx, spk in groups:
+                tokens, lens = tokenize_batch([texts[i] for i in idx])
+                wav, wav_lens = self.synthesize_tokens(tokens, lens, speaker_embedding=spk)
+                host = wav.cpu().numpy()
+                for r, i in enumerate(idx):
+                    out[i] = host[r, : int(wav_lens[r])].astype(np.float32, copy=False)
+        return out
 
     def speaker_embedding(self, audio_prompt_path: Optional[str]) -> Optional[np.ndarray]:
         """The voice for `audio_prompt_path` (the reference's voice_id -> path,

@@ -93,8 +93,13 @@ class DynamicBatcher:
         for b0 in range(0, len(order), self.max_sentences):
             chunk = order[b0:b0 + self.max_sentences]
             texts = [work[k][2] for k in chunk]
+            voices = [getattr(reqs[work[k][0]], "voice", None) for k in chunk]
             try:
-                audios = await loop.run_in_executor(None, self.synth_batch, texts)
+                if any(v is not None for v in voices):  # per-sentence voice (registered embedding)
+                    audios = await loop.run_in_executor(
+                        None, lambda: self.synth_batch(texts, speaker_embeddings=voices))
+                else:
+                    audios = await loop.run_in_executor(None, self.synth_batch, texts)
             except Exception as e:
                 self.stats["errors"] += 1
                 logger.error("synthesis_failed: %s", e)

@@ -17,7 +17,7 @@ import asyncio
 import logging
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Any, Dict, List, Optional
 
 logger = logging.getLogger(__name__)
 
@@ -31,6 +31,7 @@ class SynthesisRequest:
     chunk_size: int = 50
     exaggeration: float = 0.5
     streaming: bool = True
+    voice: Optional[Any] = None  # the voice_id's registered speaker embedding (None: default voice)
 
 
 @dataclass
@@ -92,8 +93,9 @@ class TTSQueueManager:
 
     # ------------------------------------------------------------------ requests
     async def enqueue_request(self, connection_id: str, text: str, voice_id: str = "default", chunk_size: int = 50,
-                              exaggeration: float = 0.5, streaming: bool = True, timeout: float = 2.0) -> bool:
-        req = SynthesisRequest(connection_id, text, voice_id, time.time(), chunk_size, exaggeration, streaming)
+                              exaggeration: float = 0.5, streaming: bool = True, timeout: float = 2.0,
+                              voice: Optional[Any] = None) -> bool:
+        req = SynthesisRequest(connection_id, text, voice_id, time.time(), chunk_size, exaggeration, streaming, voice)
         try:
             await asyncio.wait_for(self.input_queue.put(req), timeout=timeout)
         except asyncio.TimeoutError:

@@ -24,6 +24,8 @@ import time
 import uuid
 from typing import Callable, Optional
 
+import numpy as np
+
 from .batcher import DynamicBatcher
 from .queues import TTSQueueManager
 
@@ -65,6 +67,8 @@ class TTSService:
         self.rate_limiter = RateLimiter()
         self.active_connections = 0
         self.sockets = {}
+        self.voices = {}      # voice_id -> speaker embedding (register_voice)
+        self.voice_info = {}  # voice_id -> description
         self.max_sentences = max_sentences
         self.max_wait = max_wait
         self.notify_errors = notify_errors
@@ -120,15 +124,17 @@ class TTSService:
                     continue
                 kind = data.get("type")
                 if kind == "synthesize":
+                    vid = data.get("voice_id", "default")
+                    # unknown voices fall back to the default voice (reference server.py:127-138)
                     await self.queues.enqueue_request(
-                        connection_id=conn_id, text=data.get("text", ""), voice_id=data.get("voice_id", "default"),
+                        connection_id=conn_id, text=data.get("text", ""), voice_id=vid,
                         chunk_size=data.get("chunk_size", self.chunk_size),
-                        exaggeration=data.get("exaggeration", 0.5), streaming=data.get("streaming", True))
+                        exaggeration=data.get("exaggeration", 0.5), streaming=data.get("streaming", True),
+                        voice=self.voices.get(vid))
                 elif kind == "register_voice":
-                    await ws.send_json({"type": "error", "message": "Voice registration failed: "
-                                        "this engine has no voice cloning (FastSpeech2 + HiFi-GAN)"})
+                    await ws.send_json(self.register_voice(data))
                 elif kind == "list_voices":
-                    await ws.send_json({"type": "voice_list", "voices": []})
+                    await ws.send_json({"type": "voice_list", "voices": self.list_voices()})
 
         async def send():
             while True:
@@ -157,11 +163,35 @@ class TTSService:
             self.sockets.pop(conn_id, None)
             self.active_connections -= 1
 
+    def register_voice(self, data: dict) -> dict:
+        """`register_voice` (reference server.py:226-248): this engine conditions on speaker
+        embeddings (HF speaker_embed_dim), so a voice is registered from
+        `{"voice_id", "speaker_embedding": [E floats], "description"}`.  `reference_audio`
+        alone is refused -- computing an embedding from audio needs a speaker encoder this
+        engine does not have -- in the reference's error shape."""
+        vid = data.get("voice_id")
+        emb = data.get("speaker_embedding")
+        dim = getattr(getattr(self.model, "acoustic_cfg", None), "speaker_embed_dim", None)
+        if not vid or emb is None:
+            return {"type": "error", "message": "Voice registration failed: send voice_id and speaker_embedding "
+                                                "(no speaker encoder for reference_audio)"}
+        v = np.asarray(emb, np.float32).reshape(-1)
+        if not dim or v.size != dim or not np.all(np.isfinite(v)):
+            return {"type": "error", "message": f"Voice registration failed: the model takes {dim or 0}-value "
+                                                f"speaker embeddings, got {v.size}"}
+        self.voices[vid] = v
+        self.voice_info[vid] = data.get("description", "")
+        return {"type": "voice_registered", "voice_id": vid}
+
+    def list_voices(self) -> list:
+        return [{"voice_id": k, "description": self.voice_info.get(k, ""), "path": "", "is_cached": True}
+                for k in self.voices]
+
     def health(self):
         info = {"status": "healthy", "device": f"{self.device}:{self.device_index}",
                 "sample_rate": getattr(self.model, "sr", 22050), "active_connections": self.active_connections,
                 "queue_metrics": self.queues.get_metrics(), "synthesizer_stats": dict(self.batcher.stats),
-                "voice_stats": {"total_voices": 0}}
+                "voice_stats": {"total_voices": len(self.voices)}}
         try:
             import torch
             if torch.cuda.is_available():

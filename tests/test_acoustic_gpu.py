@@ -197,3 +197,22 @@ def test_speaker_embedding_file_through_generate(spk_engine, tmp_path):
     assert a.shape == a3.shape and np.abs(a - a3).max() <= 1e-5 * max(1.0, np.abs(a).max())
     assert a.shape != b.shape or not np.allclose(a, b)
     assert n.size > 0
+
+
+def test_generate_batch_mixed_voices_equals_single(spk_engine, tmp_path):
+    """generate_batch with per-sentence voices (some None) == one generate call per sentence."""
+    from gonova_tts_amd.config import AcousticConfig, VocoderConfig
+    from gonova_tts_amd.model import GonovaTTS
+    eng, _ = spk_engine
+    m = GonovaTTS(eng, AcousticConfig(speaker_embed_dim=64), VocoderConfig())
+    texts = ["Good morning.", "A second, longer sentence here.", "Third."]
+    embs = [GS["spk_a_emb"], None, GS["spk_b_emb"]]
+    batch = m.generate_batch(texts, speaker_embeddings=embs)
+    for t, e, got in zip(texts, embs, batch):
+        path = None
+        if e is not None:
+            path = str(tmp_path / f"{abs(hash(t))}.npy")
+            np.save(path, e)
+        ref = m.generate(t, audio_prompt_path=path).squeeze().cpu().numpy()
+        assert got.shape == ref.shape
+        assert np.abs(got - ref).max() <= 1e-4

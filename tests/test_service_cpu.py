@@ -115,3 +115,45 @@ def test_failure_follows_reference_by_default_and_notifies_when_asked():
             assert err["type"] == "synthesis_error"
             fin = ws.receive_json()
             assert fin["type"] == "synthesis_complete"
+
+
+class FakeSpeakerModel(FakeModel):
+    """Multi-speaker fake: records the per-sentence voices the batcher passes."""
+
+    class acoustic_cfg:
+        speaker_embed_dim = 4
+
+    def __init__(self):
+        super().__init__()
+        self.voices = []
+
+    def generate_batch(self, texts, speaker_embeddings=None):
+        with self.lock:
+            self.voices.append(None if speaker_embeddings is None else
+                               [None if e is None else np.asarray(e).tolist() for e in speaker_embeddings])
+        return super().generate_batch(texts)
+
+
+def test_registered_voice_reaches_the_model_per_sentence():
+    """voice_id -> registered speaker embedding -> generate_batch(speaker_embeddings=...)
+    (the reference's voice_id -> audio_prompt_path, server.py:127-138, 226-256)."""
+    model = FakeSpeakerModel()
+    app = create_app(lambda: model)
+    with TestClient(app) as c:
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            ws.send_text(json.dumps({"type": "register_voice", "voice_id": "ann", "speaker_embedding": [1, 2, 3, 4],
+                                     "description": "test"}))
+            assert ws.receive_json() == {"type": "voice_registered", "voice_id": "ann"}
+            ws.send_text(json.dumps({"type": "register_voice", "voice_id": "bad", "speaker_embedding": [1, 2]}))
+            assert ws.receive_json()["type"] == "error"
+            ws.send_text(json.dumps({"type": "list_voices"}))
+            v = ws.receive_json()["voices"]
+            assert [x["voice_id"] for x in v] == ["ann"] and v[0]["description"] == "test"
+            ws.send_text(json.dumps({"type": "synthesize", "text": "Hi there. Bye now.", "voice_id": "ann"}))
+            frames, final = recv_until_complete(ws)
+            assert len(frames) == 2 and final["chunk_id"] == 2
+            ws.send_text(json.dumps({"type": "synthesize", "text": "Plain voice.", "voice_id": "nobody"}))
+            recv_until_complete(ws)
+        assert [[1.0, 2.0, 3.0, 4.0]] * 2 in model.voices  # both sentences carried the voice
+        assert None in model.voices                        # unknown voice -> default voice
+        assert c.get("/health").json()["voice_stats"]["total_voices"] == 1

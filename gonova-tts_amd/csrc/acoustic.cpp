@@ -15,6 +15,7 @@
 
 #include <array>
 #include <cmath>
+#include <cstdlib>
 #include <memory>
 #include <string>
 #include <vector>
@@ -25,6 +26,12 @@
 namespace tts {
 
 namespace {
+
+// TTS_REL_ATTN=0: the unfused attention path (four launches) for A/B and parity tests
+bool rel_attn_enabled() {
+  const char* e = getenv("TTS_REL_ATTN");
+  return !e || atoi(e) != 0;
+}
 
 inline int rup(int x, int m) { return (x + m - 1) / m * m; }
 
@@ -285,6 +292,14 @@ struct AcousticModel::Impl {
       run_layer(L.qkv, Xb, Tp, lens, QKV, Tp, B, dt, s, prof);
       HIP_CHECK(launch_pos_bias(dt, QKV, rows, D, L.pos_u, L.pos_v, Qu, Qv, s));
       HIP_CHECK(launch_transpose_v(dt, QKV, lens, B, Tp, D, H, Sk, Vt, s));
+      if (rel_attn_enabled() && rel_attn_supported(dt, D, H)) {
+        // fused flash-style relative-position attention (attention.hip)
+        HIP_CHECK(launch_rel_attn(dt, Qu, Qv, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale, O, s));
+        run_layer(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
+        ln_rows(Y, Xb, rows, D, L.ln_att, nullptr, s);
+        conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
+        continue;
+      }
       const size_t e = dtype_size(dt);
       // AC[b,h][i][j] = Qu[b][i][h] . K[b][j][h]
       attn_gemm(Qu, (long long)Tp * D, dk, D, lens, Tm, (const char*)QKV + (size_t)D * e, (long long)Tp * 3 * D, dk,
@@ -298,16 +313,20 @@ struct AcousticModel::Impl {
                 (long long)dk * Sk, Sk, dk, Sk, O, (long long)Tp * D, dk, D, B, s);
       run_layer(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
       ln_rows(Y, Xb, rows, D, L.ln_att, nullptr, s);
-      // conv module: x = LN(x + pw2(silu(bn(dw(glu(pw1(x)))))))
-      run_layer(L.pw1, Xb, Tp, lens, A, Tp, B, dt, s, prof);
-      HIP_CHECK(launch_glu_dwconv(dt, A, lens, B, Tp, D, L.dw_w, L.dw_k, L.dw_b, G, s));
-      run_layer(L.pw2, G, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
-      ln_rows(Y, Xb, rows, D, L.ln_conv, nullptr, s);
-      // FFN: x = final_LN(LN(x + 0.5 * ffn(x)))
-      run_layer(L.ff1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
-      run_layer(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
-      ln_rows(Y, Xb, rows, D, L.ln_ff, &L.ln_final, s);
+      conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
     }
+  }
+
+  void conv_module_and_ffn(ConformerLayer& L, void* Xb, const int* lens, int B, int Tp, int rows, hipStream_t s) {
+    // conv module: x = LN(x + pw2(silu(bn(dw(glu(pw1(x)))))))
+    run_layer(L.pw1, Xb, Tp, lens, A, Tp, B, dt, s, prof);
+    HIP_CHECK(launch_glu_dwconv(dt, A, lens, B, Tp, D, L.dw_w, L.dw_k, L.dw_b, G, s));
+    run_layer(L.pw2, G, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
+    ln_rows(Y, Xb, rows, D, L.ln_conv, nullptr, s);
+    // FFN: x = final_LN(LN(x + 0.5 * ffn(x)))
+    run_layer(L.ff1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
+    run_layer(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
+    ln_rows(Y, Xb, rows, D, L.ln_ff, &L.ln_final, s);
   }
 
   void predict(Predictor& Pr, const void* x, const int* lens, int B, int Np, float* out, hipStream_t s) {

@@ -216,3 +216,27 @@ def test_generate_batch_mixed_voices_equals_single(spk_engine, tmp_path):
         ref = m.generate(t, audio_prompt_path=path).squeeze().cpu().numpy()
         assert got.shape == ref.shape
         assert np.abs(got - ref).max() <= 1e-4
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_fused_rel_attention_matches_unfused_and_oracle(aw, dtype, monkeypatch):
+    """The fused relative-position attention (attention.hip, default for 16-bit dtypes)
+    against the four-launch path (TTS_REL_ATTN=0) and the oracle, on a ragged batch whose
+    lengths cross the 64-query / 32-key tile edges (durations forced: predicted durations
+    may legitimately round differently between two 16-bit paths)."""
+    eng = engine(dtype, aw)
+    rng = np.random.default_rng(11)
+    ids_list = [rng.integers(1, 78, size=n) for n in (40, 1, 17, 33)]
+    durs = [np.full(len(x), 5) for x in ids_list]
+    monkeypatch.setenv("TTS_REL_ATTN", "1")
+    fused, lf, _ = run(eng, ids_list, t_cap=200, durations=durs)
+    monkeypatch.setenv("TTS_REL_ATTN", "0")
+    unfused, lu, _ = run(eng, ids_list, t_cap=200, durations=durs)
+    tol = 2.5e-2 if dtype == "bf16" else 5e-3
+    for b, ids in enumerate(ids_list):
+        L = int(lf[b])
+        assert L == int(lu[b]) == len(ids) * 5
+        assert rel_rms(fused[b, :L], unfused[b, :L]) <= tol, (b, rel_rms(fused[b, :L], unfused[b, :L]))
+        ref = acoustic_forward(ids, aw, durations=durs[b])
+        assert rel_rms(fused[b, :L], ref["mel"]) <= 5e-2
+        assert np.all(fused[b, L:] == 0)

@@ -468,10 +468,75 @@ hipError_t launch_embed(int dt, const int* ids, const int* lens, int B, int N, i
                                       (const TT*)E, V, D, scale, (TT*)out));
 }
 
+// 16-bit rows of C <= 512 channels, C % 8 == 0: one 16-byte load / store per lane (lane l
+// owns channels 8l .. 8l+7), same arithmetic as layernorm_kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void layernorm8_kernel(const T* __restrict__ in, T* __restrict__ out, int rows,
+                                                        int C, const float* __restrict__ g1,
+                                                        const float* __restrict__ b1, const float* __restrict__ g2,
+                                                        const float* __restrict__ b2, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int c0 = 8 * lane;
+  const bool on = c0 < C;
+  float v[8];
+  {
+    uint4 u = uint4{0u, 0u, 0u, 0u};
+    if (on) u = *reinterpret_cast<const uint4*>(in + (long long)row * C + c0);
+    const T* e = reinterpret_cast<const T*>(&u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = to_f32(e[i]);
+  }
+  const float invC = 1.f / (float)C;
+  for (int pass = 0; pass < (g2 ? 2 : 1); ++pass) {
+    const float* g = pass ? g2 : g1;
+    const float* bb = pass ? b2 : b1;
+    float sm = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sm += v[i];
+    const float mu = wave_sum(sm) * invC;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = on ? v[i] - mu : 0.f;
+      q += d * d;
+    }
+    const float rstd = rsqrtf(wave_sum(q) * invC + eps);
+    if (on) {
+      const f32x4 ga = *reinterpret_cast<const f32x4*>(g + c0), gb = *reinterpret_cast<const f32x4*>(g + c0 + 4);
+      const f32x4 ba = *reinterpret_cast<const f32x4*>(bb + c0), bc = *reinterpret_cast<const f32x4*>(bb + c0 + 4);
+      const float gg[8] = {ga[0], ga[1], ga[2], ga[3], gb[0], gb[1], gb[2], gb[3]};
+      const float be[8] = {ba[0], ba[1], ba[2], ba[3], bc[0], bc[1], bc[2], bc[3]};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float y = (v[i] - mu) * rstd * gg[i] + be[i];
+        if (pass == 0 && g2) y = to_f32(from_f32<T>(y));  // first LN output is materialised in T
+        v[i] = y;
+      }
+    }
+  }
+  if (on) {
+    T o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = from_f32<T>(v[i]);
+    *reinterpret_cast<uint4*>(out + (long long)row * C + c0) = *reinterpret_cast<const uint4*>(o);
+  }
+}
+
 hipError_t launch_layernorm(int dt, const void* in, void* out, int rows, int C, const float* g1, const float* b1,
                             const float* g2, const float* b2, float eps, hipStream_t s) {
   if (C > 512) return hipErrorInvalidValue;
   dim3 grid((rows + 3) / 4);
+  if (dt != DT_F32 && C % 8 == 0) {
+    if (dt == DT_F16)
+      hipLaunchKernelGGL(layernorm8_kernel<half_t>, grid, dim3(256), 0, s, (const half_t*)in, (half_t*)out, rows, C,
+                         g1, b1, g2, b2, eps);
+    else
+      hipLaunchKernelGGL(layernorm8_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, rows, C,
+                         g1, b1, g2, b2, eps);
+    return hipGetLastError();
+  }
   if (C <= 256) {
     TTS_DISPATCH(dt, hipLaunchKernelGGL((layernorm_kernel<TT, 4>), grid, dim3(256), 0, s, (const TT*)in, (TT*)out,
                                         rows, C, g1, b1, g2, b2, eps));

@@ -193,3 +193,47 @@ def test_resblock_chain_bit_identical_to_pairs(vw, dtype, monkeypatch):
     for b, L in enumerate(lens):
         assert np.array_equal(chain[b], pairs[b]), (b, float(np.abs(chain[b] - pairs[b]).max()))
         assert np.all(chain[b, L * 256:] == 0)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16", "bf16"])
+def test_zero_length_utterance_in_batch(vw, dtype):
+    """An empty utterance (0 frames) inside a ragged batch yields all-zero audio and leaves the
+    other utterances exactly as when run alone (every launch masks per utterance)."""
+    eng = engine_for(dtype, vw)
+    rng = np.random.default_rng(31)
+    lens = [0, 19, 0, 7]
+    mel = torch.from_numpy(rng.standard_normal((4, 19, 80)).astype(np.float32)).to(DEV)
+    wav = eng.vocoder(mel, torch.tensor(lens, dtype=torch.int32)).cpu()
+    assert torch.all(wav[0] == 0) and torch.all(wav[2] == 0)
+    for b in (1, 3):
+        solo = eng.vocoder(mel[b:b + 1, :lens[b]].contiguous()).cpu()
+        assert torch.equal(wav[b, :lens[b] * 256], solo[0])
+        assert torch.all(wav[b, lens[b] * 256:] == 0)
+
+
+def test_long_utterance_matches_oracle_slice(vw):
+    """A 2,600-frame (30 s) utterance: the fp16 default path against the oracle on a window
+    whose receptive field lies inside the utterance (a slice of the full oracle run would
+    take minutes on the CPU; the vocoder is local, so the window is exact up to its edges)."""
+    eng = engine_for("f16", vw)
+    rng = np.random.default_rng(32)
+    T = 2600
+    mel = rng.standard_normal((1, T, 80)).astype(np.float32)
+    wav = eng.vocoder(torch.from_numpy(mel).to(DEV)).cpu().numpy()[0]
+    assert wav.shape == (T * 256,) and np.isfinite(wav).all()
+    w0, w1, ctx = 1800, 1840, 16  # compare frames [w0, w1) computed from frames [w0-ctx, w1+ctx)
+    ref = vocoder_forward(mel[0, w0 - ctx:w1 + ctx], vw)[ctx * 256:(ctx + w1 - w0) * 256]
+    assert rel_rms(wav[w0 * 256:w1 * 256], ref) <= 5e-3
+
+
+def test_bad_arguments_raise_with_the_engine_message(vw):
+    """Errors cross the C-ABI as codes + tts_last_error text and surface as RuntimeError
+    (the reference re-raises model exceptions, synthesizer.py:323-325)."""
+    import ctypes
+    eng = engine_for("f16", vw)
+    rc = eng.lib.tts_vocoder_forward(eng.handle, None, None, 0, 10, None, None)
+    assert rc != 0
+    assert eng.lib.tts_last_error()
+    with pytest.raises(RuntimeError):
+        eng.resample(torch.zeros((1, 8), device=DEV), torch.tensor([8], dtype=torch.int32), 0, 1)
+    del ctypes

@@ -268,6 +268,9 @@ constexpr int XRES_HR = 64;            // output rows per N-wave staged per half
 #ifndef TTS_XRES_PROBE
 #define TTS_XRES_PROBE 0               // timing-only probes for A/B builds (results invalid)
 #endif
+#ifndef TTS_XRES_STORE
+#define TTS_XRES_STORE 2               // output store cache policy (store16 in common.h)
+#endif
 #ifndef TTS_XRES_OCC
 #define TTS_XRES_OCC 3                 // blocks per CU (register budget; LDS tile cap below)
 #endif
@@ -426,6 +429,15 @@ __global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams
 
   // ---- epilogue through LDS: fragments -> fp32 rows -> 8-channel row pieces ----
   T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.syb + (long long)hd * p.syh;
+#if TTS_XRES_PROBE & 2  // timing-only: no epilogue (accumulators kept live)
+  {
+    float z = 0.f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) z += acc[j][0] + acc[j][15];
+    if (z == 1234.5f) Y[tid] = (T)z;
+    return;
+  }
+#endif
   const T* R1 = p.r1 ? reinterpret_cast<const T*>(p.r1) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const T* R2 = p.r2 ? reinterpret_cast<const T*>(p.r2) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const int tlen = p.up_len ? min(p.up_len[b], (p.y_rows - 1) * p.up_s) : 0;
@@ -492,7 +504,21 @@ __global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams
       if (R1) { f32x4 a, c; ld8<T>(reinterpret_cast<const T*>(&res1[half][it]), a, c); v0 += a; v1 += c; }
       if (R2) { f32x4 a, c; ld8<T>(R2 + (long long)row * p.srr + col, a, c); v0 += a; v1 += c; }
       if (p.out_scale != 1.0f) { v0 *= p.out_scale; v1 *= p.out_scale; }
-      st8<T>(Y + (long long)row * p.syr + col, v0, v1);
+#if TTS_XRES_PROBE & 4  // timing-only: row pass without its global stores
+      if (v0[0] == 1234.5f)
+#endif
+      {
+        T e8[8] = {(T)v0[0], (T)v0[1], (T)v0[2], (T)v0[3], (T)v1[0], (T)v1[1], (T)v1[2], (T)v1[3]};
+#if TTS_XRES_PROBE & 8  // timing-only: every block stores into the same 32 KB (L2-resident, no HBM writes)
+        store16<TTS_XRES_STORE>(Y, (int)((((rl & 127) * 16 + cl) * 16) & 0x7fff), *reinterpret_cast<const uint4*>(e8));
+#elif TTS_XRES_PROBE & 16  // timing-only: each block writes its own contiguous 32 KB (same bytes, block-linear)
+        store16<TTS_XRES_STORE>(Y, (int)((blockIdx.x * gridDim.y + blockIdx.y) * 32768 + (((half * 64 + (rl & 63)) * 16 + cl) * 16) % 32768),
+                                *reinterpret_cast<const uint4*>(e8));
+#else
+        store16<TTS_XRES_STORE>(Y, (int)(((long long)row * p.syr + col) * (long long)sizeof(T)),
+                                *reinterpret_cast<const uint4*>(e8));
+#endif
+      }
     }
   }
 }

@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
     T* dst = Y + (long long)gr * C + c8 * 8;
     const uint4 y = *reinterpret_cast<const uint4*>(GT + off);
     const uint4 h = *reinterpret_cast<const uint4*>(Hs + off);
-    *reinterpret_cast<uint4*>(dst) = epi_row<T>(y, h, p.accum, sin[it], p.scale);
+    store16<TTS_ROW_STORE>(Y, (int)((dst - Y) * (long long)sizeof(T)), epi_row<T>(y, h, p.accum, sin[it], p.scale));
   }
 }
 

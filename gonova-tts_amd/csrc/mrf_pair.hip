@@ -241,7 +241,13 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     if (gr >= len) continue;
     T* dst = Y + (long long)gr * C + c8 * 8;
     const uint4 y = *reinterpret_cast<const uint4*>(smem + o * YS16 + c8 * 16);
-    *reinterpret_cast<uint4*>(dst) = epi_row<T>(y, xin[it], p.accum, sin[it], p.scale);
+#if TTS_PAIR_PROBE & 4  // timing-only: every block stores into the same 32 KB (no HBM writes)
+    (void)dst;
+    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(p.y) + ((idx * 16) & 0x7fff)) =
+        epi_row<T>(y, xin[it], p.accum, sin[it], p.scale);
+#else
+    store16<TTS_ROW_STORE>(Y, (int)((dst - Y) * (long long)sizeof(T)), epi_row<T>(y, xin[it], p.accum, sin[it], p.scale));
+#endif
   }
 }
 

@@ -48,6 +48,9 @@ struct Mfma16<bf16_t> {
 #ifndef TTS_PAIR_SU
 #define TTS_PAIR_SU 12
 #endif
+#ifndef TTS_ROW_STORE
+#define TTS_ROW_STORE 2  // cache policy of the pair / chain output stores (store16, common.h)
+#endif
 #ifndef TTS_XCD_REMAP
 #define TTS_XCD_REMAP 1
 #endif

@@ -34,6 +34,9 @@
 #include "kernels.h"
 #include "mrf_tile.h"
 
+#ifndef TTS_PAIR_C256
+#define TTS_PAIR_C256 1  // stage 0 (C = 256) as pair launches; 0: single convs (conv_xres)
+#endif
 #ifndef TTS_PAIR_PROBE
 #define TTS_PAIR_PROBE 0  // timing-only probes for A/B builds (results invalid): 1 no staging loads, 2 no weight reloads
 #endif
@@ -54,7 +57,7 @@ static size_t pair_lds_bytes(int k, int d) {
 }
 
 template <typename T, int C, int K>
-__global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
+__global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPairParams p) {
   using G = PairGeom<C>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int BN = G::BN, WM = G::WM, WN = G::WN, RS = G::RS;
@@ -62,7 +65,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   auto swz = [](int r) { return ((r * G::SW_MUL) >> G::SW_S) & G::SW_M; };  // chunk XOR of row r
   constexpr int NTHR = 256;
   constexpr int KS = C / 32;           // k-steps (of 32 channels) per tap
-  constexpr int MT = 2;                // 16-channel M tiles per wave
+  constexpr int MT = G::MT;            // 16-channel M tiles per wave
   constexpr int S = K * KS;            // k-steps per conv
   constexpr int A2 = (K - 1) / 2;
   constexpr int RT = BN + 2 * A2;      // conv1 rows conv2 needs
@@ -71,7 +74,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   constexpr int NU2 = BN / 16 / WN;    // conv2 tiles per wave
   constexpr int VPR = C / 8;           // 16-byte pieces per row
   constexpr int YS16 = C * 2 + 16;     // output tile staging row stride
-  static_assert(WM * WN * 64 == NTHR && WM * 32 == C, "wave grid");
+  static_assert(WM * WN * 64 == NTHR && WM * 16 * MT == C, "wave grid");
   static_assert(NTHR % VPR == 0, "staging");
   static_assert(2 * A2 <= 16, "conv1 overrun within one tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -93,11 +96,11 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
   char* Ts = smem;                     // T overwrites G after conv1
   const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
   const float slope = p.slope;
-  const int ch0 = 32 * wm + 4 * lq;    // + 16*mt: this lane's 4 output channels
+  const int ch0 = 16 * MT * wm + 4 * lq;  // + 16*mt: this lane's 4 output channels
 
   // weights: [C/16][k][KS][64][8] -> step s of m-tile mb at (mb*S + s) KiB
-  const char* w1 = reinterpret_cast<const char*>(p.w1) + (long long)(2 * wm) * S * 1024 + lane * 16;
-  const char* w2 = reinterpret_cast<const char*>(p.w2) + (long long)(2 * wm) * S * 1024 + lane * 16;
+  const char* w1 = reinterpret_cast<const char*>(p.w1) + (long long)(MT * wm) * S * 1024 + lane * 16;
+  const char* w2 = reinterpret_cast<const char*>(p.w2) + (long long)(MT * wm) * S * 1024 + lane * 16;
   Frag ring[D][MT];
 #pragma unroll
   for (int i = 0; i < D; ++i)
@@ -161,7 +164,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     int tile[NU1];
 #pragma unroll
     for (int u = 0; u < NU1; ++u) tile[u] = 16 * min(wn + WN * u, NT1 - 1) * RS;
-    pair_conv<T, C, S, NU1, D>(acc1, ring, w1, Gs + l15 * RS, d * RS, d, tile, l15, lq);
+    pair_conv<T, C, S, NU1, D, MT>(acc1, ring, w1, Gs + l15 * RS, d * RS, d, tile, l15, lq);
   }
   __builtin_amdgcn_sched_barrier(0);
   // conv2's first weight steps in flight during the conv1 epilogue
@@ -204,7 +207,7 @@ __global__ __launch_bounds__(256, 3) void mrf_pair_kernel(MrfPairParams p) {
     int tile[NU2];
 #pragma unroll
     for (int u = 0; u < NU2; ++u) tile[u] = 16 * (wn + WN * u) * RS;
-    pair_conv<T, C, S, NU2, D>(acc2, ring, w2, Ts + l15 * RS, RS, 1, tile, l15, lq);
+    pair_conv<T, C, S, NU2, D, MT>(acc2, ring, w2, Ts + l15 * RS, RS, 1, tile, l15, lq);
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the epilogue's loads out of the MFMA tail
   // residual h (input rows) and, for accumulating launches, the MRF-sum rows in flight while
@@ -275,7 +278,7 @@ static hipError_t launch_pair_k(const MrfPairParams& p, hipStream_t s) {
 // kernel sizes with a compiled pair kernel: HiFi-GAN V1/V2 (3, 7, 11) and V3 (3, 5, 7);
 // other sizes run the per-conv path
 bool mrf_pair_supported(int dtype, int C, int k) {
-  return (dtype == DT_F16 || dtype == DT_BF16) && (C == 32 || C == 64 || C == 128) &&
+  return (dtype == DT_F16 || dtype == DT_BF16) && (C == 32 || C == 64 || C == 128 || (TTS_PAIR_C256 && C == 256)) &&
          (k == 3 || k == 5 || k == 7 || k == 11);
 }
 
@@ -284,10 +287,12 @@ hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t
   if (dtype == DT_F16) {
     if (C == 32) return launch_pair_k<half_t, 32>(p, s);
     if (C == 64) return launch_pair_k<half_t, 64>(p, s);
+    if (C == 256) return launch_pair_k<half_t, 256>(p, s);
     return launch_pair_k<half_t, 128>(p, s);
   }
   if (C == 32) return launch_pair_k<bf16_t, 32>(p, s);
   if (C == 64) return launch_pair_k<bf16_t, 64>(p, s);
+  if (C == 256) return launch_pair_k<bf16_t, 256>(p, s);
   return launch_pair_k<bf16_t, 128>(p, s);
 }
 

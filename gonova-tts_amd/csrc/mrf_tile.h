@@ -17,17 +17,28 @@ struct PairGeom;
 // only, so it is shared by every 16-row tile and computed once per tap.  At C = 128 the
 // 256-byte rows are one LDS bank row each; chunk ^ ((2r) & 15) keeps the B reads
 // conflict-free for every tap offset (exhaustive check over r mod 16).
+// MT: 16-channel M tiles per wave (a wave owns 16*MT output channels); D: weight-ring depth
+// (k-steps); OCC: blocks per CU the register budget is sized for.
 template <>
 struct PairGeom<32> {
-  static constexpr int BN = 512, WM = 1, WN = 4, RS = 64, SW_MUL = 1, SW_S = 1, SW_M = 3, D = 4;
+  static constexpr int BN = 512, WM = 1, WN = 4, RS = 64, SW_MUL = 1, SW_S = 1, SW_M = 3, D = 4, MT = 2, OCC = 3;
 };
 template <>
 struct PairGeom<64> {
-  static constexpr int BN = 256, WM = 2, WN = 2, RS = 128, SW_MUL = 1, SW_S = 0, SW_M = 7, D = 4;
+  static constexpr int BN = 256, WM = 2, WN = 2, RS = 128, SW_MUL = 1, SW_S = 0, SW_M = 7, D = 4, MT = 2, OCC = 3;
 };
 template <>
 struct PairGeom<128> {
-  static constexpr int BN = 128, WM = 4, WN = 1, RS = 256, SW_MUL = 2, SW_S = 0, SW_M = 15, D = 4;
+  static constexpr int BN = 128, WM = 4, WN = 1, RS = 256, SW_MUL = 2, SW_S = 0, SW_M = 15, D = 4, MT = 2, OCC = 3;
+};
+// C = 256 (HiFi-GAN stage 0): 64-row tiles, 64 channels per wave, two blocks per CU.  The
+// 512-byte rows span two LDS bank rows; the same chunk ^ ((2r) & 15) keeps the B reads
+// conflict-free (the XOR never leaves a chunk's 256-byte half).  Weights streamed per row
+// equal conv_xres's 128-channel x 128-row blocks (both read 2*C*C*k / 64 B per output row
+// and conv), but t never leaves the block.
+template <>
+struct PairGeom<256> {
+  static constexpr int BN = 64, WM = 4, WN = 1, RS = 512, SW_MUL = 2, SW_S = 0, SW_M = 15, D = 3, MT = 4, OCC = 2;
 };
 
 template <typename T>
@@ -159,8 +170,8 @@ __device__ inline void pair_st8(T* p, f32x4 a, f32x4 b) {
 // 2*(D-1) younger loads in flight (a conditional reload made it drain vmcnt to 0 every step).
 // lb: this lane's LDS base (its row rb of the first tile, tap 0); tstep: LDS bytes per tap;
 // trow: rows per tap (swizzle); tile[u]: byte offset of tile u (a multiple of 16 rows).
-template <typename T, int C, int S, int NU, int D>
-__device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][2], typename Mfma<T>::frag (&ring)[D][2],
+template <typename T, int C, int S, int NU, int D, int MT = 2>
+__device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][MT], typename Mfma<T>::frag (&ring)[D][MT],
                                           const char* __restrict__ wp, const char* lb, int tstep, int trow,
                                           const int (&tile)[NU], int rb, int lq) {
   using G = PairGeom<C>;
@@ -178,14 +189,14 @@ __device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][2], typename Mfma<T>:
 #pragma unroll
     for (int u = 0; u < NU; ++u)
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) acc[u][mt] = MF::mma(ring[slot][mt], bf[u], acc[u][mt]);
+      for (int mt = 0; mt < MT; ++mt) acc[u][mt] = MF::mma(ring[slot][mt], bf[u], acc[u][mt]);
 #if defined(TTS_PAIR_PROBE) && (TTS_PAIR_PROBE & 2)
     if (false) {
 #else
     if (reload) {
 #endif
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
         ring[slot][mt] = *reinterpret_cast<const Frag*>(wp + ((long long)mt * S + s + D) * 1024);
       __builtin_amdgcn_sched_barrier(0);  // issue the reload here, D steps ahead of its use
     }

@@ -53,7 +53,7 @@ def per_dispatch(path, counter):
 CHAIN = {(32, 3), (32, 7), (64, 3)}   # (C, k) resblocks run as one chain launch (mrf_chain.hip)
 
 
-def step_launches(B, T, elt=2, pair_channels=(32, 64, 128), chain=CHAIN):
+def step_launches(B, T, elt=2, pair_channels=(32, 64, 128, 256), chain=CHAIN):
     """[(label, algorithmic bytes, algorithmic FLOPs)] of one default-path step, in launch
     order: single convs for stages whose width has no pair kernel (C=256), one chain launch
     per resblock in `chain`, ResBlock-pair launches otherwise."""
@@ -86,7 +86,7 @@ def step_launches(B, T, elt=2, pair_channels=(32, 64, 128), chain=CHAIN):
     return out
 
 
-def fused_step_layers(B, T, elt=2, pair_channels=(32, 64, 128)):
+def fused_step_layers(B, T, elt=2, pair_channels=(32, 64, 128, 256)):
     """[(label, algorithmic bytes)] of one default-path step, in launch order."""
     return [(lab, by) for lab, by, _ in step_launches(B, T, elt, pair_channels)]
 

@@ -27,9 +27,22 @@ template <>
 struct PairGeom<64> {
   static constexpr int BN = 256, WM = 2, WN = 2, RS = 128, SW_MUL = 1, SW_S = 0, SW_M = 7, D = 4, MT = 2, OCC = 3;
 };
+#ifndef TTS_P128_WM
+#define TTS_P128_WM 4
+#endif
+#ifndef TTS_P128_D
+#define TTS_P128_D 4
+#endif
+#ifndef TTS_P128_OCC
+#define TTS_P128_OCC 3
+#endif
+#ifndef TTS_P256_D
+#define TTS_P256_D 2
+#endif
 template <>
 struct PairGeom<128> {
-  static constexpr int BN = 128, WM = 4, WN = 1, RS = 256, SW_MUL = 2, SW_S = 0, SW_M = 15, D = 4, MT = 2, OCC = 3;
+  static constexpr int BN = 128, WM = TTS_P128_WM, WN = 4 / WM, RS = 256, SW_MUL = 2, SW_S = 0, SW_M = 15,
+                       D = TTS_P128_D, MT = 8 / WM, OCC = TTS_P128_OCC;
 };
 // C = 256 (HiFi-GAN stage 0): 64-row tiles, 64 channels per wave, two blocks per CU.  The
 // 512-byte rows span two LDS bank rows; the same chunk ^ ((2r) & 15) keeps the B reads
@@ -38,7 +51,7 @@ struct PairGeom<128> {
 // and conv), but t never leaves the block.
 template <>
 struct PairGeom<256> {
-  static constexpr int BN = 64, WM = 4, WN = 1, RS = 512, SW_MUL = 2, SW_S = 0, SW_M = 15, D = 3, MT = 4, OCC = 2;
+  static constexpr int BN = 64, WM = 4, WN = 1, RS = 512, SW_MUL = 2, SW_S = 0, SW_M = 15, D = TTS_P256_D, MT = 4, OCC = 2;
 };
 
 template <typename T>

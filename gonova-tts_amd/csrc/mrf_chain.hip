@@ -53,12 +53,26 @@ struct ChainGeom;
 #ifndef TTS_CHAIN_C64K7
 #define TTS_CHAIN_C64K7 0          // chain the k = 7 resblock at C = 64 too
 #endif
+#ifndef TTS_CHAIN_OCC32_3
+#define TTS_CHAIN_OCC32_3 3
+#endif
+#ifndef TTS_CHAIN_OCC32_7
+#define TTS_CHAIN_OCC32_7 3
+#endif
+#ifndef TTS_CHAIN_OCC64_3
+#define TTS_CHAIN_OCC64_3 3
+#endif
+// Measured (same-box A/B, tools/ab.sh): smaller tiles at 4-5 blocks per CU (BN 192/192/96) and a
+// third LDS tile that halves the block barriers (2 per pair; LDS then allows 2-3 blocks per CU)
+// were both slower (chains 2.15 -> 2.23-2.72 ms per C2 step): the halo recompute and the
+// occupancy loss cost more than the barriers.  At C = 32 the per-tile epilogue (bias, lrelu,
+// residual, LDS writes) is as long as the tile's 3 MFMAs, so these kernels run at 30-45 % MFMA.
 template <>
-struct ChainGeom<32, 3> { static constexpr int BN = TTS_CHAIN_BN32_3, OCC = 3; };
+struct ChainGeom<32, 3> { static constexpr int BN = TTS_CHAIN_BN32_3, OCC = TTS_CHAIN_OCC32_3; };
 template <>
-struct ChainGeom<32, 7> { static constexpr int BN = TTS_CHAIN_BN32_7, OCC = 3; };
+struct ChainGeom<32, 7> { static constexpr int BN = TTS_CHAIN_BN32_7, OCC = TTS_CHAIN_OCC32_7; };
 template <>
-struct ChainGeom<64, 3> { static constexpr int BN = TTS_CHAIN_BN64_3, OCC = 3; };
+struct ChainGeom<64, 3> { static constexpr int BN = TTS_CHAIN_BN64_3, OCC = TTS_CHAIN_OCC64_3; };
 template <>
 struct ChainGeom<64, 7> { static constexpr int BN = TTS_CHAIN_BN64_7, OCC = TTS_CHAIN_OCC64_7; };
 

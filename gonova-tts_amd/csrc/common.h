@@ -149,4 +149,22 @@ __device__ inline float apply_act(float v, int act, float slope) {
   }
 }
 
+// v_dot2_f32_{f16,bf16}: c + a.lo*b.lo + a.hi*b.hi over packed 16-bit pairs (conv_post)
+template <typename T>
+struct Dot2;
+template <>
+struct Dot2<half_t> {
+  typedef _Float16 v2 __attribute__((ext_vector_type(2)));
+  __device__ static inline float dot(unsigned a, unsigned b, float c) {
+    return __builtin_amdgcn_fdot2(*reinterpret_cast<v2*>(&a), *reinterpret_cast<v2*>(&b), c, false);
+  }
+};
+template <>
+struct Dot2<bf16_t> {
+  typedef __bf16 v2 __attribute__((ext_vector_type(2)));
+  __device__ static inline float dot(unsigned a, unsigned b, float c) {
+    return __builtin_amdgcn_fdot2_f32_bf16(*reinterpret_cast<v2*>(&a), *reinterpret_cast<v2*>(&b), c, false);
+  }
+};
+
 }  // namespace tts

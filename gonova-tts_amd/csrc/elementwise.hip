@@ -109,23 +109,6 @@ __global__ __launch_bounds__(256) void conv_post_kernel(const T* __restrict__ x,
 // distinct slots -- and each sample is 4 x 7 row reads + 112 v_dot2_f32_{f16,bf16}
 // against wave-uniform packed weights.  Thread tid produces samples t0+tid, t0+tid+256.
 template <typename T>
-struct Dot2;
-template <>
-struct Dot2<half_t> {
-  typedef _Float16 v2 __attribute__((ext_vector_type(2)));
-  __device__ static inline float dot(unsigned a, unsigned b, float c) {
-    return __builtin_amdgcn_fdot2(*reinterpret_cast<v2*>(&a), *reinterpret_cast<v2*>(&b), c, false);
-  }
-};
-template <>
-struct Dot2<bf16_t> {
-  typedef __bf16 v2 __attribute__((ext_vector_type(2)));
-  __device__ static inline float dot(unsigned a, unsigned b, float c) {
-    return __builtin_amdgcn_fdot2_f32_bf16(*reinterpret_cast<v2*>(&a), *reinterpret_cast<v2*>(&b), c, false);
-  }
-};
-
-template <typename T>
 __global__ __launch_bounds__(256) void conv_post16_kernel(const T* __restrict__ x, const int* __restrict__ x_len,
                                                           int T_, const unsigned* __restrict__ wpk, float bias,
                                                           int k, float slope, float* __restrict__ wav,

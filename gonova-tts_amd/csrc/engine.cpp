@@ -71,6 +71,14 @@ static bool mrf_chain_enabled() {
   const char* e = getenv("TTS_MRF_CHAIN");
   return e ? atoi(e) != 0 : TTS_MRF_CHAIN_DEFAULT != 0;
 }
+// conv_post inside the vocoder's last pair launch (default on; TTS_POST_FUSE=0: separate launch)
+#ifndef TTS_POST_FUSE_DEFAULT
+#define TTS_POST_FUSE_DEFAULT 1
+#endif
+static bool post_fuse_enabled() {
+  const char* e = getenv("TTS_POST_FUSE");
+  return e ? atoi(e) != 0 : TTS_POST_FUSE_DEFAULT != 0;
+}
 // fused MRF flavour: pair kernels (default) or the whole-stage kernel (TTS_MRF_PAIR=0)
 static bool mrf_pair_enabled() {
   const char* e = getenv("TTS_MRF_PAIR");
@@ -394,6 +402,7 @@ struct tts_engine {
              nullptr, nullptr, 0, 0, 1.f, B, nullptr, dt, s);
     int Tin = T, cin = c0;
     const float slope = 0.1f;
+    bool post_done = false;  // conv_post ran inside the last pair launch
     for (int i = 0; i < nst; ++i) {
       const int ch = v.stage_ch[i];
       const int Tout = Tin * v.up_rate[i];
@@ -448,6 +457,13 @@ struct tts_engine {
             pp.slope = slope;
             pp.accum = (last && j > 0) ? 1 : 0;
             pp.scale = (last && j == nk - 1) ? 1.0f / (float)nk : 1.f;
+            if (last && j == nk - 1 && i == nst - 1 && v.post_wh && post_fuse_enabled() &&
+                mrf_pair_post_supported(dt, ch, v.post_k)) {
+              // the final MRF sum goes straight into conv_post; S is not written
+              pp.post_wpk = v.post_wh; pp.post_b = v.post_b; pp.post_slope = 0.01f; pp.post_k = v.post_k;
+              pp.wav = wav; pp.swb = swb;
+              post_done = true;
+            }
             const double fl = 2.0 * 2.0 * ch * (double)ch * pp.k * (double)B * Tout;
             if (prof.on) {
               Profiler::Rec r{prof.get(), prof.get(), fl, PK_MRF_PAIR};
@@ -505,8 +521,9 @@ struct tts_engine {
       Tin = Tout;
       cin = ch;
     }
-    HIP_CHECK(launch_conv_post(dt, S, Lp(nst), B, Tin, cin, v.post_w, v.post_wh, v.post_b, v.post_k, 0.01f, wav, swb,
-                               s));
+    if (!post_done)
+      HIP_CHECK(launch_conv_post(dt, S, Lp(nst), B, Tin, cin, v.post_w, v.post_wh, v.post_b, v.post_k, 0.01f, wav,
+                                 swb, s));
   }
 };
 

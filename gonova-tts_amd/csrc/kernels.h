@@ -78,8 +78,18 @@ struct MrfPairParams {
   int T, B, k, d;
   float slope, scale;
   int accum;
+  // conv_post fused into the last pair of the vocoder (post_wpk != null; C = 32): the final
+  // MRF sum never leaves the block, wav[b][t] = tanh(post_b + conv_post(lrelu(S, post_slope)))
+  // is written instead of y (zero for len <= t < T).  Bit-identical to launch_conv_post.
+  const void* post_wpk;  // [post_k][C/2] packed 16-bit pairs (the 16-bit conv_post layout)
+  float post_b, post_slope;
+  int post_k;
+  float* wav;
+  long long swb;
 };
 bool mrf_pair_supported(int dtype, int C, int k);
+// the pair launch can carry conv_post (C, k and post_k it was compiled for)
+bool mrf_pair_post_supported(int dtype, int C, int post_k);
 hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s);
 
 // Fused resblock (mrf_chain.hip): the three pairs of one resblock (dilations 1, 3, 5) in one

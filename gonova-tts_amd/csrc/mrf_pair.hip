@@ -45,18 +45,23 @@
 
 namespace tts {
 
-// LDS bytes of one launch (G tile incl. conv1 overrun rows, T tile; >= fp32 output tile)
+// conv_post fused into the vocoder's last pair (POST): the block computes PAIR_PO extra output
+// rows per side so conv_post's halo (post_k <= 2*PAIR_PO + 1 taps) is in the block
+constexpr int PAIR_PO = 8;
+
+// LDS bytes of one launch (G tile incl. conv1 overrun rows, T tile; >= output staging tile)
 template <int C>
-static size_t pair_lds_bytes(int k, int d) {
+static size_t pair_lds_bytes(int k, int d, bool post) {
   using G = PairGeom<C>;
   const int a1 = (k - 1) / 2 * d, a2 = (k - 1) / 2;
-  const int nt1 = (G::BN + 2 * a2 + 15) / 16;
+  const int bo = G::BN + (post ? 2 * PAIR_PO : 0);
+  const int nt1 = (bo + 2 * a2 + 15) / 16;
   const size_t g = (size_t)(16 * nt1 + 2 * a1) * G::RS;
   const size_t t = (size_t)16 * nt1 * G::RS;
-  return std::max(std::max(g, t), (size_t)G::BN * (C * 2 + 16));
+  return std::max(std::max(g, t), (size_t)bo * (C * 2 + 16));
 }
 
-template <typename T, int C, int K>
+template <typename T, int C, int K, bool POST = false>
 __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPairParams p) {
   using G = PairGeom<C>;
   typedef typename Mfma<T>::frag Frag;
@@ -68,10 +73,14 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
   constexpr int MT = G::MT;            // 16-channel M tiles per wave
   constexpr int S = K * KS;            // k-steps per conv
   constexpr int A2 = (K - 1) / 2;
-  constexpr int RT = BN + 2 * A2;      // conv1 rows conv2 needs
+  constexpr int PO = POST ? PAIR_PO : 0;  // extra output rows per side (conv_post's halo)
+  constexpr int BO = BN + 2 * PO;      // output rows: block row o <-> utterance row n0 - PO + o
+  constexpr int RT = BO + 2 * A2;      // conv1 rows conv2 needs
   constexpr int NT1 = (RT + 15) / 16;  // conv1 tiles (block)
   constexpr int NU1 = (NT1 + WN - 1) / WN;  // conv1 tiles per wave (the last may be a repeat)
-  constexpr int NU2 = BN / 16 / WN;    // conv2 tiles per wave
+  constexpr int NT2 = BO / 16;         // conv2 tiles (block)
+  constexpr int NU2 = (NT2 + WN - 1) / WN;  // conv2 tiles per wave (the last may be a repeat)
+  static_assert(!POST || (C == 32 && BN == 512), "conv_post fusion: C = 32, two samples per thread");
   constexpr int VPR = C / 8;           // 16-byte pieces per row
   constexpr int YS16 = C * 2 + 16;     // output tile staging row stride
   static_assert(WM * WN * 64 == NTHR && WM * 16 * MT == C, "wave grid");
@@ -83,15 +92,21 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
   if (!xcd_tile((p.T + BN - 1) / BN, p.B, b, tile0)) return;
   const int n0 = tile0 * BN;
   const int len = min(p.len[b], p.T);
-  if (n0 >= len) return;
   const int tid = threadIdx.x;
+  if (n0 >= len) {
+    if constexpr (POST) {  // conv_post's grid covered every row: zeros past the utterance
+      if (n0 + tid < p.T) p.wav[b * p.swb + n0 + tid] = 0.f;
+      if (n0 + tid + 256 < p.T) p.wav[b * p.swb + n0 + tid + 256] = 0.f;
+    }
+    return;
+  }
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = WM == 1 ? 0 : wave % WM, wn = WN == 1 ? 0 : wave / WM;
   const int l15 = lane & 15, lq = lane >> 4;
   const int d = p.d;
   const int a1 = A2 * d;
-  const int RG = BN + 2 * (a1 + A2);
+  const int RG = BO + 2 * (a1 + A2);
   char* Gs = smem;
   char* Ts = smem;                     // T overwrites G after conv1
   const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
@@ -112,7 +127,7 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
   {
     const int cc = tid % VPR, r0 = tid / VPR;
     constexpr int rstep = NTHR / VPR;
-    const int gs = n0 - a1 - A2;
+    const int gs = n0 - PO - a1 - A2;
     const T* xc = X + cc * 8;
     if (gs >= 0 && gs + RG <= len) {  // interior tile: no clamps, no masks
       for (int rb = r0; rb < RG; rb += PAIR_SU * rstep) {
@@ -152,7 +167,7 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
   }
   __syncthreads();
 
-  // ---- conv1 over T rows [0, 16*NT1): T row t <-> global row n0 - a2 + t ----
+  // ---- conv1 over T rows [0, 16*NT1): T row t <-> global row n0 - PO - a2 + t ----
   // Tiles are dealt round-robin to the WN waves of an M slice; a wave whose share is one
   // short repeats the block's last tile (straight-line loop, result not stored).
   f32x4 acc1[NU1][MT];
@@ -182,7 +197,7 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
     for (int u = 0; u < NU1; ++u)
       if (NT1 % WN == 0 || wn + WN * u < NT1) {
         const int tr = 16 * (wn + WN * u) + l15;
-        const int gr = n0 - A2 + tr;
+        const int gr = n0 - PO - A2 + tr;
         const bool valid = gr >= 0 && gr < len;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
@@ -195,7 +210,8 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
   }
   __syncthreads();
 
-  constexpr int NIT = BN * VPR / NTHR;  // 16-byte row pieces per thread in the row pass
+  constexpr int NIT = (BO * VPR + NTHR - 1) / NTHR;  // 16-byte row pieces per thread in the row pass
+  static_assert(POST || BO * VPR % NTHR == 0, "row pass");
 
   // ---- conv2 over the BN output rows: output row o reads T rows o .. o + 2*a2 ----
   f32x4 acc2[NU2][MT];
@@ -206,7 +222,7 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
   {
     int tile[NU2];
 #pragma unroll
-    for (int u = 0; u < NU2; ++u) tile[u] = 16 * (wn + WN * u) * RS;
+    for (int u = 0; u < NU2; ++u) tile[u] = 16 * min(wn + WN * u, NT2 - 1) * RS;
     pair_conv<T, C, S, NU2, D, MT>(acc2, ring, w2, Ts + l15 * RS, RS, 1, tile, l15, lq);
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the epilogue's loads out of the MFMA tail
@@ -217,25 +233,78 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
   T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
   const auto yrsrc = __builtin_amdgcn_make_buffer_rsrc(Y, 0, p.accum ? len * C * (int)sizeof(T) : 0, 0x00020000);
   uint4 xin[NIT], sin[NIT];
+  auto load_rows = [&](bool lx, bool ls) __attribute__((always_inline)) {
 #pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int idx = tid + it * NTHR;
-    const int e = min(n0 + idx / VPR, len - 1) * C + (idx % VPR) * 8;
-    xin[it] = *reinterpret_cast<const uint4*>(X + e);
-    sin[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrsrc, e * (int)sizeof(T), 0, 0));
-  }
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NTHR;
+      const int e = min(max(n0 - PO + idx / VPR, 0), len - 1) * C + (idx % VPR) * 8;
+      if (lx) xin[it] = *reinterpret_cast<const uint4*>(X + e);
+      if (ls) sin[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrsrc, e * (int)sizeof(T), 0, 0));
+    }
+  };
+  // with conv_post fused the residual rows wait until the accumulators are staged (registers)
+  load_rows(!POST, true);
   f32x4 bias[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2 + ch0 + 16 * mt);
   __syncthreads();  // T no longer read
 #pragma unroll
-  for (int u = 0; u < NU2; ++u) {
-    const int o = 16 * (wn + WN * u) + l15;
+  for (int u = 0; u < NU2; ++u)
+    if (NT2 % WN == 0 || wn + WN * u < NT2) {
+      const int o = 16 * (wn + WN * u) + l15;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-      *reinterpret_cast<uint2*>(smem + o * YS16 + (ch0 + 16 * mt) * 2) = epi_conv2<T>(acc2[u][mt], bias[mt]);
-  }
+      for (int mt = 0; mt < MT; ++mt)
+        *reinterpret_cast<uint2*>(smem + o * YS16 + (ch0 + 16 * mt) * 2) = epi_conv2<T>(acc2[u][mt], bias[mt]);
+    }
   __syncthreads();
+  if constexpr (POST) {
+    // final MRF-sum rows (rounded to T as the unfused path stores them) -> lrelu -> LDS tile
+    // [BO][32] (chunk c of row r at c ^ ((r >> 2) & 3), conv_post16's layout), then conv_post
+    // for the BN rows in conv_post16's arithmetic order
+    load_rows(true, false);
+    uint4 gv[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NTHR;
+      const int o = min(idx / VPR, BO - 1), c8 = idx % VPR;
+      const int gr = n0 - PO + o;
+      const uint4 y = *reinterpret_cast<const uint4*>(smem + o * YS16 + c8 * 16);
+      const uint4 v = lrelu_chunk<T>(epi_row<T>(y, xin[it], p.accum, sin[it], p.scale), p.post_slope);
+      gv[it] = (gr >= 0 && gr < len) ? v : uint4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();  // output staging no longer read
+    auto slot = [](int r, int c) { return r * 64 + ((c ^ ((r >> 2) & 3)) << 4); };
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NTHR;
+      if (idx < BO * VPR) *reinterpret_cast<uint4*>(smem + slot(idx / VPR, idx % VPR)) = gv[it];
+    }
+    __syncthreads();
+    const unsigned* wpk = reinterpret_cast<const unsigned*>(p.post_wpk);
+    const int r0 = PO - (p.post_k - 1) / 2 + tid;
+    float acc0 = p.post_b, acc1 = p.post_b;
+    for (int j = 0; j < p.post_k; ++j) {
+      const unsigned* wj = wpk + j * (C / 2);
+#pragma unroll
+      for (int c = 0; c < VPR; ++c) {
+        const uint4 a = *reinterpret_cast<const uint4*>(smem + slot(r0 + j, c));
+        const uint4 e = *reinterpret_cast<const uint4*>(smem + slot(r0 + 256 + j, c));
+        acc0 = Dot2<T>::dot(a.x, wj[4 * c + 0], acc0);
+        acc0 = Dot2<T>::dot(a.y, wj[4 * c + 1], acc0);
+        acc0 = Dot2<T>::dot(a.z, wj[4 * c + 2], acc0);
+        acc0 = Dot2<T>::dot(a.w, wj[4 * c + 3], acc0);
+        acc1 = Dot2<T>::dot(e.x, wj[4 * c + 0], acc1);
+        acc1 = Dot2<T>::dot(e.y, wj[4 * c + 1], acc1);
+        acc1 = Dot2<T>::dot(e.z, wj[4 * c + 2], acc1);
+        acc1 = Dot2<T>::dot(e.w, wj[4 * c + 3], acc1);
+      }
+    }
+    const int ta = n0 + tid, tb = ta + 256;
+    float* wv = p.wav + b * p.swb;
+    if (ta < p.T) wv[ta] = ta < len ? tanhf(acc0) : 0.f;
+    if (tb < p.T) wv[tb] = tb < len ? tanhf(acc1) : 0.f;
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int idx = tid + it * NTHR;
@@ -254,23 +323,23 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
   }
 }
 
-template <typename T, int C, int K>
+template <typename T, int C, int K, bool POST = false>
 static hipError_t launch_pair_t(const MrfPairParams& p, hipStream_t s) {
   using G = PairGeom<C>;
-  const size_t lds = pair_lds_bytes<C>(K, p.d);
+  const size_t lds = pair_lds_bytes<C>(K, p.d, POST);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   dim3 grid(xcd_grid((p.T + G::BN - 1) / G::BN, p.B));
-  hipLaunchKernelGGL((mrf_pair_kernel<T, C, K>), grid, dim3(256), lds, s, p);
+  hipLaunchKernelGGL((mrf_pair_kernel<T, C, K, POST>), grid, dim3(256), lds, s, p);
   return hipGetLastError();
 }
 
-template <typename T, int C>
+template <typename T, int C, bool POST = false>
 static hipError_t launch_pair_k(const MrfPairParams& p, hipStream_t s) {
   switch (p.k) {
-    case 3: return launch_pair_t<T, C, 3>(p, s);
-    case 5: return launch_pair_t<T, C, 5>(p, s);
-    case 7: return launch_pair_t<T, C, 7>(p, s);
-    case 11: return launch_pair_t<T, C, 11>(p, s);
+    case 3: return launch_pair_t<T, C, 3, POST>(p, s);
+    case 5: return launch_pair_t<T, C, 5, POST>(p, s);
+    case 7: return launch_pair_t<T, C, 7, POST>(p, s);
+    case 11: return launch_pair_t<T, C, 11, POST>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -282,8 +351,17 @@ bool mrf_pair_supported(int dtype, int C, int k) {
          (k == 3 || k == 5 || k == 7 || k == 11);
 }
 
+bool mrf_pair_post_supported(int dtype, int C, int post_k) {
+  return (dtype == DT_F16 || dtype == DT_BF16) && C == 32 && post_k >= 1 && post_k % 2 == 1 &&
+         post_k <= 2 * PAIR_PO + 1;
+}
+
 hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s) {
   if (!mrf_pair_supported(dtype, C, p.k) || p.d < 1) return hipErrorInvalidValue;
+  if (p.post_wpk) {
+    if (!mrf_pair_post_supported(dtype, C, p.post_k) || !p.wav) return hipErrorInvalidValue;
+    return dtype == DT_F16 ? launch_pair_k<half_t, 32, true>(p, s) : launch_pair_k<bf16_t, 32, true>(p, s);
+  }
   if (dtype == DT_F16) {
     if (C == 32) return launch_pair_k<half_t, 32>(p, s);
     if (C == 64) return launch_pair_k<half_t, 64>(p, s);

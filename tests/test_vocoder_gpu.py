@@ -195,6 +195,26 @@ def test_resblock_chain_bit_identical_to_pairs(vw, dtype, monkeypatch):
         assert np.all(chain[b, L * 256:] == 0)
 
 
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_fused_conv_post_bit_identical(vw, dtype, monkeypatch):
+    """conv_post inside the last pair launch (its halo rows computed in the block, the final
+    MRF sum never written) reproduces the separate conv_post launch bit for bit: ragged and
+    empty utterances, a batch length that is not a whole number of 512-row tiles, utterances
+    shorter than one tile, and the zero tail past every utterance."""
+    eng = engine_for(dtype, vw)
+    rng = np.random.default_rng(23)
+    lens = [71, 1, 2, 0, 33, 64]
+    mel = torch.from_numpy(rng.standard_normal((6, 71, 80)).astype(np.float32)).to(DEV)
+    ln = torch.tensor(lens, dtype=torch.int32)
+    monkeypatch.setenv("TTS_POST_FUSE", "1")
+    fused = eng.vocoder(mel, ln).cpu().numpy()
+    monkeypatch.setenv("TTS_POST_FUSE", "0")
+    sep = eng.vocoder(mel, ln).cpu().numpy()
+    for b, L in enumerate(lens):
+        assert np.array_equal(fused[b], sep[b]), (b, float(np.abs(fused[b] - sep[b]).max()))
+        assert np.all(fused[b, L * 256:] == 0)
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f16", "bf16"])
 def test_zero_length_utterance_in_batch(vw, dtype):
     """An empty utterance (0 frames) inside a ragged batch yields all-zero audio and leaves the

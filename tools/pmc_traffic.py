@@ -53,16 +53,20 @@ def per_dispatch(path, counter):
 CHAIN = {(32, 3), (32, 7), (64, 3)}   # (C, k) resblocks run as one chain launch (mrf_chain.hip)
 
 
-def step_launches(B, T, elt=2, pair_channels=(32, 64, 128, 256), chain=CHAIN):
+def step_launches(B, T, elt=2, pair_channels=(32, 64, 128, 256), chain=CHAIN, post_fused=True):
     """[(label, algorithmic bytes, algorithmic FLOPs)] of one default-path step, in launch
-    order: single convs for stages whose width has no pair kernel (C=256), one chain launch
-    per resblock in `chain`, ResBlock-pair launches otherwise."""
+    order: single convs for stages whose width has no pair kernel, one chain launch per
+    resblock in `chain`, ResBlock-pair launches otherwise; conv_post inside the last pair
+    launch when `post_fused` (the final MRF sum is not written, the waveform is)."""
     out = []
     npairs = {}
     for name, M, cin, k, n in vocoder_layers(T):
         st = name.split(".")[0]
         f = 2.0 * M * cin * k * n * B
-        if name == "post":
+        if name == "post" and post_fused and out and ".pair" in out[-1][0]:
+            lab, by, fl = out[-1]
+            out[-1] = (lab + "+post", by - B * n * cin * elt + B * n * 4, fl + f)
+        elif name == "post":
             out.append(("post", B * n * cin * elt + B * n * 4, f))
         elif name == "pre" or name.endswith(".up"):
             out.append((name, B * n * cin * elt + B * n * M * elt + M * cin * k * elt, f))

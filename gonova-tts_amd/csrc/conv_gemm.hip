@@ -551,9 +551,23 @@ static int xres_mode() {  // TTS_CONV_XRES=0 disables the X-resident kernel (A/B
 // BN = 256) for M = 64 (the last upsampler)
 static int xres_wm(const ConvParams& p) { return p.M >= 128 ? 4 : 2; }
 
-template <typename T, int WM>
+#ifndef TTS_XRES_SMALL_TILES
+#define TTS_XRES_SMALL_TILES 1
+#endif
+// 64-row tiles (NT = 2) where 128-row tiles would leave much of the last tile of every
+// utterance empty (the encoder's 144 rows: 3 x 64 = 192 rows of work instead of 2 x 128)
+static int xres_nt(const ConvParams& p, int wm) {
+  const char* e = getenv("TTS_XRES_NT");  // 2 / 4 force a tile height (tests), else automatic
+  if (wm != 4) return 4;
+  if (e && (atoi(e) == 2 || atoi(e) == 4)) return atoi(e);
+  if (!TTS_XRES_SMALL_TILES) return 4;
+  const int r4 = (p.y_rows + 127) / 128 * 128, r2 = (p.y_rows + 63) / 64 * 64;
+  return 8 * r2 <= 7 * r4 ? 2 : 4;
+}
+
+template <typename T, int WM, int NT = 4>
 static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s) {
-  constexpr int NT = 4, BM = 32 * WM, BN = 32 * NT * (4 / WM);
+  constexpr int BM = 32 * WM, BN = 32 * NT * (4 / WM);
   const size_t lds = std::max((size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16),
                               (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
   dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
@@ -565,9 +579,13 @@ template <typename T>
 static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err) {
   if (!xres_mode()) return false;
   const int wm = xres_wm(p);
-  const int cg = xres_group(p, 32 * 4 * (4 / wm));
+  const int nt = xres_nt(p, wm);
+  const int cg = xres_group(p, 32 * nt * (4 / wm));  // channel group sized for the tile's rows
   if (!cg) return false;
-  *err = wm == 4 ? launch_xres_wm<T, 4>(p, cg, s) : launch_xres_wm<T, 2>(p, cg, s);
+  if (wm == 2)
+    *err = launch_xres_wm<T, 2>(p, cg, s);
+  else
+    *err = nt == 2 ? launch_xres_wm<T, 4, 2>(p, cg, s) : launch_xres_wm<T, 4>(p, cg, s);
   return true;
 }
 

@@ -37,6 +37,9 @@
 #ifndef TTS_PAIR_C256
 #define TTS_PAIR_C256 1  // stage 0 (C = 256) as pair launches; 0: single convs (conv_xres)
 #endif
+#ifndef TTS_PAIR_MTO_MIN
+#define TTS_PAIR_MTO_MIN 64  // pair_conv's M-tile-outer MFMA order from this channel count up
+#endif
 #ifndef TTS_PAIR_PROBE
 #define TTS_PAIR_PROBE 0  // timing-only probes for A/B builds (results invalid): 1 no staging loads, 2 no weight reloads
 #endif
@@ -179,7 +182,7 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
     int tile[NU1];
 #pragma unroll
     for (int u = 0; u < NU1; ++u) tile[u] = 16 * min(wn + WN * u, NT1 - 1) * RS;
-    pair_conv<T, C, S, NU1, D, MT>(acc1, ring, w1, Gs + l15 * RS, d * RS, d, tile, l15, lq);
+    pair_conv<T, C, S, NU1, D, MT, (C >= TTS_PAIR_MTO_MIN)>(acc1, ring, w1, Gs + l15 * RS, d * RS, d, tile, l15, lq);
   }
   __builtin_amdgcn_sched_barrier(0);
   // conv2's first weight steps in flight during the conv1 epilogue
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
     int tile[NU2];
 #pragma unroll
     for (int u = 0; u < NU2; ++u) tile[u] = 16 * min(wn + WN * u, NT2 - 1) * RS;
-    pair_conv<T, C, S, NU2, D, MT>(acc2, ring, w2, Ts + l15 * RS, RS, 1, tile, l15, lq);
+    pair_conv<T, C, S, NU2, D, MT, (C >= TTS_PAIR_MTO_MIN)>(acc2, ring, w2, Ts + l15 * RS, RS, 1, tile, l15, lq);
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the epilogue's loads out of the MFMA tail
   // residual h (input rows) and, for accumulating launches, the MRF-sum rows in flight while

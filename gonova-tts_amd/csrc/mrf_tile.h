@@ -183,7 +183,10 @@ __device__ inline void pair_st8(T* p, f32x4 a, f32x4 b) {
 // 2*(D-1) younger loads in flight (a conditional reload made it drain vmcnt to 0 every step).
 // lb: this lane's LDS base (its row rb of the first tile, tap 0); tstep: LDS bytes per tap;
 // trow: rows per tap (swizzle); tile[u]: byte offset of tile u (a multiple of 16 rows).
-template <typename T, int C, int S, int NU, int D, int MT = 2>
+// MTO: MFMA order within a step -- M tile outer (each A fragment feeds NU MFMAs back to
+// back) or row tile outer.  Same-box A/B: M-outer 1-3 % faster for the C = 64 / 128 / 256
+// pairs, slower for C = 32 and the chains.
+template <typename T, int C, int S, int NU, int D, int MT = 2, bool MTO = false>
 __device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][MT], typename Mfma<T>::frag (&ring)[D][MT],
                                           const char* __restrict__ wp, const char* lb, int tstep, int trow,
                                           const int (&tile)[NU], int rb, int lq) {
@@ -199,10 +202,17 @@ __device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][MT], typename Mfma<T>
     Frag bf[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) bf[u] = *reinterpret_cast<const Frag*>(bp + tile[u]);
+    if constexpr (MTO) {  // one A fragment held across the NU tiles
 #pragma unroll
-    for (int u = 0; u < NU; ++u)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[u][mt] = MF::mma(ring[slot][mt], bf[u], acc[u][mt]);
+        for (int u = 0; u < NU; ++u) acc[u][mt] = MF::mma(ring[slot][mt], bf[u], acc[u][mt]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[u][mt] = MF::mma(ring[slot][mt], bf[u], acc[u][mt]);
+    }
 #if defined(TTS_PAIR_PROBE) && (TTS_PAIR_PROBE & 2)
     if (false) {
 #else

@@ -17,9 +17,10 @@ data-path collective (weak scaling); the timed loop is bracketed by barriers and
 the max time over ranks is used.  value = samples of all ranks / max time.
 
 `roofline` is for the dominant kernel family (largest summed time per step: today the
-fused ResBlock-pair kernel of stages 1-3), timed live with hipEvents around every launch
+fused ResBlock-pair kernel of all four stages), timed live with hipEvents around every launch
 on the stream it runs on; `roofline.kernels` lists every family the same way
-(conv_gemm_kernel, conv_xres_kernel, mrf_fused_kernel, mrf_pair_kernel).  `cpu_baseline`
+(conv_gemm_kernel, conv_xres_kernel, mrf_fused_kernel, mrf_pair_kernel, mrf_chain_kernel,
+upsample_stream_kernel).  `cpu_baseline`
 is the NumPy oracle on the host cores (bounded sample, rank 0, N=1 only).
 """
 from __future__ import annotations

@@ -79,6 +79,14 @@ static bool post_fuse_enabled() {
   const char* e = getenv("TTS_POST_FUSE");
   return e ? atoi(e) != 0 : TTS_POST_FUSE_DEFAULT != 0;
 }
+// streaming upsampler for the small stages (default on; TTS_UP_STREAM=0: conv_xres)
+#ifndef TTS_UP_STREAM_DEFAULT
+#define TTS_UP_STREAM_DEFAULT 1
+#endif
+static bool up_stream_enabled() {
+  const char* e = getenv("TTS_UP_STREAM");
+  return e ? atoi(e) != 0 : TTS_UP_STREAM_DEFAULT != 0;
+}
 // fused MRF flavour: pair kernels (default) or the whole-stage kernel (TTS_MRF_PAIR=0)
 static bool mrf_pair_enabled() {
   const char* e = getenv("TTS_MRF_PAIR");
@@ -159,6 +167,7 @@ struct tts_engine {
     ConvLayer L;
     L.w = track(upload(p, dt));
     L.wpk = frag_pack(p, M, taps, ci, dt, allocs);
+    if (upsample_stream_supported(dt, ci, M, taps)) L.wup16 = frag_pack_up16(p, M, taps * ci, dt, allocs);
     const auto& bh = get(bname).data;
     std::vector<float> b(M);
     for (int r = 0; r < s; ++r)
@@ -408,8 +417,26 @@ struct tts_engine {
       const int Tout = Tin * v.up_rate[i];
       const long long sb = (long long)Tout * ch;
       // lrelu -> ConvTranspose1d (polyphase)
-      run_conv(v.ups[i], S, (long long)Tin * cin, cin, Lp(i), Tin, XS, sb, ch, Up(i), Tin + 1, slope,
-               nullptr, nullptr, 0, 0, 1.f, B, Lp(i + 1), dt, s);
+      const ConvLayer& U = v.ups[i];
+      if (U.wup16 && up_stream_enabled()) {
+        UpsampleParams up{};
+        up.x = S; up.sxb = (long long)Tin * cin; up.len = Lp(i); up.up_len = Lp(i + 1);
+        up.wpk = U.wup16; up.bias = U.bias; up.y = XS; up.syb = sb;
+        up.T = Tin; up.B = B; up.s = U.up_s; up.co = U.up_cout; up.pad = U.up_p; up.slope = slope;
+        const double fl = 2.0 * U.M * (double)U.Cin * U.taps * (double)B * Tin;
+        if (prof.on) {
+          Profiler::Rec r{prof.get(), prof.get(), fl, PK_UPSAMPLE};
+          HIP_CHECK(hipEventRecord(r.a, s));
+          HIP_CHECK(upsample_stream_launch(dt, U.Cin, U.M, up, s));
+          HIP_CHECK(hipEventRecord(r.b, s));
+          prof.recs.push_back(r);
+        } else {
+          HIP_CHECK(upsample_stream_launch(dt, U.Cin, U.M, up, s));
+        }
+      } else {
+        run_conv(U, S, (long long)Tin * cin, cin, Lp(i), Tin, XS, sb, ch, Up(i), Tin + 1, slope, nullptr, nullptr,
+                 0, 0, 1.f, B, Lp(i + 1), dt, s);
+      }
       const int nk = (int)v.mrf[i].size();
       bool pair_ok = mrf_fused_enabled() && mrf_pair_enabled();
       for (int j = 0; j < nk && pair_ok; ++j)

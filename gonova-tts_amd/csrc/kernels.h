@@ -40,7 +40,7 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why);
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s);
 
 // kernel family a launch runs as (live profiling buckets; tts_engine_profile_read_kinds)
-enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_MRF_FUSED = 2, PK_MRF_PAIR = 3, PK_MRF_CHAIN = 4, PK_N = 5 };
+enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_MRF_FUSED = 2, PK_MRF_PAIR = 3, PK_MRF_CHAIN = 4, PK_UPSAMPLE = 5, PK_N = 6 };
 int conv_gemm_kind(int dtype, const ConvParams& p);
 
 // Fused MRF stage (mrf_fused.hip): all resblocks of one HiFi-GAN stage in one launch.
@@ -88,6 +88,24 @@ struct MrfPairParams {
   long long swb;
 };
 bool mrf_pair_supported(int dtype, int C, int k);
+
+// Streaming ConvTranspose1d with two taps (k = 2s) for the small upsamplers (upsample.hip):
+// x [B][T][Cin] (len[b] valid rows) -> y [B][T*s][Co], rows s*u + r - pad for u = 0 .. len,
+// r < s, clipped to [0, up_len[b]); weights packed as [M/16][2*Cin/32][64][8] (M = s*Co,
+// K = tap*Cin + ci), LeakyReLU(slope) on the input.
+struct UpsampleParams {
+  const void* x;
+  long long sxb, syb;
+  const int* len;
+  const int* up_len;
+  const void* wpk;
+  const float* bias;  // fp32 [M]
+  void* y;
+  int T, B, s, co, pad;
+  float slope;
+};
+bool upsample_stream_supported(int dtype, int Cin, int M, int taps);
+hipError_t upsample_stream_launch(int dtype, int Cin, int M, const UpsampleParams& p, hipStream_t s);
 // the pair launch can carry conv_post (C, k and post_k it was compiled for)
 bool mrf_pair_post_supported(int dtype, int C, int post_k);
 hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s);

@@ -65,6 +65,7 @@ struct ConvLayer {
   void* w = nullptr;
   void* wpk = nullptr;    // fragment-packed copy (frag_pack), or null
   void* wpk16 = nullptr;  // 16x16 fragment-packed copy (frag_pack16, MRF convs at C <= 64), or null
+  void* wup16 = nullptr;  // transposed conv: [M/16][K/32][64][8] copy (frag_pack_up16), or null
   float* bias = nullptr;
   int M = 0, Cin = 0, taps = 1, dil = 1, pad = 0;
   int up_s = 0, up_cout = 0, up_p = 0;  // transposed-conv output mapping
@@ -107,6 +108,22 @@ inline void* frag_pack16(const std::vector<float>& w, int C, int k, int dt, std:
           const int m = mb * 16 + (l & 15);
           for (int j = 0; j < 8; ++j, ++o) p[o] = w[((size_t)m * C + ks * 32 + 8 * (l >> 4) + j) * k + t];
         }
+  void* d = upload(p, dt);
+  allocs.push_back(d);
+  return d;
+}
+
+// Packing for upsample_stream_kernel: W'[M][K] (host fp32, K = tap*Cin + ci) ->
+//   P[M/16][K/32][lane 0..63][8],  lane l holding row 16*mt + (l & 15), k 32*ks + 8*(l >> 4) + [0, 8)
+// (the A operand of v_mfma_f32_16x16x32_*; one 1 KiB LDS fragment per (mt, ks)).
+inline void* frag_pack_up16(const std::vector<float>& w, int M, int K, int dt, std::vector<void*>& allocs) {
+  if (dt == DT_F32 || M % 16 || K % 32) return nullptr;
+  std::vector<float> p((size_t)M * K);
+  size_t o = 0;
+  for (int mt = 0; mt < M / 16; ++mt)
+    for (int ks = 0; ks < K / 32; ++ks)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j, ++o) p[o] = w[(size_t)(mt * 16 + (l & 15)) * K + ks * 32 + 8 * (l >> 4) + j];
   void* d = upload(p, dt);
   allocs.push_back(d);
   return d;

@@ -286,7 +286,8 @@ class HipEngine:
               "profile_read")
         return ms.value, fl.value, n.value
 
-    PROFILE_KINDS = ("conv_gemm_kernel", "conv_xres_kernel", "mrf_fused_kernel", "mrf_pair_kernel", "mrf_chain_kernel")
+    PROFILE_KINDS = ("conv_gemm_kernel", "conv_xres_kernel", "mrf_fused_kernel", "mrf_pair_kernel", "mrf_chain_kernel",
+                     "upsample_stream_kernel")
 
     def profile_read_kinds(self):
         """-> {kernel name: (summed ms, algorithmic FLOPs, launch count)}; resets."""

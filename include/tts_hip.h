@@ -115,7 +115,7 @@ int tts_engine_profile(tts_engine* eng, int enable);
 int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops, int* n_launches);
 /* The same, split by kernel family into arrays of nkinds entries:
  * 0 = conv_gemm_kernel, 1 = conv_xres_kernel, 2 = mrf_fused_kernel, 3 = mrf_pair_kernel,
- * 4 = mrf_chain_kernel. */
+ * 4 = mrf_chain_kernel, 5 = upsample_stream_kernel. */
 int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, double* flops, int* n_launches);
 
 /* Rational-rate resampling of waveforms (22,050 -> 24,000 Hz for

@@ -215,6 +215,30 @@ def test_fused_conv_post_bit_identical(vw, dtype, monkeypatch):
         assert np.all(fused[b, L * 256:] == 0)
 
 
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_streaming_upsampler_matches_conv_path(vw, dtype, monkeypatch):
+    """The streaming transposed-conv kernel of stages 2-3 (weights in LDS, B fragments straight
+    from HBM, zero rows outside each utterance through the buffer descriptor) against the
+    conv_xres polyphase path and the oracle: ragged and empty utterances, lengths that end
+    mid-item; the zero tail past each utterance stays zero."""
+    eng = engine_for(dtype, vw)
+    rng = np.random.default_rng(24)
+    lens = [45, 1, 0, 17, 32]
+    mel = torch.from_numpy(rng.standard_normal((5, 45, 80)).astype(np.float32)).to(DEV)
+    ln = torch.tensor(lens, dtype=torch.int32)
+    monkeypatch.setenv("TTS_UP_STREAM", "1")
+    st = eng.vocoder(mel, ln).cpu().numpy()
+    monkeypatch.setenv("TTS_UP_STREAM", "0")
+    cv = eng.vocoder(mel, ln).cpu().numpy()
+    tol = 2e-3 if dtype == "f16" else 1.5e-2
+    for b, L in enumerate(lens):
+        if L:
+            assert rel_rms(st[b, :L * 256], cv[b, :L * 256]) <= tol, b
+        assert np.all(st[b, L * 256:] == 0)
+    ref = vocoder_forward(mel[3, :17].cpu().numpy(), vw)
+    assert rel_rms(st[3, :17 * 256], ref) <= (5e-3 if dtype == "f16" else 2.5e-2)
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f16", "bf16"])
 def test_zero_length_utterance_in_batch(vw, dtype):
     """An empty utterance (0 frames) inside a ragged batch yields all-zero audio and leaves the

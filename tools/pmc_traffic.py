@@ -28,7 +28,7 @@ from collections import defaultdict
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tools.layer_breakdown import vocoder_layers  # noqa: E402
 
-FAMILIES = ("conv_gemm", "conv_xres", "mrf_fused", "mrf_pair", "mrf_chain", "conv_post")
+FAMILIES = ("conv_gemm", "conv_xres", "mrf_fused", "mrf_pair", "mrf_chain", "conv_post", "upsample_stream")
 
 
 def family(name):

@@ -580,7 +580,10 @@ static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err) {
   if (!xres_mode()) return false;
   const int wm = xres_wm(p);
   const int nt = xres_nt(p, wm);
-  const int cg = xres_group(p, 32 * nt * (4 / wm));  // channel group sized for the tile's rows
+  // channel group sized for 128-row tiles whatever the tile height: the group fixes the K
+  // order of the accumulation, so a row's result does not depend on the tiling (streamed
+  // chunks stay bit-identical to the full pass)
+  const int cg = xres_group(p, 32 * 4 * (4 / wm));
   if (!cg) return false;
   if (wm == 2)
     *err = launch_xres_wm<T, 2>(p, cg, s);

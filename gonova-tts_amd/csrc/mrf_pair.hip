@@ -65,13 +65,14 @@ static size_t pair_lds_bytes(int k, int d, bool post) {
 }
 
 template <typename T, int C, int K, bool POST = false>
-__global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPairParams p) {
+__global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom<C>::OCC)) void mrf_pair_kernel(
+    MrfPairParams p) {
   using G = PairGeom<C>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int BN = G::BN, WM = G::WM, WN = G::WN, RS = G::RS;
   constexpr int D = G::D;              // weight ring depth (k-steps)
   auto swz = [](int r) { return ((r * G::SW_MUL) >> G::SW_S) & G::SW_M; };  // chunk XOR of row r
-  constexpr int NTHR = 256;
+  constexpr int NTHR = 64 * WM * WN;    // 4 waves; 8 at C = 256 with 128-row tiles
   constexpr int KS = C / 32;           // k-steps (of 32 channels) per tap
   constexpr int MT = G::MT;            // 16-channel M tiles per wave
   constexpr int S = K * KS;            // k-steps per conv
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(256, (PairGeom<C>::OCC)) void mrf_pair_kernel(MrfPa
   constexpr int NU1 = (NT1 + WN - 1) / WN;  // conv1 tiles per wave (the last may be a repeat)
   constexpr int NT2 = BO / 16;         // conv2 tiles (block)
   constexpr int NU2 = (NT2 + WN - 1) / WN;  // conv2 tiles per wave (the last may be a repeat)
-  static_assert(!POST || (C == 32 && BN == 512), "conv_post fusion: C = 32, two samples per thread");
+  static_assert(!POST || (C == 32 && BN == 512 && NTHR == 256), "conv_post fusion: C = 32, two samples per thread");
   constexpr int VPR = C / 8;           // 16-byte pieces per row
   constexpr int YS16 = C * 2 + 16;     // output tile staging row stride
   static_assert(WM * WN * 64 == NTHR && WM * 16 * MT == C, "wave grid");
@@ -332,7 +333,7 @@ static hipError_t launch_pair_t(const MrfPairParams& p, hipStream_t s) {
   const size_t lds = pair_lds_bytes<C>(K, p.d, POST);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   dim3 grid(xcd_grid((p.T + G::BN - 1) / G::BN, p.B));
-  hipLaunchKernelGGL((mrf_pair_kernel<T, C, K, POST>), grid, dim3(256), lds, s, p);
+  hipLaunchKernelGGL((mrf_pair_kernel<T, C, K, POST>), grid, dim3(64 * G::WM * G::WN), lds, s, p);
   return hipGetLastError();
 }
 

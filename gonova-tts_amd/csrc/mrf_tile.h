@@ -49,9 +49,13 @@ struct PairGeom<128> {
 // conflict-free (the XOR never leaves a chunk's 256-byte half).  Weights streamed per row
 // equal conv_xres's 128-channel x 128-row blocks (both read 2*C*C*k / 64 B per output row
 // and conv), but t never leaves the block.
+#ifndef TTS_P256_WN
+#define TTS_P256_WN 1  // 2: 8-wave blocks of 128 rows (half the weight stream per row, one block per CU)
+#endif
 template <>
 struct PairGeom<256> {
-  static constexpr int BN = 64, WM = 4, WN = 1, RS = 512, SW_MUL = 2, SW_S = 0, SW_M = 15, D = TTS_P256_D, MT = 4, OCC = 2;
+  static constexpr int BN = 64 * TTS_P256_WN, WM = 4, WN = TTS_P256_WN, RS = 512, SW_MUL = 2, SW_S = 0, SW_M = 15,
+                       D = TTS_P256_D, MT = 4, OCC = TTS_P256_WN == 1 ? 2 : 1;
 };
 
 template <typename T>

@@ -271,6 +271,9 @@ constexpr int XRES_HR = 64;            // output rows per N-wave staged per half
 #ifndef TTS_XRES_STORE
 #define TTS_XRES_STORE 2               // output store cache policy (store16 in common.h)
 #endif
+#ifndef TTS_XRES_EPI16
+#define TTS_XRES_EPI16 1               // epilogue staged in the compute dtype (0: fp32 staging in two halves)
+#endif
 #ifndef TTS_XRES_OCC
 #define TTS_XRES_OCC 3                 // blocks per CU (register budget; LDS tile cap below)
 #endif
@@ -441,19 +444,84 @@ __global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams
   const T* R1 = p.r1 ? reinterpret_cast<const T*>(p.r1) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const T* R2 = p.r2 ? reinterpret_cast<const T*>(p.r2) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const int tlen = p.up_len ? min(p.up_len[b], (p.y_rows - 1) * p.up_s) : 0;
-  // staged half h holds rows wn*32*NT + 64h + [0, 64) of every N-wave, compacted to
-  // staged row wn*64 + r; the row pass maps staged row sr back to its output row
   const int cl = tid % PPR;                   // 8-channel piece of the block's BM channels
   const int m8 = blockIdx.y * BM + cl * 8;
-  auto out_row = [&](int half, int sr) { return n0 + (sr >> 6) * (32 * NT) + half * XRES_HR + (sr & 63); };
   const bool mok = m8 < p.M;
+  int q = 0, col = m8;
+  if (p.up_s) { q = m8 / p.up_cout; col = m8 - q * p.up_cout; }
+#if TTS_XRES_EPI16
+  // Bias, alpha and activation applied on the fragments, rounded to T once and staged in LDS
+  // as T (half the bytes of fp32; the whole tile in one round: one barrier pair).  The row
+  // pass moves 16-byte pieces out; launches with residuals / an output scale add them in
+  // fp32 there and round again (the pair kernels' epilogue order).
+  constexpr int OS16 = BM * 2 + 16;           // staged row stride (bytes)
+  constexpr int NIT = BN * PPR / NTHR;        // row pieces per thread
+  static_assert(BN * PPR % NTHR == 0 && NTHR % PPR == 0, "row pass");
+  uint4 res1[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int rl = tid / PPR + it * (NTHR / PPR);
+    int row = min(n0 + rl, ylen - 1);
+    if (p.up_s) row = min(max(row * p.up_s + q - p.up_p, 0), max(tlen - 1, 0));
+    if (R1) res1[it] = *reinterpret_cast<const uint4*>(R1 + (long long)row * p.srr + (mok ? col : 0));
+  }
+  f32x4 bl[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int m = blockIdx.y * BM + wm * 32 + 8 * g + 4 * hh;
+    bl[g] = (p.bias && m < p.M) ? *reinterpret_cast<const f32x4*>(p.bias + m) : f32x4{};
+  }
+  __syncthreads();  // X tile no longer read
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v = f32x4{acc[j][4 * g + 0], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]} + bl[g];
+      if (p.alpha != 1.0f) v *= p.alpha;
+      if (p.act_out) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = apply_act(v[i], p.act_out, p.out_slope);
+      }
+      const T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
+      *reinterpret_cast<uint2*>(smem + (wn * 32 * NT + j * 32 + l31) * OS16 + (wm * 32 + 8 * g + 4 * hh) * 2) =
+          *reinterpret_cast<const uint2*>(o);
+    }
+  __syncthreads();
+  const bool plain = !R1 && !R2 && p.out_scale == 1.0f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int rl = tid / PPR + it * (NTHR / PPR);
+    const int n = n0 + rl;
+    if (n >= ylen || !mok) continue;
+    int row = n;
+    if (p.up_s) {
+      row = n * p.up_s + q - p.up_p;
+      if (row < 0 || row >= tlen) continue;
+    }
+    uint4 y = *reinterpret_cast<const uint4*>(smem + rl * OS16 + cl * 16);
+    if (!plain) {
+      f32x4 v0, v1;
+      ld8<T>(reinterpret_cast<const T*>(&y), v0, v1);
+      if (R1) { f32x4 a, c; ld8<T>(reinterpret_cast<const T*>(&res1[it]), a, c); v0 += a; v1 += c; }
+      if (R2) { f32x4 a, c; ld8<T>(R2 + (long long)row * p.srr + col, a, c); v0 += a; v1 += c; }
+      if (p.out_scale != 1.0f) { v0 *= p.out_scale; v1 *= p.out_scale; }
+      const T e8[8] = {(T)v0[0], (T)v0[1], (T)v0[2], (T)v0[3], (T)v1[0], (T)v1[1], (T)v1[2], (T)v1[3]};
+      y = *reinterpret_cast<const uint4*>(e8);
+    }
+#if TTS_XRES_PROBE & 4  // timing-only: row pass without its global stores
+    if (y.x == 0x12345678u)
+#endif
+    store16<TTS_XRES_STORE>(Y, (int)(((long long)row * p.syr + col) * (long long)sizeof(T)), y);
+  }
+#else
+  // staged half h holds rows wn*32*NT + 64h + [0, 64) of every N-wave, compacted to
+  // staged row wn*64 + r; the row pass maps staged row sr back to its output row
+  auto out_row = [&](int half, int sr) { return n0 + (sr >> 6) * (32 * NT) + half * XRES_HR + (sr & 63); };
   f32x4 bias0 = {}, bias1 = {};
   if (p.bias && mok) {
     bias0 = *reinterpret_cast<const f32x4*>(p.bias + m8);
     bias1 = *reinterpret_cast<const f32x4*>(p.bias + m8 + 4);
   }
-  int q = 0, col = m8;
-  if (p.up_s) { q = m8 / p.up_cout; col = m8 - q * p.up_cout; }
   // every item's first-residual rows in flight before the staging barriers (the weight
   // ring is dead here, so these registers do not raise the kernel's peak; prefetching r2
   // as well would spill)
@@ -521,6 +589,7 @@ __global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams
       }
     }
   }
+#endif
 }
 
 constexpr int XRES_LDS_MAX = (160 / TTS_XRES_OCC - 1) * 1024;  // TTS_XRES_OCC blocks per CU (53 KB at 3)
@@ -569,7 +638,7 @@ template <typename T, int WM, int NT = 4>
 static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s) {
   constexpr int BM = 32 * WM, BN = 32 * NT * (4 / WM);
   const size_t lds = std::max((size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16),
-                              (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
+                              TTS_XRES_EPI16 ? (size_t)BN * (BM * 2 + 16) : (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
   dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
   hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM>), grid, dim3(256), lds, s, p, cg);
   return hipGetLastError();

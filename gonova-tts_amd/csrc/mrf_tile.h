@@ -19,13 +19,19 @@ struct PairGeom;
 // conflict-free for every tap offset (exhaustive check over r mod 16).
 // MT: 16-channel M tiles per wave (a wave owns 16*MT output channels); D: weight-ring depth
 // (k-steps); OCC: blocks per CU the register budget is sized for.
+#ifndef TTS_P32_D
+#define TTS_P32_D 4
+#endif
+#ifndef TTS_P64_D
+#define TTS_P64_D 4
+#endif
 template <>
 struct PairGeom<32> {
-  static constexpr int BN = 512, WM = 1, WN = 4, RS = 64, SW_MUL = 1, SW_S = 1, SW_M = 3, D = 4, MT = 2, OCC = 3;
+  static constexpr int BN = 512, WM = 1, WN = 4, RS = 64, SW_MUL = 1, SW_S = 1, SW_M = 3, D = TTS_P32_D, MT = 2, OCC = 3;
 };
 template <>
 struct PairGeom<64> {
-  static constexpr int BN = 256, WM = 2, WN = 2, RS = 128, SW_MUL = 1, SW_S = 0, SW_M = 7, D = 4, MT = 2, OCC = 3;
+  static constexpr int BN = 256, WM = 2, WN = 2, RS = 128, SW_MUL = 1, SW_S = 0, SW_M = 7, D = TTS_P64_D, MT = 2, OCC = 3;
 };
 #ifndef TTS_P128_WM
 #define TTS_P128_WM 4

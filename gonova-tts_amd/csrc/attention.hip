@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const T* __restrict__ 
                                                          const T* __restrict__ qkv, const T* __restrict__ vt,
                                                          const T* __restrict__ ptab, const int* __restrict__ lens,
                                                          int Tp, int D, int H, int Sk, int rmax, float scale,
-                                                         T* __restrict__ out) {
+                                                         T* __restrict__ out, int nqb, int nbatch) {
   using MF = Mfma16<T>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int KS = DK / 32;         // k-steps over dk
@@ -48,8 +48,12 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const T* __restrict__ 
   char* Rs = Vs + DK * VR;                          // [96 slots][DK]
   float* Gs = reinterpret_cast<float*>(Rs + AT_RW * KR);  // [4 waves][48 slots][16 q]
 
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int i0 = blockIdx.x * AT_BQ;
+  // 1-D grid, XCD-grouped: the query blocks of one (utterance, head) -- which all stream the
+  // same K / Vt / R rows -- run on one XCD, so those rows come from its L2 after the first
+  int bh, qb;
+  if (!xcd_tile(nqb, H * nbatch, bh, qb)) return;
+  const int b = bh / H, h = bh - b * H;
+  const int i0 = qb * AT_BQ;
   const int len = lens[b];
   if (i0 >= len) return;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -89,12 +93,15 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const T* __restrict__ 
       const int p = tid + 256 * i;
       const int r = p / (DK / 8), c = p - r * (DK / 8);
       const int j = j0 + r;
-      pkv[i] = j < len ? *reinterpret_cast<const uint4*>(qkv + ((long long)b * Tp + j) * 3 * rowD + D + h * DK + c * 8)
-                       : uint4{0u, 0u, 0u, 0u};
+      // addresses clamped into the buffers and the loads consumed unconditionally (a load under
+      // a branch or consumed only under a mask makes the waitcnt pass drain vmcnt); keys past
+      // len are masked out of the softmax, so their K / Vt only have to be finite
+      const uint4 kv = *reinterpret_cast<const uint4*>(qkv + ((long long)b * Tp + min(j, Tp - 1)) * 3 * rowD + D + h * DK + c * 8);
+      pkv[i] = j < len ? kv : uint4{0u, 0u, 0u, 0u};
       const int d = p / (AT_BK / 8), cv = p - d * (AT_BK / 8);
       const int jv = j0 + cv * 8;  // Vt is zero past len (transpose_v) and padded to Sk
-      pvt[i] = jv < Sk ? *reinterpret_cast<const uint4*>(vt + (((long long)b * H + h) * DK + d) * Sk + jv)
-                       : uint4{0u, 0u, 0u, 0u};
+      const uint4 vv = *reinterpret_cast<const uint4*>(vt + (((long long)b * H + h) * DK + d) * Sk + min(jv, Sk - 8));
+      pvt[i] = jv < Sk ? vv : uint4{0u, 0u, 0u, 0u};
       // R rows entering the window: m = i0 - j0 - 31 + [0, 32) (the first step loads all 96 below)
       const int m = i0 - j0 - (AT_BK - 1) + r;
       if (!first) prr[i] = *reinterpret_cast<const uint4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 8);
@@ -127,7 +134,7 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const T* __restrict__ 
 
   for (int j0 = 0; j0 < len; j0 += AT_BK) {
     const bool more = j0 + AT_BK < len;
-    if (more) stage_load(j0 + AT_BK, false);  // in flight during this step's MFMAs
+    stage_load(j0 + AT_BK, false);  // in flight during this step's MFMAs (the last step's is unused)
     const int mbw = i0w - j0 - (AT_BK - 1);  // m of this wave's G slot 0
     // S^T tiles (keys 16 kt + 4g + e, query q) and G^T tiles (slots 16 t + 4g + e)
     f32x4 sacc[2] = {f32x4{}, f32x4{}};
@@ -229,16 +236,17 @@ hipError_t launch_rel_attn(int dt, const void* qu, const void* qv, const void* q
                            const int* lens, int B, int Tm, int Tp, int D, int H, int Sk, int rmax, float scale,
                            void* out, hipStream_t s) {
   if (!rel_attn_supported(dt, D, H) || Tm > rmax || Sk % 8) return hipErrorInvalidValue;
-  dim3 grid((Tm + AT_BQ - 1) / AT_BQ, H, B);
+  const int nqb = (Tm + AT_BQ - 1) / AT_BQ;
+  dim3 grid(xcd_grid(nqb, H * B));
   const size_t lds = rel_attn_lds<192>();
   if (dt == DT_F16)
     hipLaunchKernelGGL((rel_attn_kernel<half_t, 192>), grid, dim3(256), lds, s, (const half_t*)qu, (const half_t*)qv,
                        (const half_t*)qkv, (const half_t*)vt, (const half_t*)ptab, lens, Tp, D, H, Sk, rmax, scale,
-                       (half_t*)out);
+                       (half_t*)out, nqb, B);
   else
     hipLaunchKernelGGL((rel_attn_kernel<bf16_t, 192>), grid, dim3(256), lds, s, (const bf16_t*)qu, (const bf16_t*)qv,
                        (const bf16_t*)qkv, (const bf16_t*)vt, (const bf16_t*)ptab, lens, Tp, D, H, Sk, rmax, scale,
-                       (bf16_t*)out);
+                       (bf16_t*)out, nqb, B);
   return hipGetLastError();
 }
 

@@ -457,19 +457,32 @@ __global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams
   constexpr int OS16 = BM * 2 + 16;           // staged row stride (bytes)
   constexpr int NIT = BN * PPR / NTHR;        // row pieces per thread
   static_assert(BN * PPR % NTHR == 0 && NTHR % PPR == 0, "row pass");
-  uint4 res1[NIT];
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int rl = tid / PPR + it * (NTHR / PPR);
-    int row = min(n0 + rl, ylen - 1);
-    if (p.up_s) row = min(max(row * p.up_s + q - p.up_p, 0), max(tlen - 1, 0));
-    if (R1) res1[it] = *reinterpret_cast<const uint4*>(R1 + (long long)row * p.srr + (mok ? col : 0));
-  }
+  // bias before the residual loads: vmcnt retires in order, so the staging's wait for the
+  // bias leaves the residual loads in flight
   f32x4 bl[4];
+  {  // channels past M or a null bias read 0 (descriptor range), no branch
+    const auto brsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.bias ? p.bias : reinterpret_cast<const float*>(Y)),
+                                                         0, p.bias ? p.M * 4 : 0, 0x00020000);
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int m = blockIdx.y * BM + wm * 32 + 8 * g + 4 * hh;
-    bl[g] = (p.bias && m < p.M) ? *reinterpret_cast<const f32x4*>(p.bias + m) : f32x4{};
+    for (int g = 0; g < 4; ++g)
+      bl[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            brsrc, (blockIdx.y * BM + wm * 32 + 8 * g + 4 * hh) * 4, 0, 0));
+  }
+  // first-residual rows in flight before the staging barriers, through a descriptor with no
+  // records when there is no residual: the loads are unconditional (a load under `if (R1)`
+  // made the waitcnt pass wait for each one right after issuing it) and fetch nothing then
+  uint4 res1[NIT];
+  {
+    const auto r1rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(R1 ? R1 : Y), 0, R1 ? 0x7fffffff : 0,
+                                                          0x00020000);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int rl = tid / PPR + it * (NTHR / PPR);
+      int row = min(n0 + rl, ylen - 1);
+      if (p.up_s) row = min(max(row * p.up_s + q - p.up_p, 0), max(tlen - 1, 0));
+      const int off = (int)(((long long)row * p.srr + (mok ? col : 0)) * (long long)sizeof(T));
+      res1[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r1rsrc, off, 0, 0));
+    }
   }
   __syncthreads();  // X tile no longer read
 #pragma unroll

@@ -224,10 +224,11 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
       const int rb = LO1 - A * DQ + l15;
       pair_conv<T, C, S, NU1, D>(acc1, ring, w1, GT + rb * RS, DQ * RS, DQ, tile, rb, lq);
       __builtin_amdgcn_sched_barrier(0);
-      preload(p.w2[Q]);  // conv2's first steps in flight during the epilogue
-      f32x4 bias[MT];
+      f32x4 bias[MT];  // bias before the weight preload: in-order vmcnt
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b1[Q] + ch0 + 16 * mt);
+      preload(p.w2[Q]);  // conv2's first steps in flight during the epilogue
+      __builtin_amdgcn_sched_barrier(0);
       __syncthreads();  // T overwrites G
 #pragma unroll
       for (int u = 0; u < NU1; ++u)
@@ -257,6 +258,9 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
       const int rb = LO2 - A + l15;
       pair_conv<T, C, S, NU2, D>(acc2, ring, w2, GT + rb * RS, RS, 1, tile, rb, lq);
       __builtin_amdgcn_sched_barrier(0);
+      f32x4 bias[MT];  // bias before the weight / MRF-sum prefetch: in-order vmcnt
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2[Q] + ch0 + 16 * mt);
       if constexpr (Q < 2) {
         preload(p.w1[Q + 1]);
       } else {  // MRF-sum rows in flight during the last epilogue (no records: not accumulating)
@@ -268,9 +272,7 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
           sin[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrsrc, e * (int)sizeof(T), 0, 0));
         }
       }
-      f32x4 bias[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2[Q] + ch0 + 16 * mt);
+      __builtin_amdgcn_sched_barrier(0);
       __syncthreads();  // T no longer read
 #pragma unroll
       for (int u = 0; u < NU2; ++u)

@@ -186,17 +186,20 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
     pair_conv<T, C, S, NU1, D, MT, (C >= TTS_PAIR_MTO_MIN)>(acc1, ring, w1, Gs + l15 * RS, d * RS, d, tile, l15, lq);
   }
   __builtin_amdgcn_sched_barrier(0);
-  // conv2's first weight steps in flight during the conv1 epilogue
+  // bias first, then conv2's first weight steps (in flight during the conv1 epilogue): vmcnt
+  // retires in order, so waiting for the bias does not wait for the weights
+  f32x4 bias1[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) bias1[mt] = *reinterpret_cast<const f32x4*>(p.b1 + ch0 + 16 * mt);
 #pragma unroll
   for (int i = 0; i < D; ++i)
     if (i < S)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) ring[i][mt] = *reinterpret_cast<const Frag*>(w2 + ((long long)mt * S + i) * 1024);
+  __builtin_amdgcn_sched_barrier(0);
   __syncthreads();  // T overwrites G: every wave is done reading it
   {
-    f32x4 bias[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b1 + ch0 + 16 * mt);
+    const f32x4 (&bias)[MT] = bias1;
 #pragma unroll
     for (int u = 0; u < NU1; ++u)
       if (NT1 % WN == 0 || wn + WN * u < NT1) {
@@ -247,10 +250,11 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
     }
   };
   // with conv_post fused the residual rows wait until the accumulators are staged (registers)
-  load_rows(!POST, true);
-  f32x4 bias[MT];
+  f32x4 bias[MT];  // before the row loads (in-order vmcnt: the staging waits for the bias only)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2 + ch0 + 16 * mt);
+  load_rows(!POST, true);
+  __builtin_amdgcn_sched_barrier(0);
   __syncthreads();  // T no longer read
 #pragma unroll
   for (int u = 0; u < NU2; ++u)

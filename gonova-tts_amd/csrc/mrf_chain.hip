@@ -121,7 +121,7 @@ __device__ inline uint2 epi_add4(uint2 y, uint2 h) {
 }
 template <typename T>
 __device__ inline uint2 lrelu4(uint2 v, float slope) {
-  const uint4 w = lrelu_chunk<T>(uint4{v.x, v.y, 0u, 0u}, slope);
+  const uint4 w = lrelu_unit<T>(uint4{v.x, v.y, 0u, 0u}, slope);
   return uint2{w.x, w.y};
 }
 
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
         const int gr = r0g + r;
         const bool in = gr >= 0 && gr < len;
         const uint4 h = in ? v[i] : uint4{0u, 0u, 0u, 0u};
-        const uint4 g = lrelu_chunk<T>(h, slope);  // consumed unconditionally (waitcnt)
+        const uint4 g = lrelu_unit<T>(h, slope);  // consumed unconditionally (waitcnt)
         if (r < NR) {
           const int o = r * RS + ((cc ^ swz(r)) << 4);
           *reinterpret_cast<uint4*>(Hs + o) = h;
@@ -333,6 +333,7 @@ bool mrf_chain_supported(int dtype, int C, int k, const int* dil, int npair) {
 }
 
 hipError_t mrf_chain_launch(int dtype, int C, int k, const MrfChainParams& p, hipStream_t s) {
+  if (!(p.slope >= 0.f && p.slope <= 1.f)) return hipErrorInvalidValue;  // lrelu_unit / epi_conv1
   const bool f16 = dtype == DT_F16;
   if (C == 32 && k == 3) return f16 ? launch_chain_t<half_t, 32, 3>(p, s) : launch_chain_t<bf16_t, 32, 3>(p, s);
   if (C == 32 && k == 7) return f16 ? launch_chain_t<half_t, 32, 7>(p, s) : launch_chain_t<bf16_t, 32, 7>(p, s);

@@ -147,7 +147,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
 #pragma unroll
         for (int i = 0; i < PAIR_SU; ++i) {
           const int r = rb + i * rstep;
-          const uint4 g = lrelu_chunk<T>(v[i], slope);  // consumed unconditionally (waitcnt)
+          const uint4 g = lrelu_unit<T>(v[i], slope);  // consumed unconditionally (waitcnt)
           if (r < RG) *reinterpret_cast<uint4*>(Gs + r * RS + (cc ^ swz(r)) * 16) = g;
         }
       }
@@ -163,7 +163,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
       for (int i = 0; i < PAIR_SU; ++i) {
         const int r = rb + i * rstep;
         const int gr = gs + r;
-        const uint4 g = lrelu_chunk<T>(v[i], slope);
+        const uint4 g = lrelu_unit<T>(v[i], slope);
         if (r < RG)
           *reinterpret_cast<uint4*>(Gs + r * RS + (cc ^ swz(r)) * 16) = (gr >= 0 && gr < len) ? g : uint4{0u, 0u, 0u, 0u};
       }
@@ -277,7 +277,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
       const int o = min(idx / VPR, BO - 1), c8 = idx % VPR;
       const int gr = n0 - PO + o;
       const uint4 y = *reinterpret_cast<const uint4*>(smem + o * YS16 + c8 * 16);
-      const uint4 v = lrelu_chunk<T>(epi_row<T>(y, xin[it], p.accum, sin[it], p.scale), p.post_slope);
+      const uint4 v = lrelu_unit<T>(epi_row<T>(y, xin[it], p.accum, sin[it], p.scale), p.post_slope);
       gv[it] = (gr >= 0 && gr < len) ? v : uint4{0u, 0u, 0u, 0u};
     }
     __syncthreads();  // output staging no longer read
@@ -366,6 +366,8 @@ bool mrf_pair_post_supported(int dtype, int C, int post_k) {
 
 hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s) {
   if (!mrf_pair_supported(dtype, C, p.k) || p.d < 1) return hipErrorInvalidValue;
+  if (!(p.slope >= 0.f && p.slope <= 1.f)) return hipErrorInvalidValue;  // lrelu_unit / epi_conv1
+  if (p.post_wpk && !(p.post_slope >= 0.f && p.post_slope <= 1.f)) return hipErrorInvalidValue;
   if (p.post_wpk) {
     if (!mrf_pair_post_supported(dtype, C, p.post_k) || !p.wav) return hipErrorInvalidValue;
     return dtype == DT_F16 ? launch_pair_k<half_t, 32, true>(p, s) : launch_pair_k<bf16_t, 32, true>(p, s);

@@ -55,7 +55,7 @@ __device__ inline uint4 up_lrelu(uint4 u, float slope) {
     v = __builtin_elementwise_max(v, v * (_Float16)slope);
     return *reinterpret_cast<uint4*>(&v);
   } else {
-    return lrelu_chunk<T>(u, slope);
+    return lrelu_unit<T>(u, slope);
   }
 }
 

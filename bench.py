@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--dtype", default="f16")
     ap.add_argument("--workload", default="vocoder", choices=["vocoder", "full", "c4"])
     ap.add_argument("--c4-batch", type=int, default=256)
+    ap.add_argument("--c4-bucket", type=int, default=64, help="utterances per length bucket (one synthesis call; 64 measured best of 32/64/128)")
     ap.add_argument("--no-streaming", action="store_true", help="skip the C5 streaming latency side measurement")
     ap.add_argument("--no-full", action="store_true", help="skip the full-pipeline side measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -240,7 +241,7 @@ def bench_c4(ctx, args):
     from gonova_tts_amd.model import GonovaTTS
     B = args.c4_batch
     m = GonovaTTS.from_pretrained(ctx.dev.index, vocoder_dtype="bf16", acoustic_dtype="bf16",
-                                  max_batch=32, max_frames=864, max_tokens=144)
+                                  max_batch=args.c4_bucket, max_frames=864, max_tokens=144)
     rng = np.random.default_rng(7)
     lens = rng.integers(29, 145, size=B).astype(np.int32)
     tok = np.zeros((B, 144), np.int32)
@@ -251,7 +252,7 @@ def bench_c4(ctx, args):
         d = np.where(np.arange(t.shape[1])[None, :] < l[:, None], 6, 0).astype(np.int32)
         return m.synthesize_tokens(t, l, durations=d)
 
-    sh = ShardedSynthesis(synth, ctx.dev, bucket=32)
+    sh = ShardedSynthesis(synth, ctx.dev, bucket=args.c4_bucket)
     run = lambda: sh.run(tok if ctx.rank == 0 else None, lens if ctx.rank == 0 else None)  # noqa: E731
     el, _ = ctx.timed(run, args.steps, args.warmup)
     samples = int(lens.sum()) * 6 * 256 * args.steps

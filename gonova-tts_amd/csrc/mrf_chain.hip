@@ -120,9 +120,21 @@ __device__ inline uint2 epi_add4(uint2 y, uint2 h) {
   }
 }
 template <typename T>
-__device__ inline uint2 lrelu4(uint2 v, float slope) {
-  const uint4 w = lrelu_unit<T>(uint4{v.x, v.y, 0u, 0u}, slope);
-  return uint2{w.x, w.y};
+__device__ inline uint2 lrelu4(uint2 v, float slope) {  // 4 x T, 0 <= slope <= 1 (lrelu_unit on 4 lanes)
+  if constexpr (__is_same(T, half_t)) {
+    half4 h = *reinterpret_cast<const half4*>(&v);
+    h = __builtin_elementwise_max(h, h * (half_t)slope);
+    return *reinterpret_cast<const uint2*>(&h);
+  } else {
+    const T* e = reinterpret_cast<const T*>(&v);
+    T o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = (float)e[i];
+      o[i] = (T)__builtin_fmaxf(x, x * slope);
+    }
+    return *reinterpret_cast<const uint2*>(o);
+  }
 }
 
 template <typename T, int C, int K>

@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
   using G = PairGeom<C>;
   using P = ChainPlan<C, K>;
   typedef typename Mfma<T>::frag Frag;
-  constexpr int BN = P::BN, WM = G::WM, WN = G::WN, RS = G::RS, D = G::D, A = P::A;
+  constexpr int BN = P::BN, WM = C / 32, WN = 4 / WM, RS = G::RS, D = G::D, A = P::A;  // 32 channels per wave
   constexpr int NTHR = 256, MT = 2, KS = C / 32, S = K * KS, VPR = C / 8;
   constexpr int H0 = P::H0, NR = P::NR, NRA = P::NRA;
   static_assert(WM * WN * 64 == NTHR && WM * 32 == C, "wave grid");

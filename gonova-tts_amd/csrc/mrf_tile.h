@@ -29,9 +29,16 @@ template <>
 struct PairGeom<32> {
   static constexpr int BN = 512, WM = 1, WN = 4, RS = 64, SW_MUL = 1, SW_S = 1, SW_M = 3, D = TTS_P32_D, MT = 2, OCC = 3;
 };
+#ifndef TTS_P64_OCC
+#define TTS_P64_OCC 3
+#endif
+#ifndef TTS_P64_WM
+#define TTS_P64_WM 2  // 1: 64-channel wave tiles (MT = 4, 4 waves along the rows)
+#endif
 template <>
 struct PairGeom<64> {
-  static constexpr int BN = 256, WM = 2, WN = 2, RS = 128, SW_MUL = 1, SW_S = 0, SW_M = 7, D = TTS_P64_D, MT = 2, OCC = 3;
+  static constexpr int BN = 256, WM = TTS_P64_WM, WN = 4 / TTS_P64_WM, RS = 128, SW_MUL = 1, SW_S = 0, SW_M = 7,
+                       D = TTS_P64_D, MT = 4 / TTS_P64_WM, OCC = TTS_P64_OCC;
 };
 #ifndef TTS_P128_WM
 #define TTS_P128_WM 4

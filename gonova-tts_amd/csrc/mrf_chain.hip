@@ -71,6 +71,14 @@ template <>
 struct ChainGeom<32, 3> { static constexpr int BN = TTS_CHAIN_BN32_3, OCC = TTS_CHAIN_OCC32_3; };
 template <>
 struct ChainGeom<32, 7> { static constexpr int BN = TTS_CHAIN_BN32_7, OCC = TTS_CHAIN_OCC32_7; };
+#ifndef TTS_CHAIN_C32K11
+#define TTS_CHAIN_C32K11 0         // chain the k = 11 resblock at C = 32 too
+#endif
+#ifndef TTS_CHAIN_BN32_11
+#define TTS_CHAIN_BN32_11 256
+#endif
+template <>
+struct ChainGeom<32, 11> { static constexpr int BN = TTS_CHAIN_BN32_11, OCC = 3; };
 template <>
 struct ChainGeom<64, 3> { static constexpr int BN = TTS_CHAIN_BN64_3, OCC = TTS_CHAIN_OCC64_3; };
 template <>
@@ -341,7 +349,8 @@ static hipError_t launch_chain_t(const MrfChainParams& p, hipStream_t s) {
 bool mrf_chain_supported(int dtype, int C, int k, const int* dil, int npair) {
   if (!(dtype == DT_F16 || dtype == DT_BF16) || npair != 3) return false;
   if (dil[0] != CHAIN_D0 || dil[1] != CHAIN_D1 || dil[2] != CHAIN_D2) return false;
-  return (C == 32 && (k == 3 || k == 7)) || (C == 64 && (k == 3 || (TTS_CHAIN_C64K7 && k == 7)));
+  return (C == 32 && (k == 3 || k == 7 || (TTS_CHAIN_C32K11 && k == 11))) ||
+         (C == 64 && (k == 3 || (TTS_CHAIN_C64K7 && k == 7)));
 }
 
 hipError_t mrf_chain_launch(int dtype, int C, int k, const MrfChainParams& p, hipStream_t s) {
@@ -349,6 +358,9 @@ hipError_t mrf_chain_launch(int dtype, int C, int k, const MrfChainParams& p, hi
   const bool f16 = dtype == DT_F16;
   if (C == 32 && k == 3) return f16 ? launch_chain_t<half_t, 32, 3>(p, s) : launch_chain_t<bf16_t, 32, 3>(p, s);
   if (C == 32 && k == 7) return f16 ? launch_chain_t<half_t, 32, 7>(p, s) : launch_chain_t<bf16_t, 32, 7>(p, s);
+#if TTS_CHAIN_C32K11
+  if (C == 32 && k == 11) return f16 ? launch_chain_t<half_t, 32, 11>(p, s) : launch_chain_t<bf16_t, 32, 11>(p, s);
+#endif
   if (C == 64 && k == 3) return f16 ? launch_chain_t<half_t, 64, 3>(p, s) : launch_chain_t<bf16_t, 64, 3>(p, s);
 #if TTS_CHAIN_C64K7
   if (C == 64 && k == 7) return f16 ? launch_chain_t<half_t, 64, 7>(p, s) : launch_chain_t<bf16_t, 64, 7>(p, s);

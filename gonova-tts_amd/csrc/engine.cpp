@@ -438,14 +438,41 @@ struct tts_engine {
                  0, 0, 1.f, B, Lp(i + 1), dt, s);
       }
       const int nk = (int)v.mrf[i].size();
-      bool pair_ok = mrf_fused_enabled() && mrf_pair_enabled();
-      for (int j = 0; j < nk && pair_ok; ++j)
-        for (const auto& pr : v.mrf[i][j]) pair_ok = pair_ok && pr[0].wpk16 && pr[1].wpk16;
+      // resblock j as single convs: lrelu(h) -> T1 -> conv2 + h (the last one accumulates into S)
+      auto convs_resblock = [&](int j) {
+        const auto& blk = v.mrf[i][j];
+        const int np = (int)blk.size();
+        const void* h = XS;
+        for (int q = 0; q < np; ++q) {
+          run_conv(blk[q][0], h, sb, ch, Lp(i + 1), Tout, T1, sb, ch, Lp(i + 1), Tout, slope, nullptr, nullptr,
+                   0, 0, 1.f, B, nullptr, dt, s);
+          const bool last = q == np - 1;
+          void* out = last ? S : (q % 2 == 0 ? HA : HB);
+          const void* r2 = (last && j > 0) ? S : nullptr;
+          const float sc = (last && j == nk - 1) ? 1.0f / (float)nk : 1.f;
+          run_conv(blk[q][1], T1, sb, ch, Lp(i + 1), Tout, out, sb, ch, Lp(i + 1), Tout, slope, h, r2, sb, ch,
+                   sc, B, nullptr, dt, s);
+          h = out;
+        }
+      };
+      auto pair_capable = [&](int j) {
+        bool ok = true;
+        for (const auto& pr : v.mrf[i][j]) ok = ok && pr[0].wpk16 && pr[1].wpk16;
+        return ok;
+      };
+      bool pair_ok = false;
+      if (mrf_fused_enabled() && mrf_pair_enabled())
+        for (int j = 0; j < nk; ++j) pair_ok = pair_ok || pair_capable(j);
       if (pair_ok) {
-        // 9 pair launches: X -> HA -> HB -> S per resblock; S accumulates over resblocks
+        // 9 pair launches: X -> HA -> HB -> S per resblock; S accumulates over resblocks.  A resblock
+        // without a pair kernel (its k) runs as single convs in the same S order.
         for (int j = 0; j < nk; ++j) {
           const auto& blk = v.mrf[i][j];
           const int np = (int)blk.size();
+          if (!pair_capable(j)) {
+            convs_resblock(j);
+            continue;
+          }
           int dil[4] = {0, 0, 0, 0};
           for (int q = 0; q < np && q < 4; ++q) dil[q] = blk[q][0].dil;
           if (mrf_chain_enabled() && mrf_chain_supported(dt, ch, blk[0][0].taps, dil, np)) {
@@ -527,24 +554,7 @@ struct tts_engine {
         cin = ch;
         continue;
       }
-      for (int j = 0; j < nk; ++j) {
-        const auto& blk = v.mrf[i][j];
-        const int np = (int)blk.size();
-        const void* h = XS;
-        for (int q = 0; q < np; ++q) {
-          // conv1: lrelu(h) -> T1
-          run_conv(blk[q][0], h, sb, ch, Lp(i + 1), Tout, T1, sb, ch, Lp(i + 1), Tout, slope, nullptr, nullptr,
-                   0, 0, 1.f, B, nullptr, dt, s);
-          // conv2: lrelu(T1) -> + h ; last pair accumulates into S (sum over blocks, /nk at the end)
-          const bool last = q == np - 1;
-          void* out = last ? S : (q % 2 == 0 ? HA : HB);
-          const void* r2 = (last && j > 0) ? S : nullptr;
-          const float sc = (last && j == nk - 1) ? 1.0f / (float)nk : 1.f;
-          run_conv(blk[q][1], T1, sb, ch, Lp(i + 1), Tout, out, sb, ch, Lp(i + 1), Tout, slope, h, r2, sb, ch,
-                   sc, B, nullptr, dt, s);
-          h = out;
-        }
-      }
+      for (int j = 0; j < nk; ++j) convs_resblock(j);
       Tin = Tout;
       cin = ch;
     }

@@ -354,8 +354,12 @@ static hipError_t launch_pair_k(const MrfPairParams& p, hipStream_t s) {
 
 // kernel sizes with a compiled pair kernel: HiFi-GAN V1/V2 (3, 7, 11) and V3 (3, 5, 7);
 // other sizes run the per-conv path
+#ifndef TTS_PAIR_C256_KMAX
+#define TTS_PAIR_C256_KMAX 11  // C = 256 resblocks with a larger k run as single convs (A/B knob)
+#endif
 bool mrf_pair_supported(int dtype, int C, int k) {
-  return (dtype == DT_F16 || dtype == DT_BF16) && (C == 32 || C == 64 || C == 128 || (TTS_PAIR_C256 && C == 256)) &&
+  return (dtype == DT_F16 || dtype == DT_BF16) &&
+         (C == 32 || C == 64 || C == 128 || (TTS_PAIR_C256 && C == 256 && k <= TTS_PAIR_C256_KMAX)) &&
          (k == 3 || k == 5 || k == 7 || k == 11);
 }
 

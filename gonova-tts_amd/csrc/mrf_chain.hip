@@ -119,12 +119,8 @@ __device__ inline uint2 epi_add4(uint2 y, uint2 h) {
     const half4 v = *reinterpret_cast<const half4*>(&y) + *reinterpret_cast<const half4*>(&h);
     return *reinterpret_cast<const uint2*>(&v);
   } else {
-    const T* ye = reinterpret_cast<const T*>(&y);
-    const T* he = reinterpret_cast<const T*>(&h);
-    T o[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (T)((float)ye[e] + (float)he[e]);
-    return *reinterpret_cast<const uint2*>(o);
+    return uint2{bf16x2_pack(bf16x2_unpack(y.x) + bf16x2_unpack(h.x)),
+                 bf16x2_pack(bf16x2_unpack(y.y) + bf16x2_unpack(h.y))};
   }
 }
 template <typename T>
@@ -134,14 +130,7 @@ __device__ inline uint2 lrelu4(uint2 v, float slope) {  // 4 x T, 0 <= slope <= 
     h = __builtin_elementwise_max(h, h * (half_t)slope);
     return *reinterpret_cast<const uint2*>(&h);
   } else {
-    const T* e = reinterpret_cast<const T*>(&v);
-    T o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float x = (float)e[i];
-      o[i] = (T)__builtin_fmaxf(x, x * slope);
-    }
-    return *reinterpret_cast<const uint2*>(o);
+    return uint2{lrelu_bf16x2(v.x, slope), lrelu_bf16x2(v.y, slope)};
   }
 }
 

@@ -129,6 +129,12 @@ __device__ inline void pair_ld8(const T* p, f32x4& a, f32x4& b) {
   a = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
   b = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
 }
+// 4 x f32 -> 4 x T (16-bit T): two v_cvt_pk_{f16,bf16}_f32
+template <typename T>
+__device__ inline uint2 pack4(f32x4 v) {
+  typedef T t4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(uint2, __builtin_convertvector(v, t4));
+}
 // Epilogue arithmetic.  f16: packed half math after one cvt_pk per pair of accumulators
 // (v_pk_add/mul/max_f16: a fraction of the f32 instruction count; a sum of two f16 values
 // is correctly rounded either way, the bias/slope products differ by <= 1 ulp).  bf16:
@@ -143,8 +149,7 @@ __device__ inline uint2 epi_conv1(f32x4 acc, f32x4 bias, float slope) {  // lrel
     f32x4 v = acc + bias;
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaxf(v[e], v[e] * slope);  // 0 <= slope <= 1
-    T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
-    return *reinterpret_cast<const uint2*>(o);
+    return pack4<T>(v);
   }
 }
 template <typename T>
@@ -153,9 +158,7 @@ __device__ inline uint2 epi_conv2(f32x4 acc, f32x4 bias) {  // acc + b -> 4 x T
     half4 h = __builtin_convertvector(acc, half4) + __builtin_convertvector(bias, half4);
     return *reinterpret_cast<const uint2*>(&h);
   } else {
-    const f32x4 v = acc + bias;
-    T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
-    return *reinterpret_cast<const uint2*>(o);
+    return pack4<T>(acc + bias);
   }
 }
 // row pass: (y + h (+ s)) * scale on 8 elements
@@ -166,6 +169,18 @@ __device__ inline uint4 epi_row(uint4 y, uint4 h, bool acc, uint4 s, float scale
     if (acc) v += *reinterpret_cast<const half8*>(&s);
     if (scale != 1.0f) v *= (half_t)scale;
     return *reinterpret_cast<const uint4*>(&v);
+  } else if constexpr (__is_same(T, bf16_t)) {
+    const unsigned* yw = reinterpret_cast<const unsigned*>(&y);
+    const unsigned* hw = reinterpret_cast<const unsigned*>(&h);
+    const unsigned* sw = reinterpret_cast<const unsigned*>(&s);
+    unsigned o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f32x2 v = bf16x2_unpack(yw[i]) + bf16x2_unpack(hw[i]);
+      if (acc) v += bf16x2_unpack(sw[i]);
+      o[i] = bf16x2_pack(v * scale);
+    }
+    return uint4{o[0], o[1], o[2], o[3]};
   } else {
     const T* ye = reinterpret_cast<const T*>(&y);
     const T* he = reinterpret_cast<const T*>(&h);
@@ -182,14 +197,9 @@ __device__ inline uint4 epi_row(uint4 y, uint4 h, bool acc, uint4 s, float scale
 }
 
 template <typename T>
-__device__ inline uint2 pack4(f32x4 v) {
-  T e[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
-  return *reinterpret_cast<const uint2*>(e);
-}
-template <typename T>
 __device__ inline void pair_st8(T* p, f32x4 a, f32x4 b) {
-  T e[8] = {(T)a[0], (T)a[1], (T)a[2], (T)a[3], (T)b[0], (T)b[1], (T)b[2], (T)b[3]};
-  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(e);
+  const uint2 lo = pack4<T>(a), hi = pack4<T>(b);
+  *reinterpret_cast<uint4*>(p) = uint4{lo.x, lo.y, hi.x, hi.y};
 }
 
 // One conv of the pair over NU 16-row tiles per wave: acc[u][mt] += W[mt] x tile u.

@@ -47,6 +47,11 @@ def summarize(path):
     print(f"one forward: {n} launches, kernel time {busy:.1f} us, span {span:.1f} us")
     for k, (us, c) in sorted(tot.items(), key=lambda kv: -kv[1][0]):
         print(f"{us:9.1f} us {c:4d}x  {k}")
+    if os.environ.get("ACOUSTIC_PROF_LAUNCHES"):
+        for r in last:
+            us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            print(f"{us:8.1f} us grid {r.get('Grid_Size', '?'):>9} wg {r.get('Workgroup_Size', '?'):>4} "
+                  f"lds {r.get('LDS_Block_Size', r.get('Lds_Size', '?')):>6}  {r['Kernel_Name'][:90]}")
 
 
 if __name__ == "__main__":

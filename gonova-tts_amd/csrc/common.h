@@ -123,6 +123,19 @@ __device__ inline unsigned lrelu_bf16x2(unsigned w, float slope) {
   return r;
 }
 
+// 4 / 8 x f32 -> 16-bit T: one v_cvt_pk_{f16,bf16}_f32 per pair
+template <typename T>
+__device__ inline uint2 pack4(f32x4 v) {
+  static_assert(sizeof(T) == 2, "16-bit dtypes only");
+  typedef T t4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(uint2, __builtin_convertvector(v, t4));
+}
+template <typename T>
+__device__ inline uint4 pack8(f32x4 a, f32x4 b) {
+  const uint2 lo = pack4<T>(a), hi = pack4<T>(b);
+  return uint4{lo.x, lo.y, hi.x, hi.y};
+}
+
 // LeakyReLU of one 16-byte chunk.  f16 with 0 <= slope <= 1 runs packed:
 // max(x, slope*x) as v_pk_mul_f16 + v_pk_max_f16 (8 instructions per chunk instead of ~40
 // unpacked converts/compares); slope is then rounded to f16 (0.1 -> 0.09998, within the

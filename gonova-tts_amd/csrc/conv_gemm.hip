@@ -289,18 +289,13 @@ __device__ inline void ld8(const T* p, f32x4& a, f32x4& b) {
   a = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
   b = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
 }
-template <typename T>
-__device__ inline void st8(T* p, f32x4 a, f32x4 b) {
-  T e[8] = {(T)a[0], (T)a[1], (T)a[2], (T)a[3], (T)b[0], (T)b[1], (T)b[2], (T)b[3]};
-  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(e);
-}
 
 template <typename T, int NT, int WM>
 __global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams p, int CG) {
   using MF = Mfma<T>;
   typedef typename MF::frag Frag;
   static_assert(sizeof(T) == 2, "16-bit dtypes only");
-  static_assert(NT % 2 == 0, "output staged in 64-row halves");
+  static_assert(NT % 2 == 0 || TTS_XRES_EPI16, "fp32 staging goes in 64-row halves");
   static_assert(WM == 4 || WM == 2, "4 waves: 4 x 1 or 2 x 2");
   constexpr int WN = 4 / WM;
   constexpr int BM = 32 * WM;          // output channels per block
@@ -495,9 +490,8 @@ __global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = apply_act(v[i], p.act_out, p.out_slope);
       }
-      const T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
       *reinterpret_cast<uint2*>(smem + (wn * 32 * NT + j * 32 + l31) * OS16 + (wm * 32 + 8 * g + 4 * hh) * 2) =
-          *reinterpret_cast<const uint2*>(o);
+          pack4<T>(v);
     }
   __syncthreads();
   const bool plain = !R1 && !R2 && p.out_scale == 1.0f;
@@ -518,8 +512,7 @@ __global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams
       if (R1) { f32x4 a, c; ld8<T>(reinterpret_cast<const T*>(&res1[it]), a, c); v0 += a; v1 += c; }
       if (R2) { f32x4 a, c; ld8<T>(R2 + (long long)row * p.srr + col, a, c); v0 += a; v1 += c; }
       if (p.out_scale != 1.0f) { v0 *= p.out_scale; v1 *= p.out_scale; }
-      const T e8[8] = {(T)v0[0], (T)v0[1], (T)v0[2], (T)v0[3], (T)v1[0], (T)v1[1], (T)v1[2], (T)v1[3]};
-      y = *reinterpret_cast<const uint4*>(e8);
+      y = pack8<T>(v0, v1);
     }
 #if TTS_XRES_PROBE & 4  // timing-only: row pass without its global stores
     if (y.x == 0x12345678u)
@@ -589,15 +582,15 @@ __global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams
       if (v0[0] == 1234.5f)
 #endif
       {
-        T e8[8] = {(T)v0[0], (T)v0[1], (T)v0[2], (T)v0[3], (T)v1[0], (T)v1[1], (T)v1[2], (T)v1[3]};
+        const uint4 e8 = pack8<T>(v0, v1);
 #if TTS_XRES_PROBE & 8  // timing-only: every block stores into the same 32 KB (L2-resident, no HBM writes)
-        store16<TTS_XRES_STORE>(Y, (int)((((rl & 127) * 16 + cl) * 16) & 0x7fff), *reinterpret_cast<const uint4*>(e8));
+        store16<TTS_XRES_STORE>(Y, (int)((((rl & 127) * 16 + cl) * 16) & 0x7fff), e8);
 #elif TTS_XRES_PROBE & 16  // timing-only: each block writes its own contiguous 32 KB (same bytes, block-linear)
         store16<TTS_XRES_STORE>(Y, (int)((blockIdx.x * gridDim.y + blockIdx.y) * 32768 + (((half * 64 + (rl & 63)) * 16 + cl) * 16) % 32768),
-                                *reinterpret_cast<const uint4*>(e8));
+                                e8);
 #else
         store16<TTS_XRES_STORE>(Y, (int)(((long long)row * p.syr + col) * (long long)sizeof(T)),
-                                *reinterpret_cast<const uint4*>(e8));
+                                e8);
 #endif
       }
     }
@@ -632,6 +625,23 @@ static int xres_mode() {  // TTS_CONV_XRES=0 disables the X-resident kernel (A/B
 // 128-channel blocks (4 x 1 waves, BN = 128) for M >= 128; 64-channel blocks (2 x 2 waves,
 // BN = 256) for M = 64 (the last upsampler)
 static int xres_wm(const ConvParams& p) { return p.M >= 128 ? 4 : 2; }
+
+#ifndef TTS_XRES_NARROW_MAXBLK
+#define TTS_XRES_NARROW_MAXBLK 256     // 0 disables; 512 measured slower for C3 (encoder at batch 32)
+#endif
+// Narrow 64 x 64 tiles (2 x 2 waves, one 32 x 32 MFMA tile each) for launches whose 128-channel
+// grid would leave the chip under-filled: the small-batch acoustic passes (streaming: batch 8;
+// the encoder's 144-row utterances), where an M = 384 projection over K = 4608 made 54-168
+// blocks for 256 CUs.  Same channel group (K order) as the wide tiles, so a row's result does
+// not depend on the choice (bit-identical; tests/test_acoustic_gpu.py).  TTS_XRES_NARROW=0/1
+// forces it off / on where eligible (A/B runs and tests).
+static bool xres_narrow(const ConvParams& p, int nt) {
+  if (p.M % 64 || !TTS_XRES_EPI16) return false;
+  const char* e = getenv("TTS_XRES_NARROW");
+  if (e) return atoi(e) != 0;
+  const long long blocks = (long long)((p.y_rows + 32 * nt - 1) / (32 * nt)) * ((p.M + 127) / 128) * p.B * p.nh;
+  return blocks < TTS_XRES_NARROW_MAXBLK;
+}
 
 #ifndef TTS_XRES_SMALL_TILES
 #define TTS_XRES_SMALL_TILES 1
@@ -669,6 +679,8 @@ static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err) {
   if (!cg) return false;
   if (wm == 2)
     *err = launch_xres_wm<T, 2>(p, cg, s);
+  else if (xres_narrow(p, nt))
+    *err = launch_xres_wm<T, 2, 1>(p, cg, s);
   else
     *err = nt == 2 ? launch_xres_wm<T, 4, 2>(p, cg, s) : launch_xres_wm<T, 4>(p, cg, s);
   return true;

@@ -129,12 +129,6 @@ __device__ inline void pair_ld8(const T* p, f32x4& a, f32x4& b) {
   a = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
   b = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
 }
-// 4 x f32 -> 4 x T (16-bit T): two v_cvt_pk_{f16,bf16}_f32
-template <typename T>
-__device__ inline uint2 pack4(f32x4 v) {
-  typedef T t4 __attribute__((ext_vector_type(4)));
-  return __builtin_bit_cast(uint2, __builtin_convertvector(v, t4));
-}
 // Epilogue arithmetic.  f16: packed half math after one cvt_pk per pair of accumulators
 // (v_pk_add/mul/max_f16: a fraction of the f32 instruction count; a sum of two f16 values
 // is correctly rounded either way, the bias/slope products differ by <= 1 ulp).  bf16:
@@ -198,8 +192,7 @@ __device__ inline uint4 epi_row(uint4 y, uint4 h, bool acc, uint4 s, float scale
 
 template <typename T>
 __device__ inline void pair_st8(T* p, f32x4 a, f32x4 b) {
-  const uint2 lo = pack4<T>(a), hi = pack4<T>(b);
-  *reinterpret_cast<uint4*>(p) = uint4{lo.x, lo.y, hi.x, hi.y};
+  *reinterpret_cast<uint4*>(p) = pack8<T>(a, b);
 }
 
 // One conv of the pair over NU 16-row tiles per wave: acc[u][mt] += W[mt] x tile u.

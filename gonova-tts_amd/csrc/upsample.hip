@@ -147,9 +147,7 @@ __global__ __launch_bounds__((64 * UpGeom<CIN, M>::NW)) void upsample_stream_ker
       for (int mt = 0; mt < MT; ++mt)
       {  // fp32 bias add, one rounding (as conv_xres)
         const f32x4 v = acc[j][mt] + *reinterpret_cast<const f32x4*>(Bs + mt * 16 + 4 * lq);
-        const T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
-        *reinterpret_cast<uint2*>(Ys + (16 * j + l15) * YS + (mt * 16 + 4 * lq) * 2) =
-            *reinterpret_cast<const uint2*>(o);
+        *reinterpret_cast<uint2*>(Ys + (16 * j + l15) * YS + (mt * 16 + 4 * lq) * 2) = pack4<T>(v);
       }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the slice is written before it is read back

@@ -248,20 +248,27 @@ def test_short_row_tiles_bit_identical(aw, dtype, monkeypatch):
     last tile empty (the encoder's short token rows).  The channel group, and so the K order
     of the accumulation, is the same for both tile heights, so the mel matches the 128-row
     run bit for bit (ragged batch, lengths across 64-row edges, durations forced) -- the
-    property the chunked vocoder's bit-exactness rests on."""
+    property the chunked vocoder's bit-exactness rests on.  The narrow 64 x 64 tiles picked
+    for under-filled grids (this batch of 4 picks them everywhere eligible) keep the same K
+    order too: forced on, forced off and automatic all agree bit for bit."""
     eng = engine(dtype, aw)
     rng = np.random.default_rng(12)
     ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70)]
     durs = [np.full(len(x), 3) for x in ids_list]
+    monkeypatch.setenv("TTS_XRES_NARROW", "0")   # 128-channel tiles: the tile-height pair
     monkeypatch.setenv("TTS_XRES_NT", "4")
     big, lb, _ = run(eng, ids_list, t_cap=432, durations=durs)
     monkeypatch.setenv("TTS_XRES_NT", "2")
     small, ls, _ = run(eng, ids_list, t_cap=432, durations=durs)
     monkeypatch.delenv("TTS_XRES_NT")
+    monkeypatch.setenv("TTS_XRES_NARROW", "1")   # 64 x 64 tiles wherever eligible
+    narrow, ln, _ = run(eng, ids_list, t_cap=432, durations=durs)
+    monkeypatch.delenv("TTS_XRES_NARROW")
     auto, la, _ = run(eng, ids_list, t_cap=432, durations=durs)
     for b, ids in enumerate(ids_list):
         L = int(la[b])
-        assert int(lb[b]) == L == int(ls[b]) == len(ids) * 3
+        assert int(lb[b]) == L == int(ls[b]) == int(ln[b]) == len(ids) * 3
         assert np.array_equal(auto[b], big[b]) and np.array_equal(small[b], big[b]), b
+        assert np.array_equal(narrow[b], big[b]), b
         ref = acoustic_forward(ids, aw, durations=durs[b])
         assert rel_rms(auto[b, :L], ref["mel"]) <= 5e-2

@@ -19,7 +19,7 @@ def run():
     import torch
     from gonova_tts_amd.engine import HipEngine
     from gonova_tts_amd.weights import make_acoustic_weights
-    B, N, dur = 32, 144, 6
+    B, N, dur = int(os.environ.get("ACOUSTIC_PROF_B", "32")), 144, 6
     eng = HipEngine("cuda:0", acoustic_dtype="bf16", max_batch=B, max_frames=N * dur, max_tokens=N)
     eng.load_weights(acoustic=make_acoustic_weights(seed=0, fixed_duration=dur))
     g = torch.Generator(device="cpu").manual_seed(2000)

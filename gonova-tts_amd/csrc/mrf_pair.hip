@@ -30,6 +30,8 @@
 // K = taps x C.  Weights are fragment-packed on the host (frag_pack16, runtime.h) so each
 // wave's A fragment is one contiguous 1 KiB load, streamed through a 4-step register ring
 // (no barriers inside a conv).  Activation tiles are XOR-swizzled (PairGeom).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 #include "mrf_tile.h"
@@ -52,10 +54,20 @@ namespace tts {
 // rows per side so conv_post's halo (post_k <= 2*PAIR_PO + 1 taps) is in the block
 constexpr int PAIR_PO = 8;
 
+// Short-tile geometry: BN / DIV output rows per block, everything else as PairGeom<C>.  The
+// launcher picks DIV = 4 when the full-height grid would not give every CU a block (the
+// streamed vocoder's 48-64-frame windows at batch 8: 48-192 blocks for 256 CUs).  A row's
+// arithmetic (k-step order, roundings) does not depend on the tile height, so the output is
+// bit-identical to the full-height launch (tests/test_vocoder_gpu.py).
+template <int C, int DIV>
+struct PairGeomS : PairGeom<C> {
+  static constexpr int BN = PairGeom<C>::BN / DIV;
+};
+
 // LDS bytes of one launch (G tile incl. conv1 overrun rows, T tile; >= output staging tile)
-template <int C>
+template <int C, int DIV = 1>
 static size_t pair_lds_bytes(int k, int d, bool post) {
-  using G = PairGeom<C>;
+  using G = PairGeomS<C, DIV>;
   const int a1 = (k - 1) / 2 * d, a2 = (k - 1) / 2;
   const int bo = G::BN + (post ? 2 * PAIR_PO : 0);
   const int nt1 = (bo + 2 * a2 + 15) / 16;
@@ -64,10 +76,10 @@ static size_t pair_lds_bytes(int k, int d, bool post) {
   return std::max(std::max(g, t), (size_t)bo * (C * 2 + 16));
 }
 
-template <typename T, int C, int K, bool POST = false>
+template <typename T, int C, int K, bool POST = false, int DIV = 1>
 __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom<C>::OCC)) void mrf_pair_kernel(
     MrfPairParams p) {
-  using G = PairGeom<C>;
+  using G = PairGeomS<C, DIV>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int BN = G::BN, WM = G::WM, WN = G::WN, RS = G::RS;
   constexpr int D = G::D;              // weight ring depth (k-steps)
@@ -331,14 +343,33 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   }
 }
 
-template <typename T, int C, int K, bool POST = false>
-static hipError_t launch_pair_t(const MrfPairParams& p, hipStream_t s) {
-  using G = PairGeom<C>;
-  const size_t lds = pair_lds_bytes<C>(K, p.d, POST);
+#ifndef TTS_PAIR_SHORT
+#define TTS_PAIR_SHORT 1               // 0: always full-height tiles (A/B knob)
+#endif
+// 4 = quarter-height tiles for a grid that would leave CUs idle; TTS_PAIR_DIV=1/4 forces (tests)
+static int pair_div(int C, const MrfPairParams& p, bool post) {
+  if (post || !TTS_PAIR_SHORT) return 1;
+  const char* e = getenv("TTS_PAIR_DIV");
+  if (e) return atoi(e) == 4 ? 4 : 1;
+  const int bn = C == 32 ? PairGeom<32>::BN : C == 64 ? PairGeom<64>::BN : C == 128 ? PairGeom<128>::BN : PairGeom<256>::BN;
+  return (long long)((p.T + bn - 1) / bn) * p.B < 256 ? 4 : 1;
+}
+
+template <typename T, int C, int K, bool POST, int DIV>
+static hipError_t launch_pair_g(const MrfPairParams& p, hipStream_t s) {
+  using G = PairGeomS<C, DIV>;
+  const size_t lds = pair_lds_bytes<C, DIV>(K, p.d, POST);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   dim3 grid(xcd_grid((p.T + G::BN - 1) / G::BN, p.B));
-  hipLaunchKernelGGL((mrf_pair_kernel<T, C, K, POST>), grid, dim3(64 * G::WM * G::WN), lds, s, p);
+  hipLaunchKernelGGL((mrf_pair_kernel<T, C, K, POST, DIV>), grid, dim3(64 * G::WM * G::WN), lds, s, p);
   return hipGetLastError();
+}
+
+template <typename T, int C, int K, bool POST = false>
+static hipError_t launch_pair_t(const MrfPairParams& p, hipStream_t s) {
+  if constexpr (!POST)
+    if (pair_div(C, p, POST) == 4) return launch_pair_g<T, C, K, POST, 4>(p, s);
+  return launch_pair_g<T, C, K, POST, 1>(p, s);
 }
 
 template <typename T, int C, bool POST = false>

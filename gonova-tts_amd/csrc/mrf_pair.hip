@@ -55,8 +55,8 @@ namespace tts {
 constexpr int PAIR_PO = 8;
 
 // Short-tile geometry: BN / DIV output rows per block, everything else as PairGeom<C>.  The
-// launcher picks DIV = 4 when the full-height grid would not give every CU a block (the
-// streamed vocoder's 48-64-frame windows at batch 8: 48-192 blocks for 256 CUs).  A row's
+// launcher picks it when the full-height grid leaves most CUs idle (the streamed vocoder's
+// stage 0 at batch 8: 48 blocks for 256 CUs; see pair_div).  A row's
 // arithmetic (k-step order, roundings) does not depend on the tile height, so the output is
 // bit-identical to the full-height launch (tests/test_vocoder_gpu.py).
 template <int C, int DIV>
@@ -344,15 +344,22 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
 }
 
 #ifndef TTS_PAIR_SHORT
-#define TTS_PAIR_SHORT 1               // 0: always full-height tiles (A/B knob)
+#define TTS_PAIR_SHORT 128             // short tiles below this many full-height blocks (0: never)
 #endif
-// 4 = quarter-height tiles for a grid that would leave CUs idle; TTS_PAIR_DIV=1/4 forces (tests)
+#ifndef TTS_PAIR_SHORT_DIV
+#define TTS_PAIR_SHORT_DIV 4           // tile height divisor of the short tiles
+#endif
+// Short tiles multiply the L2 weight stream (every block reads the pair's 2*k*C*C weights), so
+// they pay only where the full-height grid leaves most CUs idle.  Measured on the C5 windows
+// (batch 8, 48 frames, tools/c5_probe.py under rocprofv3): C = 256 at 48 blocks 380 -> 329 us
+// for the stage's 9 launches; C = 128 at 192 blocks 167 -> 193 us (slower), C = 32 / 64 neutral.
+// TTS_PAIR_DIV=1 / any other value forces full-height / short tiles (tests).
 static int pair_div(int C, const MrfPairParams& p, bool post) {
-  if (post || !TTS_PAIR_SHORT) return 1;
+  if (post) return 1;
   const char* e = getenv("TTS_PAIR_DIV");
-  if (e) return atoi(e) == 4 ? 4 : 1;
+  if (e) return atoi(e) == 1 ? 1 : TTS_PAIR_SHORT_DIV;
   const int bn = C == 32 ? PairGeom<32>::BN : C == 64 ? PairGeom<64>::BN : C == 128 ? PairGeom<128>::BN : PairGeom<256>::BN;
-  return (long long)((p.T + bn - 1) / bn) * p.B < 256 ? 4 : 1;
+  return (long long)((p.T + bn - 1) / bn) * p.B < TTS_PAIR_SHORT ? TTS_PAIR_SHORT_DIV : 1;
 }
 
 template <typename T, int C, int K, bool POST, int DIV>
@@ -368,7 +375,7 @@ static hipError_t launch_pair_g(const MrfPairParams& p, hipStream_t s) {
 template <typename T, int C, int K, bool POST = false>
 static hipError_t launch_pair_t(const MrfPairParams& p, hipStream_t s) {
   if constexpr (!POST)
-    if (pair_div(C, p, POST) == 4) return launch_pair_g<T, C, K, POST, 4>(p, s);
+    if (pair_div(C, p, POST) != 1) return launch_pair_g<T, C, K, POST, TTS_PAIR_SHORT_DIV>(p, s);
   return launch_pair_g<T, C, K, POST, 1>(p, s);
 }
 

@@ -250,7 +250,7 @@ def bench_c4(ctx, args):
 
     def synth(t, l):
         d = np.where(np.arange(t.shape[1])[None, :] < l[:, None], 6, 0).astype(np.int32)
-        return m.synthesize_tokens(t, l, durations=d)
+        return m.synthesize_tokens(t, l, durations=d, host_lens=False)
 
     sh = ShardedSynthesis(synth, ctx.dev, bucket=args.c4_bucket)
     run = lambda: sh.run(tok if ctx.rank == 0 else None, lens if ctx.rank == 0 else None)  # noqa: E731

@@ -60,7 +60,10 @@ class ShardedSynthesis:
     """Run one batch of utterances across all ranks of a process group, results on `root`.
 
     synth_fn(tokens int32 [b, N], lens int32 [b]) -> (wav tensor [b, S] float32, wav_lens int64 [b])
-    runs on the calling rank's device (a GonovaTTS.synthesize_tokens, or a fake on CPU).
+    runs on the calling rank's device (a GonovaTTS.synthesize_tokens, or a fake on CPU).  wav_lens
+    may be a numpy array or a device tensor; with device tensors (synthesize_tokens(...,
+    host_lens=False)) every bucket is queued before the first host sync.  On the root the
+    waveforms come back as views into one host buffer per rank (one pinned D2H copy each).
     """
 
     def __init__(self, synth_fn: SynthFn, device, group=None, root: int = 0, bucket: int = 32):
@@ -104,9 +107,13 @@ class ShardedSynthesis:
         mine = plan[self.rank]
         # ---- 4: local synthesis, packed as [index, length] table + flat samples ----
         idx_list, len_list, parts = [], [], []
-        for bk in mine:
+        done = []
+        for bk in mine:  # queue every bucket first: no host sync between them
             n_b = int(ln_h[bk].max())
-            wav, wav_lens = self.synth_fn(tok_h[bk, :n_b], ln_h[bk])
+            done.append((bk,) + tuple(self.synth_fn(tok_h[bk, :n_b], ln_h[bk])))
+        for bk, wav, wav_lens in done:
+            if isinstance(wav_lens, torch.Tensor):
+                wav_lens = wav_lens.cpu().numpy()
             for j, u in enumerate(bk):
                 L = int(wav_lens[j])
                 idx_list.append(u)
@@ -143,11 +150,14 @@ class ShardedSynthesis:
         out: List[Optional[np.ndarray]] = [None] * B
         for r in range(self.world):
             t = tables[r].cpu().numpy()
-            f = flats[r].cpu().numpy()
+            f = flats[r]
+            if f.is_cuda:  # one D2H copy through a pinned (cached) host buffer
+                f = torch.empty(f.shape, dtype=f.dtype, pin_memory=True).copy_(f)
+            f = f.numpy()
             n = int(t[0])
             ids, ls = t[1:1 + n], t[1 + n:1 + 2 * n]
             off = 0
             for u, L in zip(ids, ls):
-                out[int(u)] = f[off:off + int(L)].copy()
+                out[int(u)] = f[off:off + int(L)]
                 off += int(L)
         return out

@@ -116,8 +116,10 @@ class GonovaTTS:
 
     # -------------------------------------------------------------- synthesis
     def synthesize_tokens(self, tokens: np.ndarray, lens: np.ndarray, durations: Optional[np.ndarray] = None,
-                          stream=None, speaker_embedding: Optional[np.ndarray] = None):
-        """tokens int32 [B, N], lens [B] -> (wav cuda float32 [B, T*256], wav_lens np.int64 [B])."""
+                          stream=None, speaker_embedding: Optional[np.ndarray] = None, host_lens: bool = True):
+        """tokens int32 [B, N], lens [B] -> (wav cuda float32 [B, T*256], wav_lens np.int64 [B]).
+        host_lens=False returns wav_lens as a cuda int64 tensor instead: no host sync, so a caller
+        can queue several batches back to back (dist.ShardedSynthesis)."""
         import torch
         dev = self.engine.torch_device
         B, N = tokens.shape
@@ -140,9 +142,10 @@ class GonovaTTS:
             g = gcd(self.sr, self.native_sr)
             wav, out_lens = self.engine.resample(wav, mel_lens * self.vocoder_cfg.hop, self.sr // g,
                                                  self.native_sr // g, stream=stream)
-            return wav, out_lens.to(torch.int64).cpu().numpy()
-        wav_lens = mel_lens.to(torch.int64).cpu().numpy() * self.vocoder_cfg.hop
-        return wav, wav_lens
+            out_lens = out_lens.to(torch.int64)
+            return wav, (out_lens.cpu().numpy() if host_lens else out_lens)
+        wav_lens = mel_lens.to(torch.int64) * self.vocoder_cfg.hop
+        return wav, (wav_lens.cpu().numpy() if host_lens else wav_lens)
 
     # -------------------------------------------------------------- streaming
     STREAM_CONTEXT = 16  # mel frames of context per side; HiFi-GAN V1's receptive field is < 13

@@ -626,6 +626,9 @@ static int xres_mode() {  // TTS_CONV_XRES=0 disables the X-resident kernel (A/B
 // BN = 256) for M = 64 (the last upsampler)
 static int xres_wm(const ConvParams& p) { return p.M >= 128 ? 4 : 2; }
 
+#ifndef TTS_XRES_NARROW_KMIN
+#define TTS_XRES_NARROW_KMIN 0         // > 0: also below 2x the block limit when Cin*taps >= this (4096 / 1024 measured neutral on C3/C5)
+#endif
 #ifndef TTS_XRES_NARROW_MAXBLK
 #define TTS_XRES_NARROW_MAXBLK 256     // 0 disables; 512 measured slower for C3 (encoder at batch 32)
 #endif
@@ -640,7 +643,9 @@ static bool xres_narrow(const ConvParams& p, int nt) {
   const char* e = getenv("TTS_XRES_NARROW");
   if (e) return atoi(e) != 0;
   const long long blocks = (long long)((p.y_rows + 32 * nt - 1) / (32 * nt)) * ((p.M + 127) / 128) * p.B * p.nh;
-  return blocks < TTS_XRES_NARROW_MAXBLK;
+  if (blocks < TTS_XRES_NARROW_MAXBLK) return true;
+  // long-K launches (the encoder's FFN down-projection, K = 4608) up to twice that many blocks
+  return TTS_XRES_NARROW_KMIN > 0 && p.Cin * p.taps >= TTS_XRES_NARROW_KMIN && blocks < 2 * TTS_XRES_NARROW_MAXBLK;
 }
 
 #ifndef TTS_XRES_SMALL_TILES

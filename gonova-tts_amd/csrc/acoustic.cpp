@@ -290,11 +290,12 @@ struct AcousticModel::Impl {
       ln_rows(Y, Xb, rows, D, L.ln_mac, nullptr, s);
       // relative-position MHSA: x = LN(x + mhsa(x))
       run_layer(L.qkv, Xb, Tp, lens, QKV, Tp, B, dt, s, prof);
-      HIP_CHECK(launch_pos_bias(dt, QKV, rows, D, L.pos_u, L.pos_v, Qu, Qv, s));
+      const bool fused_attn = rel_attn_enabled() && rel_attn_supported(dt, D, H);
+      if (!fused_attn) HIP_CHECK(launch_pos_bias(dt, QKV, rows, D, L.pos_u, L.pos_v, Qu, Qv, s));
       HIP_CHECK(launch_transpose_v(dt, QKV, lens, B, Tp, D, H, Sk, Vt, s));
-      if (rel_attn_enabled() && rel_attn_supported(dt, D, H)) {
-        // fused flash-style relative-position attention (attention.hip)
-        HIP_CHECK(launch_rel_attn(dt, Qu, Qv, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale, O, s));
+      if (fused_attn) {
+        // fused flash-style relative-position attention (attention.hip); Qu / Qv formed in it
+        HIP_CHECK(launch_rel_attn(dt, L.pos_u, L.pos_v, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale, O, s));
         run_layer(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
         ln_rows(Y, Xb, rows, D, L.ln_att, nullptr, s);
         conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);

@@ -32,7 +32,7 @@ hipError_t launch_spk_bias(int dt, const float* e, int B, int E, const float* We
 
 // attention.hip: fused relative-position attention (16-bit dtypes, dk = 192)
 bool rel_attn_supported(int dt, int D, int H);
-hipError_t launch_rel_attn(int dt, const void* qu, const void* qv, const void* qkv, const void* vt, const void* ptab,
+hipError_t launch_rel_attn(int dt, const float* pos_u, const float* pos_v, const void* qkv, const void* vt, const void* ptab,
                            const int* lens, int B, int Tm, int Tp, int D, int H, int Sk, int rmax, float scale,
                            void* out, hipStream_t s);
 

@@ -31,7 +31,7 @@ constexpr int AT_BK = 32;   // keys per step
 constexpr int AT_RW = AT_BQ + AT_BK;  // R window rows per block (95 used)
 
 template <typename T, int DK>
-__global__ __launch_bounds__(256, 2) void rel_attn_kernel(const T* __restrict__ qu, const T* __restrict__ qv,
+__global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restrict__ pu, const float* __restrict__ pv,
                                                          const T* __restrict__ qkv, const T* __restrict__ vt,
                                                          const T* __restrict__ ptab, const int* __restrict__ lens,
                                                          int Tp, int D, int H, int Sk, int rmax, float scale,
@@ -63,12 +63,19 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const T* __restrict__ 
   const long long rowD = D;
   // this lane's query row (clamped into the buffer; rows >= len are computed, not stored)
   const int iq = min(i0w + q, Tp - 1);
+  // Qu = q + pos_bias_u, Qv = q + pos_bias_v (HF:420-423), formed here from the q slice of
+  // QKV and rounded to T once, exactly as the separate pos_bias_kernel materialised them
   Frag bu[KS], bv[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    const long long o = ((long long)b * Tp + iq) * rowD + h * DK + ks * 32 + 8 * g;
-    bu[ks] = *reinterpret_cast<const Frag*>(qu + o);
-    bv[ks] = *reinterpret_cast<const Frag*>(qv + o);
+    const int c = h * DK + ks * 32 + 8 * g;
+    const uint4 qw = *reinterpret_cast<const uint4*>(qkv + ((long long)b * Tp + iq) * 3 * rowD + c);
+    f32x4 q0, q1;
+    pair_ld8<T>(reinterpret_cast<const T*>(&qw), q0, q1);
+    const f32x4 u0 = *reinterpret_cast<const f32x4*>(pu + c), u1 = *reinterpret_cast<const f32x4*>(pu + c + 4);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(pv + c), v1 = *reinterpret_cast<const f32x4*>(pv + c + 4);
+    bu[ks] = __builtin_bit_cast(Frag, pack8<T>(q0 + u0, q1 + u1));
+    bv[ks] = __builtin_bit_cast(Frag, pack8<T>(q0 + v0, q1 + v1));
   }
   f32x4 oacc[DT];
 #pragma unroll
@@ -232,7 +239,7 @@ bool rel_attn_supported(int dt, int D, int H) {
   return (dt == DT_F16 || dt == DT_BF16) && H > 0 && D % H == 0 && D / H == 192;
 }
 
-hipError_t launch_rel_attn(int dt, const void* qu, const void* qv, const void* qkv, const void* vt, const void* ptab,
+hipError_t launch_rel_attn(int dt, const float* pos_u, const float* pos_v, const void* qkv, const void* vt, const void* ptab,
                            const int* lens, int B, int Tm, int Tp, int D, int H, int Sk, int rmax, float scale,
                            void* out, hipStream_t s) {
   if (!rel_attn_supported(dt, D, H) || Tm > rmax || Sk % 8) return hipErrorInvalidValue;
@@ -240,11 +247,11 @@ hipError_t launch_rel_attn(int dt, const void* qu, const void* qv, const void* q
   dim3 grid(xcd_grid(nqb, H * B));
   const size_t lds = rel_attn_lds<192>();
   if (dt == DT_F16)
-    hipLaunchKernelGGL((rel_attn_kernel<half_t, 192>), grid, dim3(256), lds, s, (const half_t*)qu, (const half_t*)qv,
+    hipLaunchKernelGGL((rel_attn_kernel<half_t, 192>), grid, dim3(256), lds, s, pos_u, pos_v,
                        (const half_t*)qkv, (const half_t*)vt, (const half_t*)ptab, lens, Tp, D, H, Sk, rmax, scale,
                        (half_t*)out, nqb, B);
   else
-    hipLaunchKernelGGL((rel_attn_kernel<bf16_t, 192>), grid, dim3(256), lds, s, (const bf16_t*)qu, (const bf16_t*)qv,
+    hipLaunchKernelGGL((rel_attn_kernel<bf16_t, 192>), grid, dim3(256), lds, s, pos_u, pos_v,
                        (const bf16_t*)qkv, (const bf16_t*)vt, (const bf16_t*)ptab, lens, Tp, D, H, Sk, rmax, scale,
                        (bf16_t*)out, nqb, B);
   return hipGetLastError();

@@ -108,12 +108,31 @@ class ShardedSynthesis:
         # ---- 4: local synthesis, packed as [index, length] table + flat samples ----
         idx_list, len_list, parts = [], [], []
         done = []
+        # the root's own audio goes to the host bucket by bucket on a side stream, overlapped
+        # with the next bucket's synthesis (pinned, cached buffers); the other ranks pack theirs
+        # for the gather
+        overlap = self.rank == self.root and torch.device(dev).type == "cuda"
+        side = torch.cuda.Stream(device=dev) if overlap else None
         for bk in mine:  # queue every bucket first: no host sync between them
             n_b = int(ln_h[bk].max())
-            done.append((bk,) + tuple(self.synth_fn(tok_h[bk, :n_b], ln_h[bk])))
-        for bk, wav, wav_lens in done:
+            wav, wav_lens = self.synth_fn(tok_h[bk, :n_b], ln_h[bk])
+            host = None
+            if overlap:
+                ev = torch.cuda.Event()
+                ev.record()
+                host = torch.empty(wav.shape, dtype=torch.float32, pin_memory=True)
+                with torch.cuda.stream(side):
+                    side.wait_event(ev)
+                    host.copy_(wav, non_blocking=True)
+                wav.record_stream(side)
+            done.append((bk, wav, wav_lens, host))
+        own = []
+        for bk, wav, wav_lens, host in done:
             if isinstance(wav_lens, torch.Tensor):
                 wav_lens = wav_lens.cpu().numpy()
+            if overlap:
+                own.append((bk, wav_lens, host))
+                continue
             for j, u in enumerate(bk):
                 L = int(wav_lens[j])
                 idx_list.append(u)
@@ -148,7 +167,15 @@ class ShardedSynthesis:
                 q.wait()
         tables[self.root], flats[self.root] = table, flat
         out: List[Optional[np.ndarray]] = [None] * B
+        if overlap:
+            side.synchronize()
+            for bk, wav_lens, host in own:
+                h = host.numpy()
+                for j, u in enumerate(bk):
+                    out[int(u)] = h[j, :int(wav_lens[j])]
         for r in range(self.world):
+            if overlap and r == self.root:
+                continue
             t = tables[r].cpu().numpy()
             f = flats[r]
             if f.is_cuda:  # one D2H copy through a pinned (cached) host buffer

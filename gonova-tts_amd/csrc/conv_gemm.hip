@@ -290,8 +290,8 @@ __device__ inline void ld8(const T* p, f32x4& a, f32x4& b) {
   b = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
 }
 
-template <typename T, int NT, int WM>
-__global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams p, int CG) {
+template <typename T, int NT, int WM, int OCC = TTS_XRES_OCC>
+__global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int CG) {
   using MF = Mfma<T>;
   typedef typename MF::frag Frag;
   static_assert(sizeof(T) == 2, "16-bit dtypes only");
@@ -599,17 +599,22 @@ __global__ __launch_bounds__(256, TTS_XRES_OCC) void conv_xres_kernel(ConvParams
 }
 
 constexpr int XRES_LDS_MAX = (160 / TTS_XRES_OCC - 1) * 1024;  // TTS_XRES_OCC blocks per CU (53 KB at 3)
+#ifndef TTS_XRES_BIGCG_MIN
+#define TTS_XRES_BIGCG_MIN 0           // > 0: Cin from which conv_xres stages big channel groups, one block per CU
+                                       // (1024 measured slower: C3 acoustic 5.14 -> 5.51 ms, C5 acoustic +40 us)
+#endif
+constexpr int XRES_LDS_BIG = 159 * 1024;
 
 // channel group for the X-resident kernel: largest power-of-two CG | Cin, CG >= 64, tile within
 // XRES_LDS_MAX; 0 = not eligible
-static int xres_group(const ConvParams& p, int BN) {
+static int xres_group(const ConvParams& p, int BN, int lds_max = XRES_LDS_MAX) {
   if (!p.wpk || p.M < 64 || p.Cin % 64 || p.M % 8 || p.nh != 1) return 0;
   if (p.syr % 8 || p.syb % 8 || ((p.r1 || p.r2) && (p.srr % 8 || p.srb % 8))) return 0;
   if (p.up_s && p.up_cout % 8) return 0;
   const int R = BN + (p.taps - 1) * p.dil;
   for (int cg = 2048; cg >= 64; cg /= 2) {  // powers of two (division-free staging)
     if (cg > p.Cin || p.Cin % cg) continue;
-    if ((size_t)R * (cg * 2 + 16) <= XRES_LDS_MAX) return cg;
+    if ((size_t)R * (cg * 2 + 16) <= (size_t)lds_max) return cg;
   }
   return 0;
 }
@@ -662,13 +667,13 @@ static int xres_nt(const ConvParams& p, int wm) {
   return 8 * r2 <= 7 * r4 ? 2 : 4;
 }
 
-template <typename T, int WM, int NT = 4>
+template <typename T, int WM, int NT = 4, int OCC = TTS_XRES_OCC>
 static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s) {
   constexpr int BM = 32 * WM, BN = 32 * NT * (4 / WM);
   const size_t lds = std::max((size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16),
                               TTS_XRES_EPI16 ? (size_t)BN * (BM * 2 + 16) : (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
   dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
-  hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM>), grid, dim3(256), lds, s, p, cg);
+  hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM, OCC>), grid, dim3(256), lds, s, p, cg);
   return hipGetLastError();
 }
 
@@ -680,10 +685,19 @@ static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err) {
   // channel group sized for 128-row tiles whatever the tile height: the group fixes the K
   // order of the accumulation, so a row's result does not depend on the tiling (streamed
   // chunks stay bit-identical to the full pass)
-  const int cg = xres_group(p, 32 * 4 * (4 / wm));
+  // long-K convs (Cin >= TTS_XRES_BIGCG_MIN: the FFN down-projections) stage 4x larger channel
+  // groups at one block per CU: a quarter of the single-buffered group stagings, each a full
+  // HBM/L2 round trip.  The choice depends on the layer shape only, so the K order is still
+  // the same for every batch size and tile shape.
+  const bool big = TTS_XRES_BIGCG_MIN > 0 && wm == 4 && p.Cin >= TTS_XRES_BIGCG_MIN;
+  const int cg = xres_group(p, 32 * 4 * (4 / wm), big ? XRES_LDS_BIG : XRES_LDS_MAX);
   if (!cg) return false;
   if (wm == 2)
     *err = launch_xres_wm<T, 2>(p, cg, s);
+  else if (big)
+    *err = xres_narrow(p, nt) ? launch_xres_wm<T, 2, 1, 1>(p, cg, s)
+           : nt == 2          ? launch_xres_wm<T, 4, 2, 1>(p, cg, s)
+                              : launch_xres_wm<T, 4, 4, 1>(p, cg, s);
   else if (xres_narrow(p, nt))
     *err = launch_xres_wm<T, 2, 1>(p, cg, s);
   else

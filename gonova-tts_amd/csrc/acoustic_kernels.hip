@@ -128,6 +128,44 @@ __global__ void transpose_v_kernel(const T* __restrict__ qkv, const int* __restr
   }
 }
 
+// 16-bit Vt for dk % 64 == 0, Sk % 8 == 0: 64 keys x 64 channels per block, 16-byte loads of
+// 8 channels of one key and 16-byte stores of 8 keys of one channel through an LDS tile (row
+// stride 72 elements: the column reads of a row group hit distinct banks).  The bits are copied
+// (the f32 round trip of the generic kernel is exact for 16-bit values); keys >= len are 0.
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_v16_kernel(const T* __restrict__ qkv, const int* __restrict__ lens,
+                                                            int Tm, int D, int H, int Sk, T* __restrict__ vt) {
+  constexpr int TS = 72;  // LDS row stride (elements)
+  __shared__ __attribute__((aligned(16))) T tile[64 * TS];
+  const int dk = D / H;
+  const int bh = blockIdx.z;
+  const int b = bh / H, h = bh - b * H;
+  const int L = min(lens[b], Tm);
+  const int j0 = blockIdx.x * 64, d0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = tid + 256 * i;
+    const int r = p >> 3, c = p & 7;
+    const int j = j0 + r;
+    uint4 u = uint4{0u, 0u, 0u, 0u};
+    if (j < L) u = *reinterpret_cast<const uint4*>(qkv + ((long long)b * Tm + j) * 3 * D + 2 * D + h * dk + d0 + 8 * c);
+    *reinterpret_cast<uint4*>(tile + r * TS + 8 * c) = u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = tid + 256 * i;
+    const int d = p >> 3, jc = p & 7;
+    const int j = j0 + 8 * jc;
+    if (j >= Sk) continue;
+    T o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = tile[(8 * jc + e) * TS + d];
+    *reinterpret_cast<uint4*>(vt + (((long long)b * H + h) * dk + d0 + d) * Sk + j) = *reinterpret_cast<const uint4*>(o);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // scores = (AC[i][j] + BD[i][(Tm-1) - i + j]) / sqrt(dk), key-masked softmax (HF:430-449,
 // shift_relative_position_tensor HF:381-393).  One wave per query row.
@@ -553,6 +591,16 @@ hipError_t launch_pos_bias(int dt, const void* qkv, int rows, int D, const float
 
 hipError_t launch_transpose_v(int dt, const void* qkv, const int* lens, int B, int Tm, int D, int H, int Sk, void* vt,
                               hipStream_t s) {
+  if (dt != DT_F32 && (D / H) % 64 == 0 && Sk % 8 == 0) {
+    dim3 g16((Sk + 63) / 64, (D / H) / 64, B * H);
+    if (dt == DT_F16)
+      hipLaunchKernelGGL(transpose_v16_kernel<half_t>, g16, dim3(256), 0, s, (const half_t*)qkv, lens, Tm, D, H, Sk,
+                         (half_t*)vt);
+    else
+      hipLaunchKernelGGL(transpose_v16_kernel<bf16_t>, g16, dim3(256), 0, s, (const bf16_t*)qkv, lens, Tm, D, H, Sk,
+                         (bf16_t*)vt);
+    return hipGetLastError();
+  }
   dim3 grid((Sk + 31) / 32, (D / H + 31) / 32, B * H);
   TTS_DISPATCH(dt, hipLaunchKernelGGL(transpose_v_kernel<TT>, grid, dim3(256), 0, s, (const TT*)qkv, lens, Tm, D, H,
                                       Sk, (TT*)vt));

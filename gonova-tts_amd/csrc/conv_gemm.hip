@@ -635,7 +635,7 @@ static int xres_wm(const ConvParams& p) { return p.M >= 128 ? 4 : 2; }
 #define TTS_XRES_NARROW_KMIN 0         // > 0: also below 2x the block limit when Cin*taps >= this (4096 / 1024 measured neutral on C3/C5)
 #endif
 #ifndef TTS_XRES_NARROW_MAXBLK
-#define TTS_XRES_NARROW_MAXBLK 256     // 0 disables; 512 measured slower for C3 (encoder at batch 32)
+#define TTS_XRES_NARROW_MAXBLK 256     // 0 disables; 512 slower for C3 (encoder at batch 32); 192 / 384 within noise
 #endif
 // Narrow 64 x 64 tiles (2 x 2 waves, one 32 x 32 MFMA tile each) for launches whose 128-channel
 // grid would leave the chip under-filled: the small-batch acoustic passes (streaming: batch 8;

@@ -11,17 +11,25 @@ durations forced to 6 frames/token -> 864 frames; acoustic bf16 + vocoder bf16,
 tokens in HBM -> waveform in HBM), measured after the headline loop.
 `--workload full` makes that the headline instead.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-utterances are independent, so every rank runs its own batch-32 shard with no
-data-path collective (weak scaling); the timed loop is bracketed by barriers and
-the max time over ranks is used.  value = samples of all ranks / max time.
+Multi-GPU: `bench.py --gpus N` runs one process per GPU.  Launched under
+`torch.distributed.run` (RANK / WORLD_SIZE set) it is a rank; launched plainly with N > 1
+it is a launcher that never touches the GPU and starts N fresh rank processes itself
+(RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1), then exits with their status.
+Every rank checks that the process group has exactly N ranks (a 1-GPU box asked for
+--gpus 2 fails loudly).  Utterances are independent, so C2 runs a batch-32 shard per
+rank with no data-path collective (weak scaling); the timed loop is bracketed by
+barriers and the max time over ranks is used.  value = samples of all ranks / max time.
+The same line carries `c4` (configs[3]: 256 mixed-length utterances owned by rank 0,
+RCCL broadcast -> per-rank length-bucketed synthesis -> RCCL P2P gather to rank 0 inside
+the timed region; strong scaling over N).
 
 `roofline` is for the dominant kernel family (largest summed time per step: today the
 fused ResBlock-pair kernel of all four stages), timed live with hipEvents around every launch
 on the stream it runs on; `roofline.kernels` lists every family the same way
 (conv_gemm_kernel, conv_xres_kernel, mrf_fused_kernel, mrf_pair_kernel, mrf_chain_kernel,
-upsample_stream_kernel).  `cpu_baseline`
-is the NumPy oracle on the host cores (bounded sample, rank 0, N=1 only).
+upsample_stream_kernel).  `cpu_baseline` (rank 0, N=1 only) is the torch-CPU fp32
+restatement (oracle/torch_cpu.py) timed on the host cores on a bounded
+sample of C2 (4 utterances) and C3 (2 utterances).
 """
 from __future__ import annotations
 
@@ -50,50 +58,127 @@ def parse():
     ap.add_argument("--frames", type=int, default=862)
     ap.add_argument("--tokens", type=int, default=144)
     ap.add_argument("--dtype", default="f16")
-    ap.add_argument("--workload", default="vocoder", choices=["vocoder", "full", "c4"])
+    ap.add_argument("--workload", default="vocoder", choices=["vocoder", "full", "c4", "selftest"],
+                    help="selftest: CPU-only gloo check of the launcher / process group (no GPU)")
     ap.add_argument("--c4-batch", type=int, default=256)
     ap.add_argument("--c4-bucket", type=int, default=64, help="utterances per length bucket (one synthesis call; 64 measured best of 32/64/128)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 sharded side measurement")
     ap.add_argument("--no-streaming", action="store_true", help="skip the C5 streaming latency side measurement")
     ap.add_argument("--no-full", action="store_true", help="skip the full-pipeline side measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=862, help="frames in the CPU-baseline sample")
+    ap.add_argument("--cpu-c2-batch", type=int, default=4, help="C2 utterances in the CPU-baseline sample")
+    ap.add_argument("--cpu-c3-batch", type=int, default=2, help="C3 utterances in the CPU-baseline sample")
     return ap.parse_args()
 
 
-def cpu_baseline(frames: int):
-    """NumPy fp32 oracle (oracle/vocoder.py) on one utterance of `frames` frames."""
-    from gonova_tts_amd.weights import make_vocoder_weights
-    from oracle.vocoder import vocoder_forward
-    w = make_vocoder_weights(seed=0)
-    mel = np.random.default_rng(0).standard_normal((frames, 80)).astype(np.float32)
-    vocoder_forward(mel[:8], w)  # warm BLAS
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without torch.distributed.run: start N rank processes of this
+    script (one per GPU) and return the first non-zero exit status.  This process does not
+    touch the GPU (torch.cuda.device_count() does not initialise HIP on this image), so the
+    children are fresh processes, never an exec of a GPU-initialised one."""
+    import socket
+    import subprocess
+    if args.workload != "selftest":
+        import torch
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {have} HIP device(s) visible", file=sys.stderr, flush=True)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        code = p.wait()
+        if code and not rc:
+            rc = code
+    return rc
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(b2: int, b3: int):
+    """torch-CPU fp32 restatement (oracle/torch_cpu.py) of C2 (vocoder, b2 x 862 frames) and C3
+    (tokens -> acoustic -> vocoder, b3 x 144 tokens x 6 frames) on the host cores.  value = the
+    C2 samples/s (the headline metric's config); c3 holds the full-pipeline rate."""
+    import torch
+    from gonova_tts_amd.weights import make_acoustic_weights, make_vocoder_weights
+    from oracle.torch_cpu import TorchAcoustic, TorchVocoder
+    # the box's CPU share is what OMP_NUM_THREADS says (os.cpu_count() is the whole host)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    threads = min(threads, os.cpu_count() or threads)
+    torch.set_num_threads(threads)
+    voc = TorchVocoder(make_vocoder_weights(seed=0))
+    g = torch.Generator().manual_seed(0)
+    mel = torch.randn((b2, 862, 80), generator=g)
+    voc(mel[:1, :16])  # warm up the thread pool
     t = time.perf_counter()
-    wav = vocoder_forward(mel, w)
-    dt = time.perf_counter() - t
-    threads = os.environ.get("OMP_NUM_THREADS") or os.environ.get("OPENBLAS_NUM_THREADS")
-    cores = int(threads) if threads else (os.cpu_count() or 1)
-    return {"value": round(len(wav) / dt, 1), "unit": "samples/s", "cores": cores, "kind": "port",
-            "sample": f"1 utterance x {frames} frames ({len(wav) / SR:.2f} s audio), NumPy fp32 oracle "
-                      f"(oracle/vocoder.py), {dt:.1f} s wall"}
+    wav = voc(mel)
+    dt2 = time.perf_counter() - t
+    ac = TorchAcoustic(make_acoustic_weights(seed=0, fixed_duration=6))
+    ids = torch.randint(1, 78, (b3, 144), generator=g)
+    dur = torch.full((b3, 144), 6, dtype=torch.int64)
+    t = time.perf_counter()
+    m, _ = ac(ids, dur)
+    w3 = voc(m)
+    dt3 = time.perf_counter() - t
+    return {"value": round(wav.numel() / dt2, 1), "unit": "samples/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(),
+            "sample": f"C2: {b2} utterances x 862 frames ({wav.numel() / SR:.1f} s audio) in {dt2:.1f} s; "
+                      f"torch-CPU fp32 restatement (oracle/torch_cpu.py), {threads} threads",
+            "c3": {"value": round(w3.numel() / dt3, 1), "unit": "samples/s",
+                   "sample": f"C3: {b3} utterances x 144 tokens x 6 frames ({w3.numel() / SR:.1f} s audio) in "
+                             f"{dt3:.1f} s (acoustic + vocoder)"}}
 
 
 class Ctx:
-    def __init__(self):
+    def __init__(self, args):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.cpu = args.workload == "selftest"
         if self.world > 1:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
-        torch.cuda.set_device(self.local)
-        self.dev = torch.device("cuda", self.local)
+            if self.cpu:
+                dist.init_process_group("gloo")
+            else:
+                if self.local >= torch.cuda.device_count():
+                    raise SystemExit(f"bench.py rank {self.rank}: LOCAL_RANK {self.local} but only "
+                                     f"{torch.cuda.device_count()} HIP device(s) visible")
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            self.world = dist.get_world_size()
+            self.rank = dist.get_rank()
+        if self.world != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {self.world} rank(s); "
+                             "run `bench.py --gpus N` (it starts N ranks) or torch.distributed.run "
+                             "--nproc-per-node N bench.py --gpus N")
+        if self.cpu:
+            self.dev = torch.device("cpu")
+        else:
+            torch.cuda.set_device(self.local)
+            self.dev = torch.device("cuda", self.local)
 
     def barrier(self):
         if self.world > 1:
             self.dist.barrier()
-        self.torch.cuda.synchronize()
+        if not self.cpu:
+            self.torch.cuda.synchronize()
 
     def max_over_ranks(self, x: float) -> float:
         if self.world == 1:
@@ -105,7 +190,8 @@ class Ctx:
     def timed(self, step, steps, warmup, eng=None):
         for _ in range(warmup):
             step()
-        self.torch.cuda.synchronize()
+        if not self.cpu:
+            self.torch.cuda.synchronize()
         # Live kernel timing (hipEvents around every MFMA launch, on its own stream) brackets
         # the LAST `nprof` timed steps only: two events per launch cost ~0.3 ms per C2 step
         # (1.6 %), which production runs do not pay.  The per-family averages come from those
@@ -233,10 +319,10 @@ def bench_full(ctx, args, steps, warmup):
             "roofline": roofline(prof, el, steps, "bf16", None, getattr(ctx, "prof_steps", None))}
 
 
-def bench_c4(ctx, args):
+def bench_c4(ctx, args, steps, warmup):
     """Config C4: B utterances of mixed length (N_i ~ U{29..144} tokens x 6 frames) owned by rank 0,
-    broadcast -> per-rank length-bucketed synthesis -> RCCL P2P gather to rank 0 (strong scaling)."""
-    torch = ctx.torch
+    RCCL broadcast -> per-rank length-bucketed synthesis -> RCCL P2P gather to rank 0, all inside
+    the timed region (strong scaling: the same 256 utterances whatever N)."""
     from gonova_tts_amd.dist import ShardedSynthesis
     from gonova_tts_amd.model import GonovaTTS
     B = args.c4_batch
@@ -254,11 +340,22 @@ def bench_c4(ctx, args):
 
     sh = ShardedSynthesis(synth, ctx.dev, bucket=args.c4_bucket)
     run = lambda: sh.run(tok if ctx.rank == 0 else None, lens if ctx.rank == 0 else None)  # noqa: E731
-    el, _ = ctx.timed(run, args.steps, args.warmup)
-    samples = int(lens.sum()) * 6 * 256 * args.steps
+    el, _ = ctx.timed(run, steps, warmup)
+    out = run()  # one more pass, checked: every utterance back on the root at its length
+    if ctx.rank == 0:
+        bad = [i for i in range(B) if out[i] is None or out[i].shape[0] != int(lens[i]) * 6 * 256]
+        assert not bad, f"C4 gather lost utterances {bad[:8]}"
+    m.engine.close()
+    samples = int(lens.sum()) * 6 * 256 * steps
     value = samples / el
-    return {"value": value, "ms_per_step": el * 1e3 / args.steps, "batch": B,
-            "audio_s_per_step": int(lens.sum()) * 6 * 256 / SR}
+    return {"value": round(value, 1), "unit": "samples/s", "n_gpus": ctx.world, "scaling": "strong",
+            "steps": steps, "warmup": warmup, "ms_per_step": round(el * 1e3 / steps, 3),
+            "per_gpu_samples_per_s": round(value / ctx.world, 1),
+            "x_realtime_per_gpu": round(value / ctx.world / SR, 2), "dtype": "bf16",
+            "config": {"workload": f"C4 batch-{B} mixed-length utterances (N_i ~ U{{29..144}} tokens x 6 frames, "
+                                   f"{int(lens.sum()) * 6 * 256 / SR:.0f} s audio), length buckets of "
+                                   f"{args.c4_bucket}, RCCL broadcast + P2P gather to rank 0 inside the timed region",
+                       "global_batch": B, "parallelism": f"utterance-sharded dp{ctx.world}"}}
 
 
 def bench_streaming(ctx, trials=50, B=8, N=144, chunk=32):
@@ -288,26 +385,29 @@ def bench_streaming(ctx, trials=50, B=8, N=144, chunk=32):
                       f"+ 16 frames context, bf16"}
 
 
+def selftest(ctx, args):
+    """CPU-only check of the launcher and process group (tests/test_bench_cpu.py): every rank
+    contributes its rank to a gloo all-reduce inside the same barrier-bracketed timing."""
+    t = ctx.torch.tensor([float(ctx.rank)])
+    el, _ = ctx.timed(lambda: ctx.dist.all_reduce(t) if ctx.world > 1 else None, 1, 0)
+    return {"metric": METRIC, "value": None, "unit": "samples/s", "n_gpus": ctx.world, "steps": 1, "warmup": 0,
+            "ms_per_step": round(el * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "none", "data": "selftest (no GPU)", "rank_sum": float(t.item()),
+            "config": {"workload": "selftest", "parallelism": f"dp{ctx.world}"}}
+
+
 def main():
     args = parse()
-    ctx = Ctx()
-    if args.workload == "c4":
-        c = bench_c4(ctx, args)
-        out = {"metric": METRIC, "value": round(c["value"], 1), "unit": "samples/s", "n_gpus": ctx.world,
-               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(c["ms_per_step"], 3),
-               "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
-               "data": "synthetic (token ids U[1,77], N_i ~ U{29..144}, forced 6 frames/token, seeded weights)",
-               "config": {"workload": f"C4 batch-{c['batch']} mixed-length utterances, length-bucketed, "
-                                      "broadcast + RCCL P2P gather to rank 0 inside the timed region",
-                          "global_batch": c["batch"], "parallelism": f"utterance-sharded dp{ctx.world}"},
-               "per_gpu_samples_per_s": round(c["value"] / ctx.world, 1),
-               "x_realtime_per_gpu": round(c["value"] / ctx.world / SR, 2)}
-        if ctx.rank == 0:
-            print(json.dumps(out), flush=True)
-        if ctx.world > 1:
-            ctx.dist.destroy_process_group()
-        return
-    if args.workload == "vocoder":
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    ctx = Ctx(args)
+    if args.workload == "selftest":
+        out = selftest(ctx, args)
+    elif args.workload == "c4":
+        c = bench_c4(ctx, args, args.steps, args.warmup)
+        out = dict({"metric": METRIC}, **c, higher_is_better=True, vs_baseline=None,
+                   data="synthetic (token ids U[1,77], N_i ~ U{29..144}, forced 6 frames/token, seeded weights)")
+    elif args.workload == "vocoder":
         v = bench_vocoder(ctx, args)
         per_gpu = v["value"] / ctx.world
         out = {
@@ -328,6 +428,8 @@ def main():
         }
         if not args.no_full:
             out["full_pipeline"] = bench_full(ctx, args, steps=max(3, args.steps // 2), warmup=1)
+        if not args.no_c4:
+            out["c4"] = bench_c4(ctx, args, steps=max(2, args.steps // 3), warmup=1)
         if not args.no_streaming and ctx.rank == 0:
             out["streaming"] = bench_streaming(ctx)
     else:
@@ -342,8 +444,8 @@ def main():
                "per_gpu_samples_per_s": round(per_gpu, 1), "x_realtime_per_gpu": round(per_gpu / SR, 2),
                "rtf": round(SR / per_gpu, 7), "acoustic_ms_per_step": f["acoustic_ms_per_step"],
                "roofline": f["roofline"]}
-    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:  # rank 0 at N=1 only
-        out["cpu_baseline"] = cpu_baseline(args.cpu_frames)
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline and args.workload != "selftest":
+        out["cpu_baseline"] = cpu_baseline(args.cpu_c2_batch, args.cpu_c3_batch)  # rank 0 at N=1 only
     if ctx.rank == 0:
         print(json.dumps(out), flush=True)
     if ctx.world > 1:

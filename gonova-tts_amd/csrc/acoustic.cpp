@@ -93,6 +93,7 @@ struct AcousticModel::Impl {
   ~Impl() {
     for (void* p : allocs) hipFree(p);
     for (void* p : ws) hipFree(p);
+    for (void* p : score_ws) hipFree(p);
   }
 
   void* track(void* p) { allocs.push_back(p); return p; }
@@ -226,11 +227,56 @@ struct AcousticModel::Impl {
     return p;
   }
 
+  // Drop the workspace: caps to 0 and every pointer to null BEFORE freeing, so a failed
+  // re-reservation (HIP_CHECK throws midway) can never leave a cap describing freed memory.
+  void drop_ws() {
+    cap_B = cap_N = cap_T = 0;
+    X = Y = O = G = Qu = Qv = H1 = QKV = A = Vt = ENC = SPK = PB1 = PB2 = BEF = PN1 = PN2 = MELT = nullptr;
+    f_pitch = f_energy = f_logd = nullptr;
+    i_dur = i_tokmap = nullptr;
+    std::vector<void*> old;
+    old.swap(ws);
+    for (void* p : old) hipFree(p);
+    drop_scores();
+  }
+
+  // The unfused attention path's score buffers (AC / BD / P: B*H*Tm*(Sac+Sbd+Sk) elements,
+  // quadratic in the frame cap) exist only while that path runs (fp32, TTS_REL_ATTN=0).
+  int cap_sB = 0, cap_sTm = 0;
+  std::vector<void*> score_ws;
+  void drop_scores() {
+    cap_sB = cap_sTm = 0;
+    AC = BD = P = nullptr;
+    std::vector<void*> old;
+    old.swap(score_ws);
+    for (void* p : old) hipFree(p);
+  }
+  void reserve_scores(int B, int Tm) {
+    if (B <= cap_sB && Tm <= cap_sTm) return;
+    B = std::max(B, cap_sB); Tm = std::max(Tm, cap_sTm);
+    drop_scores();
+    const size_t e = dtype_size(dt);
+    const int Sk = rup(Tm, 16), Sac = rup(Tm, 16), Sbd = rup(2 * Tm, 16);
+    auto al = [&](size_t n) { void* p = alloc_ws(n, e); ws.pop_back(); score_ws.push_back(p); return p; };
+    AC = al((size_t)B * H * Tm * Sac);
+    BD = al((size_t)B * H * Tm * Sbd);
+    P = al((size_t)B * H * Tm * Sk);
+    cap_sB = B; cap_sTm = Tm;
+  }
+
   void reserve(int B, int N, int T) {
     if (B <= cap_B && N <= cap_N && T <= cap_T) return;
     B = std::max(B, cap_B); N = std::max(N, cap_N); T = std::max(T, cap_T);
-    for (void* p : ws) hipFree(p);
-    ws.clear();
+    drop_ws();
+    try {
+      reserve_fresh(B, N, T);
+    } catch (...) {
+      drop_ws();  // release what was allocated before the failure; caps stay 0
+      throw;
+    }
+  }
+
+  void reserve_fresh(int B, int N, int T) {
     const size_t e = dtype_size(dt);
     const int Tm = std::max(N, T);
     const int Tp = rup(Tm, 32);
@@ -239,11 +285,8 @@ struct AcousticModel::Impl {
     X = alloc_ws(rows * D, e); Y = alloc_ws(rows * D, e); O = alloc_ws(rows * D, e); G = alloc_ws(rows * D, e);
     Qu = alloc_ws(rows * D, e); Qv = alloc_ws(rows * D, e);
     H1 = alloc_ws(rows * FFN, e); QKV = alloc_ws(rows * 3 * D, e); A = alloc_ws(rows * 2 * D, e);
-    const int Sk = rup(Tm, 16), Sac = rup(Tm, 16), Sbd = rup(2 * Tm, 16);
+    const int Sk = rup(Tm, 16);
     Vt = alloc_ws((size_t)B * H * dk * Sk, e);
-    AC = alloc_ws((size_t)B * H * Tm * Sac, e);
-    BD = alloc_ws((size_t)B * H * Tm * Sbd, e);
-    P = alloc_ws((size_t)B * H * Tm * Sk, e);
     const size_t nrows = (size_t)B * rup(N, 32);
     ENC = alloc_ws(nrows * D, e);
     SPK = alloc_ws((size_t)B * D, e);
@@ -347,6 +390,7 @@ struct AcousticModel::Impl {
                int* mel_lens, int Tcap, int* durations, const float* spk, hipStream_t s) {
     reserve(B, N, Tcap);
     const int Tm = std::max(N, Tcap);
+    if (!(rel_attn_enabled() && rel_attn_supported(dt, D, H))) reserve_scores(B, Tm);
     if (Tm > rmax) build_ptabs(rup(Tm, 256), s);
     const float xscale = std::sqrt((float)D);
     const int Np = rup(N, 32), Tp = rup(Tcap, 32);

@@ -118,8 +118,25 @@ struct tts_engine {
   struct Resampler { int up, down, nq, n_pre_remove; float* hp; };
   std::vector<Resampler> resamplers;
 
+  // The workspace above is shared by every call on this engine.  A call on a stream other
+  // than the previous call's first waits for everything already enqueued on that stream
+  // (an event edge), so two callers on two streams never overwrite each other's scratch.
+  hipStream_t last_stream = nullptr;
+  bool has_last = false;
+  hipEvent_t order_ev = nullptr;
+  void order_after_previous(hipStream_t s) {
+    if (has_last && s != last_stream) {
+      if (!order_ev) HIP_CHECK(hipEventCreateWithFlags(&order_ev, hipEventDisableTiming));
+      HIP_CHECK(hipEventRecord(order_ev, last_stream));
+      HIP_CHECK(hipStreamWaitEvent(s, order_ev, 0));
+    }
+    last_stream = s;
+    has_last = true;
+  }
+
   ~tts_engine() {
     hipSetDevice(device);
+    if (order_ev) hipEventDestroy(order_ev);
     for (void* p : allocs) hipFree(p);
     for (void*& p : vbuf) if (p) hipFree(p);
     if (vmel) hipFree(vmel);
@@ -337,7 +354,15 @@ struct tts_engine {
     if (need > vbuf_elems) {
       for (void*& p : vbuf) { if (p) hipFree(p); p = nullptr; }
       vbuf_elems = 0;
-      for (void*& p : vbuf) HIP_CHECK(hipMalloc(&p, need * dtype_size(dt)));
+      for (void*& p : vbuf) {
+        if (hipMalloc(&p, need * dtype_size(dt)) != hipSuccess) {
+          (void)hipGetLastError();
+          p = nullptr;
+          for (void*& q : vbuf) { if (q) hipFree(q); q = nullptr; }  // release the partial set
+          throw TtsError(TTS_ERR_HIP, "vocoder workspace: hipMalloc of " + std::to_string(need * dtype_size(dt)) +
+                                          " bytes failed");
+        }
+      }
       vbuf_elems = need;
     }
     const size_t mel_need = (size_t)B * T * voc.conv_pre.Cin;
@@ -353,6 +378,17 @@ struct tts_engine {
       HIP_CHECK(hipMalloc(&vlens, sizeof(int) * 16 * B));
       vlens_batch = B;
     }
+  }
+
+  // streaming window output (tts_vocoder_forward_chunk): [B][T_win * hop] fp32
+  void reserve_chunk(int B, int T_win) {
+    const size_t need = (size_t)B * T_win * voc.hop;
+    if (need <= vchunk_elems) return;
+    float* old = vchunk_wav;
+    vchunk_wav = nullptr; vchunk_elems = 0;
+    if (old) HIP_CHECK(hipFree(old));
+    HIP_CHECK(hipMalloc(&vchunk_wav, need * 4));
+    vchunk_elems = need;
   }
 
   void run_conv(const ConvLayer& L, const void* x, long long sxb, int sxr, const int* x_len, int x_rows,
@@ -656,7 +692,10 @@ int tts_engine_finalize(tts_engine* eng) {
     if (!eng->voc.loaded && !eng->ac.loaded) throw TtsError(TTS_ERR_STATE, "no known weights were set");
     eng->host.clear();
     eng->finalized = true;
-    if (eng->cfg.max_batch > 0 && eng->cfg.max_frames > 0) eng->reserve_vocoder(eng->cfg.max_batch, eng->cfg.max_frames);
+    if (eng->cfg.max_batch > 0 && eng->cfg.max_frames > 0 && eng->voc.loaded) {
+      eng->reserve_vocoder(eng->cfg.max_batch, eng->cfg.max_frames);
+      eng->reserve_chunk(eng->cfg.max_batch, eng->cfg.max_frames);
+    }
     if (eng->ac.loaded && eng->cfg.max_batch > 0 && eng->cfg.max_tokens > 0 && eng->cfg.max_frames > 0)
       eng->ac.reserve(eng->cfg.max_batch, eng->cfg.max_tokens, eng->cfg.max_frames);
   });
@@ -666,7 +705,10 @@ int tts_engine_reserve(tts_engine* eng, int max_batch, int max_frames, int max_t
   return guarded(eng, [&] {
     if (!eng->finalized) throw TtsError(TTS_ERR_STATE, "finalize first");
     if (max_batch <= 0 || max_frames <= 0) throw TtsError(TTS_ERR_INVALID, "bad reserve sizes");
-    eng->reserve_vocoder(max_batch, max_frames);
+    if (eng->voc.loaded) {
+      eng->reserve_vocoder(max_batch, max_frames);
+      eng->reserve_chunk(max_batch, max_frames);
+    }
     if (eng->ac.loaded && max_tokens > 0) eng->ac.reserve(max_batch, max_tokens, max_frames);
   });
 }
@@ -678,6 +720,7 @@ int tts_vocoder_forward(tts_engine* eng, const float* d_mel, const int32_t* d_me
   return guarded(eng, [&] {
     if (!eng->finalized) throw TtsError(TTS_ERR_STATE, "finalize first");
     if (!d_mel || !d_mel_lens || !d_wav || B <= 0 || T <= 0) throw TtsError(TTS_ERR_INVALID, "bad vocoder args");
+    eng->order_after_previous((hipStream_t)stream);
     eng->vocoder_forward(d_mel, d_mel_lens, B, T, d_wav, (long long)T * eng->voc.hop, (hipStream_t)stream);
   });
 }
@@ -689,15 +732,10 @@ int tts_vocoder_forward_chunk(tts_engine* eng, const float* d_mel, const int32_t
     if (!d_mel || !d_win_lens || !d_wav || B <= 0 || T_win <= 0 || ctx_left < 0 || T_chunk <= 0 ||
         ctx_left + T_chunk > T_win)
       throw TtsError(TTS_ERR_INVALID, "bad chunk args");
-    const int hop = eng->voc.hop;
-    const size_t need = (size_t)B * T_win * hop;
-    if (need > eng->vchunk_elems) {
-      if (eng->vchunk_wav) hipFree(eng->vchunk_wav);
-      eng->vchunk_wav = nullptr; eng->vchunk_elems = 0;
-      HIP_CHECK(hipMalloc(&eng->vchunk_wav, need * 4));
-      eng->vchunk_elems = need;
-    }
     hipStream_t s = (hipStream_t)stream;
+    eng->order_after_previous(s);
+    const int hop = eng->voc.hop;
+    eng->reserve_chunk(B, T_win);
     eng->vocoder_forward(d_mel, d_win_lens, B, T_win, eng->vchunk_wav, (long long)T_win * hop, s);
     HIP_CHECK(hipMemcpy2DAsync(d_wav, (size_t)T_chunk * hop * 4, eng->vchunk_wav + (size_t)ctx_left * hop,
                                (size_t)T_win * hop * 4, (size_t)T_chunk * hop * 4, B, hipMemcpyDeviceToDevice, s));
@@ -714,6 +752,7 @@ int tts_acoustic_forward_spk(tts_engine* eng, const int32_t* d_tokens, const int
       throw TtsError(TTS_ERR_INVALID, "bad acoustic args");
     if (d_spk_emb && eng->ac.speaker_dim() && spk_dim != eng->ac.speaker_dim())
       throw TtsError(TTS_ERR_INVALID, "speaker embedding size does not match the model's projection");
+    eng->order_after_previous((hipStream_t)stream);
     eng->ac.forward(d_tokens, d_tok_lens, B, N, d_dur_override, d_mel, d_mel_lens, Tcap, d_durations, d_spk_emb,
                     (hipStream_t)stream);
   });
@@ -786,6 +825,7 @@ int tts_resample_poly(tts_engine* eng, const float* d_in, int64_t in_stride, con
       eng->resamplers.push_back({up, down, nq, npr, d});
       rs = &eng->resamplers.back();
     }
+    eng->order_after_previous((hipStream_t)stream);
     HIP_CHECK(launch_resample_poly(d_in, in_stride, d_in_lens, B, up, down, rs->nq, rs->n_pre_remove, rs->hp, d_out,
                                    out_stride, out_cap, d_out_lens, (hipStream_t)stream));
   });

@@ -21,11 +21,16 @@ struct TtsError : std::runtime_error {
   TtsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 
+// On failure the error is also consumed from HIP's per-thread last-error slot, so a caught
+// failure (e.g. an out-of-memory reservation) is not reported again by the next launch check
+// of another library (PyTorch) on this thread.
 #define HIP_CHECK(expr)                                                                       \
   do {                                                                                        \
     hipError_t _e = (expr);                                                                   \
-    if (_e != hipSuccess)                                                                     \
+    if (_e != hipSuccess) {                                                                   \
+      (void)hipGetLastError();                                                                \
       throw ::tts::TtsError(TTS_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    }                                                                                         \
   } while (0)
 
 inline size_t dtype_size(int dt) { return dt == DT_F32 ? 4 : 2; }

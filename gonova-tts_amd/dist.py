@@ -7,8 +7,10 @@ GPU (torch.distributed, backend "nccl" = RCCL over xGMI) shares one request batc
   1. rank 0 owns the batch: token matrix int32 [B, N] + lengths [B];
   2. one broadcast of [B, N] + [B] (~147 KB at B=256, N=144) -- the "scatter": every
      rank derives the same deterministic plan and keeps only its rows;
-  3. plan: sort utterances by length, cut buckets of 32, assign buckets to ranks
-     longest-processing-time-first by total tokens (balances mixed lengths);
+  3. plan: deal utterances longest-first to the least-loaded rank (longest processing
+     time first, load = total tokens, at most ceil(B / world) utterances per rank), then
+     each rank cuts its share, sorted by length, into buckets of `bucket` utterances (one
+     engine call each);
   4. each rank synthesizes its buckets on its own GPU (no collective on the data path);
   5. gather: every rank packs its waveforms into one flat float32 buffer and sends it
      to rank 0 with RCCL point-to-point (batch_isend_irecv -> ncclSend/ncclRecv in one
@@ -115,7 +117,11 @@ class ShardedSynthesis:
         side = torch.cuda.Stream(device=dev) if overlap else None
         for bk in mine:  # queue every bucket first: no host sync between them
             n_b = int(ln_h[bk].max())
-            wav, wav_lens = self.synth_fn(tok_h[bk, :n_b], ln_h[bk])
+            if n_b == 0:  # only empty utterances: nothing to synthesize, empty waveforms
+                wav = torch.zeros((len(bk), 0), dtype=torch.float32, device=dev)
+                wav_lens = np.zeros(len(bk), np.int64)
+            else:
+                wav, wav_lens = self.synth_fn(tok_h[bk, :n_b], ln_h[bk])
             host = None
             if overlap:
                 ev = torch.cuda.Event()

@@ -118,23 +118,17 @@ class TTSService:
 
         async def receive():
             async for message in ws.iter_text():
+                # one bad message never ends the connection: the reference wraps each message
+                # in try/except and keeps going (server.py:258-263)
                 try:
                     data = json.loads(message)
-                except ValueError:
-                    continue
-                kind = data.get("type")
-                if kind == "synthesize":
-                    vid = data.get("voice_id", "default")
-                    # unknown voices fall back to the default voice (reference server.py:127-138)
-                    await self.queues.enqueue_request(
-                        connection_id=conn_id, text=data.get("text", ""), voice_id=vid,
-                        chunk_size=data.get("chunk_size", self.chunk_size),
-                        exaggeration=data.get("exaggeration", 0.5), streaming=data.get("streaming", True),
-                        voice=self.voices.get(vid))
-                elif kind == "register_voice":
-                    await ws.send_json(self.register_voice(data))
-                elif kind == "list_voices":
-                    await ws.send_json({"type": "voice_list", "voices": self.list_voices()})
+                    if not isinstance(data, dict):
+                        raise ValueError("message is not a JSON object")
+                    await self.handle_message(ws, conn_id, data)
+                except WebSocketDisconnect:
+                    raise
+                except Exception as e:  # noqa: BLE001
+                    logger.error("message handling error on %s: %s", conn_id, e)
 
         async def send():
             while True:
@@ -163,6 +157,25 @@ class TTSService:
             self.sockets.pop(conn_id, None)
             self.active_connections -= 1
 
+    async def handle_message(self, ws, conn_id: str, data: dict):
+        """One client message (reference server.py:215-256)."""
+        kind = data.get("type")
+        if kind == "synthesize":
+            vid = data.get("voice_id", "default")
+            text = data.get("text", "")
+            if not isinstance(text, str):
+                raise ValueError("text must be a string")
+            # unknown voices fall back to the default voice (reference server.py:127-138)
+            await self.queues.enqueue_request(
+                connection_id=conn_id, text=text, voice_id=vid,
+                chunk_size=data.get("chunk_size", self.chunk_size),
+                exaggeration=data.get("exaggeration", 0.5), streaming=data.get("streaming", True),
+                voice=self.voices.get(vid) if isinstance(vid, str) else None)
+        elif kind == "register_voice":
+            await ws.send_json(self.register_voice(data))
+        elif kind == "list_voices":
+            await ws.send_json({"type": "voice_list", "voices": self.list_voices()})
+
     def register_voice(self, data: dict) -> dict:
         """`register_voice` (reference server.py:226-248): this engine conditions on speaker
         embeddings (HF speaker_embed_dim), so a voice is registered from
@@ -172,10 +185,13 @@ class TTSService:
         vid = data.get("voice_id")
         emb = data.get("speaker_embedding")
         dim = getattr(getattr(self.model, "acoustic_cfg", None), "speaker_embed_dim", None)
-        if not vid or emb is None:
+        if not vid or not isinstance(vid, str) or emb is None:
             return {"type": "error", "message": "Voice registration failed: send voice_id and speaker_embedding "
                                                 "(no speaker encoder for reference_audio)"}
-        v = np.asarray(emb, np.float32).reshape(-1)
+        try:
+            v = np.asarray(emb, np.float32).reshape(-1)
+        except (TypeError, ValueError):
+            return {"type": "error", "message": "Voice registration failed: speaker_embedding must be a list of numbers"}
         if not dim or v.size != dim or not np.all(np.isfinite(v)):
             return {"type": "error", "message": f"Voice registration failed: the model takes {dim or 0}-value "
                                                 f"speaker embeddings, got {v.size}"}

@@ -27,7 +27,10 @@
  *   - Return 0 on success, a negative TTS_ERR_* on failure; no C++ exception crosses
  *     the ABI.  Every entry sets the HIP device and takes a per-engine mutex, so any
  *     host thread may call (the reference calls from a ThreadPoolExecutor,
- *     synthesizer.py:312).
+ *     synthesizer.py:312).  The engine's workspace is shared by all calls: a forward
+ *     enqueued on a stream other than the previous call's is made to wait (event edge)
+ *     for everything the previous call's stream had enqueued, so calls from different
+ *     threads / streams run one after another on the device, never interleaved.
  *   - Activations are channels-last: mel [B][T][80] float32 (HF spectrogram layout),
  *     waveform [B][T*256] float32 at 22,050 Hz.  Compute dtype per stage is chosen
  *     at create time; accumulation is always fp32.

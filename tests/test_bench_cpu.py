@@ -1,0 +1,46 @@
+"""bench.py's multi-GPU launcher on CPU (no GPU): `bench.py --gpus N` starts N rank processes
+of itself and every rank checks the process group it joined; the gloo selftest workload runs
+the same barrier-bracketed timing and max-over-ranks path as the GPU workloads."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env_extra=None, timeout=180):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout,
+                          env=env, cwd=ROOT)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_spawns_n_gloo_ranks(n):
+    r = _run(["--gpus", str(n), "--workload", "selftest"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 alone prints the one JSON line
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n
+    assert out["rank_sum"] == n * (n - 1) / 2  # every rank took part in the all-reduce
+    assert out["config"]["parallelism"] == f"dp{n}"
+
+
+def test_world_size_mismatch_fails_loudly():
+    r = _run(["--gpus", "2", "--workload", "selftest"], env_extra={"WORLD_SIZE": "1"})
+    assert r.returncode != 0
+    assert "process group has 1 rank" in r.stderr
+
+
+def test_more_gpus_than_visible_fails_loudly():
+    import torch
+    if torch.cuda.device_count() >= 64:
+        pytest.skip("machine has that many devices")
+    r = _run(["--gpus", "64"])
+    assert r.returncode == 2
+    assert "HIP device(s) visible" in r.stderr

@@ -36,11 +36,19 @@ def make_batch(B=70, seed=0):
     return tok, lens
 
 
-def _worker(rank, world, port, q):
+def make_batch_with_empties(B=40, seed=4):
+    """Mixed lengths plus enough zero-length utterances that whole buckets are empty."""
+    tok, lens = make_batch(B, seed)
+    lens[::2] = 0
+    tok[::2] = 0
+    return tok, lens
+
+
+def _worker(rank, world, port, q, empties=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        tok, lens = make_batch()
+        tok, lens = make_batch_with_empties() if empties else make_batch()
         sh = ShardedSynthesis(fake_synth, torch.device("cpu"), bucket=16)
         out = sh.run(tok if rank == 0 else None, lens if rank == 0 else None)
         if rank == 0:
@@ -59,12 +67,12 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_gather_restores_order(world):
+@pytest.mark.parametrize("world,empties", [(2, False), (3, False), (2, True)])
+def test_sharded_gather_restores_order(world, empties):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, empties)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -96,3 +104,24 @@ def test_single_process_without_group():
     out = ShardedSynthesis(fake_synth, torch.device("cpu"), bucket=16).run(tok, lens)
     for o, e in zip(out, expected(tok, lens)):
         np.testing.assert_array_equal(o, e)
+
+
+def test_all_empty_buckets_yield_empty_waveforms():
+    """Zero-length utterances collect in the last buckets (longest first); a bucket made only
+    of them is not sent to the engine (which rejects N = 0) and comes back as empty audio."""
+    calls = []
+
+    def synth(t, l):
+        assert t.shape[1] > 0
+        calls.append(len(l))
+        return fake_synth(t, l)
+
+    tok, lens = make_batch_with_empties()
+    out = ShardedSynthesis(synth, torch.device("cpu"), bucket=8).run(tok, lens)
+    for o, e, L in zip(out, expected(tok, lens), lens):
+        assert o.shape[0] == 3 * L
+        np.testing.assert_array_equal(o, e)
+    assert sum(calls) < len(lens)  # the all-empty buckets never reached the engine
+    out0 = ShardedSynthesis(synth, torch.device("cpu"), bucket=8).run(np.zeros((3, 4), np.int32),
+                                                                      np.zeros(3, np.int32))
+    assert all(o.shape == (0,) for o in out0)

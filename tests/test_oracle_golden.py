@@ -59,3 +59,26 @@ def test_speaker_embedding_oracle_matches_golden(tag):
     np.testing.assert_allclose(o["mel"], GS[f"{tag}_mel"], atol=1e-4, rtol=1e-4)
     o0 = acoustic_forward(GS[f"{tag}_ids"], w)  # no embedding: HF skips the projection
     np.testing.assert_allclose(o0["mel"], GS[f"{tag}_mel_nospk"], atol=1e-4, rtol=1e-4)
+
+
+def test_torch_cpu_restatement_matches_golden_and_numpy_oracle():
+    """oracle/torch_cpu.py (bench.py's timed CPU baseline) against the
+    transformers goldens and the NumPy oracle: vocoder batch, acoustic with forced and with
+    predicted durations."""
+    import torch
+    from oracle.torch_cpu import TorchAcoustic, TorchVocoder
+    vw, aw = make_vocoder_weights(seed=0), make_acoustic_weights(seed=0)
+    voc, ac = TorchVocoder(vw), TorchAcoustic(aw)
+    for tag in ("voc_a", "voc_b"):
+        wav = voc(torch.from_numpy(G[f"{tag}_mel"])[None])[0].numpy()
+        np.testing.assert_allclose(wav, G[f"{tag}_wav"], atol=1e-5, rtol=1e-4)
+    mel, dur = ac(torch.from_numpy(np.asarray(G["ac_a_ids"], np.int64))[None])
+    np.testing.assert_array_equal(dur[0].numpy(), G["ac_a_dur"])
+    np.testing.assert_allclose(mel[0].numpy(), G["ac_a_mel"], atol=1e-4, rtol=1e-4)
+    rng = np.random.default_rng(5)
+    ids = rng.integers(1, 78, size=(2, 9))
+    d = np.full((2, 9), 2)
+    mel, _ = ac(torch.from_numpy(ids), torch.from_numpy(d))
+    for b in range(2):
+        ref = acoustic_forward(ids[b], aw, durations=d[b])["mel"]
+        np.testing.assert_allclose(mel[b].numpy(), ref, atol=1e-4, rtol=1e-4)

@@ -157,3 +157,19 @@ def test_registered_voice_reaches_the_model_per_sentence():
         assert [[1.0, 2.0, 3.0, 4.0]] * 2 in model.voices  # both sentences carried the voice
         assert None in model.voices                        # unknown voice -> default voice
         assert c.get("/health").json()["voice_stats"]["total_voices"] == 1
+
+
+def test_bad_messages_do_not_end_the_connection():
+    """Valid JSON that is not an object, a non-numeric embedding and a non-string text are
+    logged and skipped; the connection keeps working (reference server.py:258-263)."""
+    app = create_app(lambda: FakeSpeakerModel())
+    with TestClient(app) as c:
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            ws.send_text("[1, 2, 3]")
+            ws.send_text("not json")
+            ws.send_text(json.dumps({"type": "synthesize", "text": 12}))
+            ws.send_text(json.dumps({"type": "register_voice", "voice_id": "v", "speaker_embedding": "abc"}))
+            assert ws.receive_json()["type"] == "error"
+            ws.send_text(json.dumps({"type": "synthesize", "text": "Still here."}))
+            frames, final = recv_until_complete(ws)
+            assert len(frames) == 1 and final == {"type": "synthesis_complete", "chunk_id": 1}

@@ -1,7 +1,8 @@
 """GPU parity of the HIP vocoder path (through the C-ABI) against the CPU oracle.
 
-Tolerances: fp32 atol 1e-5 / rtol 1e-4 on the waveform;
-fp16 rel-RMS <= 5e-3; bf16 rel-RMS <= 2.5e-2.
+Tolerances: fp32 atol 1e-5 / rtol 1e-4 on the waveform; 16-bit paths
+through tests/parity.py (relative RMS and max-abs error, printed and logged, bounded at
+about 2x the errors measured on MI355X).
 """
 import os
 
@@ -14,6 +15,7 @@ pytestmark = pytest.mark.gpu
 from gonova_tts_amd.engine import HipEngine, TtsConvDesc, conv1d_op  # noqa: E402
 from gonova_tts_amd.weights import make_vocoder_weights  # noqa: E402
 from oracle.vocoder import vocoder_forward, conv1d, conv_transpose1d, leaky_relu  # noqa: E402
+from parity import check  # noqa: E402
 
 G = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_v1.npz"))
 DEV = "cuda:0"
@@ -122,8 +124,8 @@ def test_vocoder_fp32_ragged_batch(vw):
         assert np.all(wav[b, L * 256:] == 0)
 
 
-@pytest.mark.parametrize("dtype,tol", [("f16", 5e-3), ("bf16", 2.5e-2)])
-def test_vocoder_low_precision_rel_rms(vw, dtype, tol):
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_vocoder_low_precision_rel_rms(vw, dtype):
     eng = engine_for(dtype, vw)
     rng = np.random.default_rng(11)
     lens = [64, 50]
@@ -131,13 +133,14 @@ def test_vocoder_low_precision_rel_rms(vw, dtype, tol):
     wav = eng.vocoder(torch.from_numpy(mel).to(DEV), torch.tensor(lens, dtype=torch.int32)).cpu().numpy()
     for b, L in enumerate(lens):
         ref = vocoder_forward(mel[b, :L], vw)
-        e = rel_rms(wav[b, :L * 256], ref)
-        assert e <= tol, (dtype, e)
+        check(f"vocoder {dtype} ragged b={b} ({L} frames)", wav[b, :L * 256], ref, kind="voc_" + dtype)
 
 
 def test_vocoder_full_size_batch_invariance(vw):
     """C2 shape (B=32, T=862, fp16): every utterance of the batch equals the same
-    utterance run alone, bit for bit (size-independent property), and is finite."""
+    utterance run alone, bit for bit (size-independent property), and is finite; a window
+    of the full-size output itself against the oracle (the vocoder is local: frames
+    [w0, w1) from mel frames [w0 - 16, w1 + 16) are exact)."""
     eng = engine_for("f16", vw)
     g = torch.Generator(device="cpu").manual_seed(0)
     mel = torch.randn((32, 862, 80), generator=g).to(DEV)
@@ -147,10 +150,9 @@ def test_vocoder_full_size_batch_invariance(vw):
     for b in (0, 17, 31):
         solo = eng.vocoder(mel[b:b + 1].contiguous())
         assert torch.equal(solo[0], wav[b])
-    # parity of a slice of the full-size run against the oracle (first utterance, first 2 s)
-    ref = vocoder_forward(mel[0, :200].cpu().numpy(), vw)
-    got = eng.vocoder(mel[0:1, :200].contiguous()).cpu().numpy()[0]
-    assert rel_rms(got, ref) <= 5e-3
+    w0, w1 = 100, 300
+    ref = vocoder_forward(mel[0, w0 - 16:w1 + 16].cpu().numpy(), vw)[16 * 256:(16 + w1 - w0) * 256]
+    check("C2 full-size f16 utt 0 frames 100-300", wav[0, w0 * 256:w1 * 256].cpu().numpy(), ref, kind="voc_f16")
 
 
 @pytest.mark.parametrize("pair", ["1", "0"], ids=["pair", "stage"])
@@ -261,7 +263,7 @@ def test_streaming_upsampler_matches_conv_path(vw, dtype, monkeypatch):
             assert rel_rms(st[b, :L * 256], cv[b, :L * 256]) <= tol, b
         assert np.all(st[b, L * 256:] == 0)
     ref = vocoder_forward(mel[3, :17].cpu().numpy(), vw)
-    assert rel_rms(st[3, :17 * 256], ref) <= (5e-3 if dtype == "f16" else 2.5e-2)
+    check(f"streaming upsampler {dtype} 17 frames", st[3, :17 * 256], ref, kind="voc_" + dtype)
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f16", "bf16"])
@@ -292,7 +294,7 @@ def test_long_utterance_matches_oracle_slice(vw):
     assert wav.shape == (T * 256,) and np.isfinite(wav).all()
     w0, w1, ctx = 1800, 1840, 16  # compare frames [w0, w1) computed from frames [w0-ctx, w1+ctx)
     ref = vocoder_forward(mel[0, w0 - ctx:w1 + ctx], vw)[ctx * 256:(ctx + w1 - w0) * 256]
-    assert rel_rms(wav[w0 * 256:w1 * 256], ref) <= 5e-3
+    check("long 2600-frame f16 frames 1800-1840", wav[w0 * 256:w1 * 256], ref, kind="voc_f16")
 
 
 def test_bad_arguments_raise_with_the_engine_message(vw):
@@ -306,3 +308,26 @@ def test_bad_arguments_raise_with_the_engine_message(vw):
     with pytest.raises(RuntimeError):
         eng.resample(torch.zeros((1, 8), device=DEV), torch.tensor([8], dtype=torch.int32), 0, 1)
     del ctypes
+
+
+def test_two_streams_share_one_engine(vw):
+    """Calls on two streams of one engine share its workspace; the engine orders a call on a
+    new stream after everything the previous call's stream enqueued (event edge), so results
+    equal single-stream runs bit for bit (advisor finding: cross-stream scratch race)."""
+    eng = engine_for("f16", vw)
+    rng = np.random.default_rng(41)
+    melA = torch.from_numpy(rng.standard_normal((4, 120, 80)).astype(np.float32)).to(DEV)
+    melB = torch.from_numpy(rng.standard_normal((3, 90, 80)).astype(np.float32)).to(DEV)
+    refA, refB = eng.vocoder(melA).clone(), eng.vocoder(melB).clone()
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for _ in range(3):
+        with torch.cuda.stream(s1):
+            a = eng.vocoder(melA, stream=s1)
+        with torch.cuda.stream(s2):
+            b = eng.vocoder(melB, stream=s2)
+        outs.append((a, b))
+    torch.cuda.synchronize()
+    for a, b in outs:
+        assert torch.equal(a, refA) and torch.equal(b, refB)

@@ -311,8 +311,18 @@ def bench_full(ctx, args, steps, warmup):
     el_ac, _ = ctx.timed(lambda: eng.acoustic(tok, tl, T), steps, 1)
     ac_ms = el_ac * 1e3 / steps
     eng.close()
+    # the same acoustic pass with encoder_precision="fast" (whole model bf16; durations may round
+    # differently near .5), to show what the default exact-duration encoder costs
+    engf = HipEngine(ctx.local, vocoder_dtype="bf16", acoustic_dtype="bf16", max_batch=B, max_frames=T, max_tokens=N,
+                     encoder_precision="fast")
+    engf.load_weights(acoustic=make_acoustic_weights(seed=0, fixed_duration=dur))
+    el_f, _ = ctx.timed(lambda: engf.acoustic(tok, tl, T), steps, 1)
+    engf.close()
     return {"value": round(value, 1), "unit": "samples/s", "ms_per_step": round(el * 1e3 / steps, 3),
-            "acoustic_ms_per_step": round(ac_ms, 3), "per_gpu_samples_per_s": round(value / ctx.world, 1),
+            "acoustic_ms_per_step": round(ac_ms, 3),
+            "acoustic_ms_per_step_fast_encoder": round(el_f * 1e3 / steps, 3),
+            "encoder_precision": "exact (fp32 encoder + variance predictors, GEMMs as 3 f16 MFMAs)",
+            "per_gpu_samples_per_s": round(value / ctx.world, 1),
             "x_realtime_per_gpu": round(value / ctx.world / SR, 2), "dtype": "bf16",
             "config": {"workload": "C3 full pipeline (tokens -> FS2-Conformer -> HiFi-GAN), "
                                    f"batch-{B} x {N} tokens x {dur} frames = {T} frames (10.03 s)"},
@@ -358,11 +368,12 @@ def bench_c4(ctx, args, steps, warmup):
                        "global_batch": B, "parallelism": f"utterance-sharded dp{ctx.world}"}}
 
 
-def bench_streaming(ctx, trials=50, B=8, N=144, chunk=32):
+def bench_streaming(ctx, trials=50, B=8, N=144, chunk=32, encoder_precision="exact"):
     """Config C5: batch-8 streaming; latency from host tokens to the first audio chunk on host."""
     torch = ctx.torch
     from gonova_tts_amd.model import GonovaTTS
-    m = GonovaTTS.from_pretrained(ctx.dev.index, vocoder_dtype="bf16", acoustic_dtype="bf16")
+    m = GonovaTTS.from_pretrained(ctx.dev.index, vocoder_dtype="bf16", acoustic_dtype="bf16",
+                                  encoder_precision=encoder_precision)
     rng = np.random.default_rng(5)
     tok = rng.integers(1, 78, size=(B, N)).astype(np.int32)
     lens = np.full(B, N, np.int32)
@@ -381,6 +392,7 @@ def bench_streaming(ctx, trials=50, B=8, N=144, chunk=32):
     m.engine.close()
     return {"p50_first_audio_ms": round(float(np.percentile(lat, 50)), 3),
             "p90_first_audio_ms": round(float(np.percentile(lat, 90)), 3), "trials": trials,
+            "encoder_precision": encoder_precision,
             "config": f"C5 batch-{B} x {N} tokens x 6 frames, chunk {chunk} frames (~{chunk * 256 / SR * 1e3:.0f} ms) "
                       f"+ 16 frames context, bf16"}
 
@@ -432,6 +444,8 @@ def main():
             out["c4"] = bench_c4(ctx, args, steps=max(2, args.steps // 3), warmup=1)
         if not args.no_streaming and ctx.rank == 0:
             out["streaming"] = bench_streaming(ctx)
+            fast = bench_streaming(ctx, encoder_precision="fast")
+            out["streaming"]["fast_encoder"] = {k: fast[k] for k in ("p50_first_audio_ms", "p90_first_audio_ms")}
     else:
         f = bench_full(ctx, args, args.steps, args.warmup)
         per_gpu = f["value"] / ctx.world

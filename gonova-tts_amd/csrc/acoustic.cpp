@@ -41,6 +41,7 @@ struct LNParam {
 };
 
 struct ConformerLayer {
+  int dt = DT_F32;  // activation dtype of this layer
   ConvLayer ffm1, ffm2, ff1, ff2, qkv, out, pw1, pw2, pos;
   float* pos_u = nullptr;
   float* pos_v = nullptr;
@@ -52,6 +53,7 @@ struct ConformerLayer {
 };
 
 struct Predictor {
+  int dt = DT_F32;
   std::vector<ConvLayer> convs;
   std::vector<LNParam> lns;
   float* lin_w = nullptr;
@@ -61,7 +63,12 @@ struct Predictor {
 }  // namespace
 
 struct AcousticModel::Impl {
-  int dt = DT_F32;
+  int dt = DT_F32;   // decoder / postnet activations
+  int dte = DT_F32;  // encoder, speaker projection, variance adaptor (fp32 + split GEMMs when dt is 16-bit)
+  int bdt = DT_F32;  // dtype of the layers being built (finalize)
+  // fp32 layers of a 16-bit model get split-packed weights (three f16 MFMAs, conv_split.hip)
+  bool split_now() const { return bdt == DT_F32 && dt != DT_F32; }
+  size_t esz() const { return std::max(dtype_size(dt), dtype_size(dte)); }
   Profiler* prof = nullptr;
   int D = 384, H = 2, V = 78, NMEL = 80, FFN = 1536, PRED = 256;
   float eps = 1e-5f;
@@ -112,8 +119,9 @@ struct AcousticModel::Impl {
     std::vector<float> bias;
     if (bias_override) bias = *bias_override;
     else if (!b.empty() && get(b)) bias = *get(b);
-    if (s.size() == 3) return make_conv(need(get, w), (int)s[0], (int)s[1], (int)s[2], bias, 1, pad, dt, allocs, scale);
-    if (s.size() == 2) return make_conv(need(get, w), (int)s[0], (int)s[1], 1, bias, 1, 0, dt, allocs, scale);
+    if (s.size() == 3)
+      return make_conv(need(get, w), (int)s[0], (int)s[1], (int)s[2], bias, 1, pad, bdt, allocs, scale, split_now());
+    if (s.size() == 2) return make_conv(need(get, w), (int)s[0], (int)s[1], 1, bias, 1, 0, bdt, allocs, scale, split_now());
     throw TtsError(TTS_ERR_INVALID, "bad weight rank: " + w);
   }
 
@@ -126,6 +134,7 @@ struct AcousticModel::Impl {
 
   ConformerLayer layer(const GetData& get, const GetShape& shape, const std::string& p) {
     ConformerLayer L;
+    L.dt = bdt;
     const int kf = (int)shape(p + "feed_forward.conv1.weight").at(2);
     L.ffm1 = conv(get, shape, p + "feed_forward_macaron.conv1.weight", p + "feed_forward_macaron.conv1.bias", (kf - 1) / 2);
     L.ffm2 = conv(get, shape, p + "feed_forward_macaron.conv2.weight", p + "feed_forward_macaron.conv2.bias", (kf - 1) / 2);
@@ -140,9 +149,9 @@ struct AcousticModel::Impl {
       wq.insert(wq.end(), w.begin(), w.end());
       bq.insert(bq.end(), b.begin(), b.end());
     }
-    L.qkv = make_conv(wq, 3 * D, D, 1, bq, 1, 0, dt, allocs);
+    L.qkv = make_conv(wq, 3 * D, D, 1, bq, 1, 0, bdt, allocs, nullptr, split_now());
     L.out = conv(get, shape, a + "linear_out.weight", a + "linear_out.bias", 0);
-    L.pos = make_conv(need(get, a + "linear_pos.weight"), D, D, 1, {}, 1, 0, dt, allocs);
+    L.pos = make_conv(need(get, a + "linear_pos.weight"), D, D, 1, {}, 1, 0, bdt, allocs, nullptr, split_now());
     L.pos_u = upf(need(get, a + "pos_bias_u"));
     L.pos_v = upf(need(get, a + "pos_bias_v"));
     const std::string c = p + "conv_module.";
@@ -175,6 +184,7 @@ struct AcousticModel::Impl {
 
   Predictor predictor(const GetData& get, const GetShape& shape, const std::string& p) {
     Predictor P;
+    P.dt = bdt;
     for (int i = 0;; ++i) {
       const std::string q = p + "conv_layers." + std::to_string(i) + ".";
       if (!get(q + "conv.weight")) break;
@@ -201,20 +211,21 @@ struct AcousticModel::Impl {
         pe[(size_t)q * D + 2 * i + 1] = (float)std::cos(ang);
       }
     }
-    void* ped = upload(pe, dt);
+    void* ped[3] = {nullptr, nullptr, nullptr};  // the table in each layer dtype used
     for (auto* stack : {&enc, &dec})
       for (auto& L : *stack) {
         if (L.ptab) {
           hipFree(L.ptab);
           for (auto& a : allocs) if (a == L.ptab) a = nullptr;
         }
+        if (!ped[L.dt]) ped[L.dt] = upload(pe, L.dt);
         void* t = nullptr;
-        HIP_CHECK(hipMalloc(&t, (size_t)rows * D * dtype_size(dt)));
+        HIP_CHECK(hipMalloc(&t, (size_t)rows * D * dtype_size(L.dt)));
         L.ptab = track(t);
-        run_layer(L.pos, ped, rows, nullptr, L.ptab, rows, 1, dt, s, nullptr);
+        run_layer(L.pos, ped[L.dt], rows, nullptr, L.ptab, rows, 1, L.dt, s, nullptr);
       }
     HIP_CHECK(hipStreamSynchronize(s));
-    hipFree(ped);
+    for (void* p : ped) if (p) hipFree(p);
     rmax = new_rmax;
   }
 
@@ -255,7 +266,7 @@ struct AcousticModel::Impl {
     if (B <= cap_sB && Tm <= cap_sTm) return;
     B = std::max(B, cap_sB); Tm = std::max(Tm, cap_sTm);
     drop_scores();
-    const size_t e = dtype_size(dt);
+    const size_t e = esz();
     const int Sk = rup(Tm, 16), Sac = rup(Tm, 16), Sbd = rup(2 * Tm, 16);
     auto al = [&](size_t n) { void* p = alloc_ws(n, e); ws.pop_back(); score_ws.push_back(p); return p; };
     AC = al((size_t)B * H * Tm * Sac);
@@ -277,7 +288,7 @@ struct AcousticModel::Impl {
   }
 
   void reserve_fresh(int B, int N, int T) {
-    const size_t e = dtype_size(dt);
+    const size_t e = esz();
     const int Tm = std::max(N, T);
     const int Tp = rup(Tm, 32);
     const int dk = D / H;
@@ -301,12 +312,12 @@ struct AcousticModel::Impl {
   }
 
   // ---------------------------------------------------------------- forward
-  void ln_rows(const void* in, void* out, int rows, int C, const LNParam& a, const LNParam* b, hipStream_t s) {
-    HIP_CHECK(launch_layernorm(dt, in, out, rows, C, a.g, a.b, b ? b->g : nullptr, b ? b->b : nullptr, eps, s));
+  void ln_rows(int d, const void* in, void* out, int rows, int C, const LNParam& a, const LNParam* b, hipStream_t s) {
+    HIP_CHECK(launch_layernorm(d, in, out, rows, C, a.g, a.b, b ? b->g : nullptr, b ? b->b : nullptr, eps, s));
   }
 
   // one head-batched attention GEMM: Y[b,h][n][m] = sum_c X[b,h][n][c] * W[b,h][m][c]
-  void attn_gemm(const void* x, long long sxb, long long sxh, int sxr, const int* lens, int x_rows, const void* w,
+  void attn_gemm(int d, const void* x, long long sxb, long long sxh, int sxr, const int* lens, int x_rows, const void* w,
                  long long swb, long long swh, int w_ld, int M, int K, void* y, long long syb, long long syh,
                  int syr, int B, hipStream_t s) {
     ConvParams p = conv_params_default();
@@ -316,7 +327,7 @@ struct AcousticModel::Impl {
     p.y_len = lens; p.y_rows = x_rows;
     p.M = M; p.Cin = K; p.taps = 1; p.dil = 1; p.pad = 0;
     p.B = B; p.nh = H;
-    launch_conv_checked(p, dt, s, prof, 2.0 * M * (double)K * x_rows * B * H);
+    launch_conv_checked(p, d, s, prof, 2.0 * M * (double)K * x_rows * B * H);
   }
 
   void stack(std::vector<ConformerLayer>& layers, void* Xb, const int* lens, int B, int Tm, hipStream_t s) {
@@ -327,10 +338,11 @@ struct AcousticModel::Impl {
     const int Mk = rup(Tm, 4), Mbd = rup(2 * Tm - 1, 4);
     const float scale = 1.0f / std::sqrt((float)dk);
     for (auto& L : layers) {
+      const int dt = L.dt;
       // macaron FFN: x = LN(x + 0.5 * ffn(x))
       run_layer(L.ffm1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
       run_layer(L.ffm2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
-      ln_rows(Y, Xb, rows, D, L.ln_mac, nullptr, s);
+      ln_rows(dt, Y, Xb, rows, D, L.ln_mac, nullptr, s);
       // relative-position MHSA: x = LN(x + mhsa(x))
       run_layer(L.qkv, Xb, Tp, lens, QKV, Tp, B, dt, s, prof);
       const bool fused_attn = rel_attn_enabled() && rel_attn_supported(dt, D, H);
@@ -340,47 +352,49 @@ struct AcousticModel::Impl {
         // fused flash-style relative-position attention (attention.hip); Qu / Qv formed in it
         HIP_CHECK(launch_rel_attn(dt, L.pos_u, L.pos_v, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale, O, s));
         run_layer(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
-        ln_rows(Y, Xb, rows, D, L.ln_att, nullptr, s);
+        ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s);
         conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
         continue;
       }
       const size_t e = dtype_size(dt);
       // AC[b,h][i][j] = Qu[b][i][h] . K[b][j][h]
-      attn_gemm(Qu, (long long)Tp * D, dk, D, lens, Tm, (const char*)QKV + (size_t)D * e, (long long)Tp * 3 * D, dk,
+      attn_gemm(dt, Qu, (long long)Tp * D, dk, D, lens, Tm, (const char*)QKV + (size_t)D * e, (long long)Tp * 3 * D, dk,
                 3 * D, Mk, dk, AC, (long long)H * Tm * Sac, (long long)Tm * Sac, Sac, B, s);
       // BD[b,h][i][q] = Qv[b][i][h] . Ptab[rmax - Tm + q][h]   (q <-> rel = Tm-1-q)
-      attn_gemm(Qv, (long long)Tp * D, dk, D, lens, Tm, (const char*)L.ptab + (size_t)(rmax - Tm) * D * e, 0, dk, D,
+      attn_gemm(dt, Qv, (long long)Tp * D, dk, D, lens, Tm, (const char*)L.ptab + (size_t)(rmax - Tm) * D * e, 0, dk, D,
                 Mbd, dk, BD, (long long)H * Tm * Sbd, (long long)Tm * Sbd, Sbd, B, s);
       HIP_CHECK(launch_rel_softmax(dt, AC, BD, lens, B, H, Tm, Sac, Sbd, Sk, scale, P, s));
       // O[b][i][h*dk + d] = sum_j P[b,h][i][j] * Vt[b,h][d][j]
-      attn_gemm(P, (long long)H * Tm * Sk, (long long)Tm * Sk, Sk, lens, Tm, Vt, (long long)H * dk * Sk,
+      attn_gemm(dt, P, (long long)H * Tm * Sk, (long long)Tm * Sk, Sk, lens, Tm, Vt, (long long)H * dk * Sk,
                 (long long)dk * Sk, Sk, dk, Sk, O, (long long)Tp * D, dk, D, B, s);
       run_layer(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
-      ln_rows(Y, Xb, rows, D, L.ln_att, nullptr, s);
+      ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s);
       conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
     }
   }
 
   void conv_module_and_ffn(ConformerLayer& L, void* Xb, const int* lens, int B, int Tp, int rows, hipStream_t s) {
+    const int dt = L.dt;
     // conv module: x = LN(x + pw2(silu(bn(dw(glu(pw1(x)))))))
     run_layer(L.pw1, Xb, Tp, lens, A, Tp, B, dt, s, prof);
     HIP_CHECK(launch_glu_dwconv(dt, A, lens, B, Tp, D, L.dw_w, L.dw_k, L.dw_b, G, s));
     run_layer(L.pw2, G, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
-    ln_rows(Y, Xb, rows, D, L.ln_conv, nullptr, s);
+    ln_rows(dt, Y, Xb, rows, D, L.ln_conv, nullptr, s);
     // FFN: x = final_LN(LN(x + 0.5 * ffn(x)))
     run_layer(L.ff1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
     run_layer(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
-    ln_rows(Y, Xb, rows, D, L.ln_ff, &L.ln_final, s);
+    ln_rows(dt, Y, Xb, rows, D, L.ln_ff, &L.ln_final, s);
   }
 
   void predict(Predictor& Pr, const void* x, const int* lens, int B, int Np, float* out, hipStream_t s) {
+    const int dt = Pr.dt;
     const void* h = x;
     void* bufs[2] = {PB1, PB2};
     const int n = (int)Pr.convs.size();
     for (int i = 0; i < n; ++i) {
       void* o = bufs[i & 1];
       run_layer(Pr.convs[i], h, Np, lens, o, Np, B, dt, s, prof, 1.f, ACT_RELU);
-      if (i + 1 < n) ln_rows(o, o, B * Np, PRED, Pr.lns[i], nullptr, s);
+      if (i + 1 < n) ln_rows(dt, o, o, B * Np, PRED, Pr.lns[i], nullptr, s);
       else HIP_CHECK(launch_ln_linear1(dt, o, B * Np, PRED, Pr.lns[i].g, Pr.lns[i].b, eps, Pr.lin_w, Pr.lin_b, out, s));
       h = o;
     }
@@ -390,15 +404,20 @@ struct AcousticModel::Impl {
                int* mel_lens, int Tcap, int* durations, const float* spk, hipStream_t s) {
     reserve(B, N, Tcap);
     const int Tm = std::max(N, Tcap);
-    if (!(rel_attn_enabled() && rel_attn_supported(dt, D, H))) reserve_scores(B, Tm);
+    {  // the unfused attention's score buffers, for the stacks that run it (fp32 / TTS_REL_ATTN=0)
+      const bool fused = rel_attn_enabled();
+      const int need = std::max(fused && rel_attn_supported(dte, D, H) ? 0 : N,
+                                fused && rel_attn_supported(dt, D, H) ? 0 : Tcap);
+      if (need) reserve_scores(B, need);
+    }
     if (Tm > rmax) build_ptabs(rup(Tm, 256), s);
     const float xscale = std::sqrt((float)D);
     const int Np = rup(N, 32), Tp = rup(Tcap, 32);
     // encoder
-    HIP_CHECK(launch_embed(dt, tokens, tok_lens, B, N, Np, embed, V, D, xscale, ENC, s));
+    HIP_CHECK(launch_embed(dte, tokens, tok_lens, B, N, Np, embed, V, D, xscale, ENC, s));
     stack(enc, ENC, tok_lens, B, N, s);
     if (spk && E) {  // speaker embedding (HF:1192-1196); without one HF skips the projection
-      HIP_CHECK(launch_spk_bias(dt, spk, B, E, proj_we, proj_b, D, SPK, s));
+      HIP_CHECK(launch_spk_bias(dte, spk, B, E, proj_we, proj_b, D, SPK, s));
       ConvParams p = conv_params_default();
       p.x = ENC; p.sxb = (long long)Np * D; p.sxr = D; p.x_len = tok_lens; p.x_rows = Np;
       p.w = proj_h.w; p.w_ld = D; p.bias = nullptr; p.wpk = proj_h.wpk;
@@ -406,8 +425,8 @@ struct AcousticModel::Impl {
       p.r1 = SPK; p.srb = D; p.srr = 0;  // the utterance's term broadcast over its frames
       p.y_len = tok_lens; p.y_rows = Np;
       p.M = D; p.Cin = D; p.B = B;
-      launch_conv_checked(p, dt, s, prof, 2.0 * D * (double)D * B * Np);
-      HIP_CHECK(hipMemcpyAsync(ENC, Y, (size_t)B * Np * D * dtype_size(dt), hipMemcpyDeviceToDevice, s));
+      launch_conv_checked(p, dte, s, prof, 2.0 * D * (double)D * B * Np);
+      HIP_CHECK(hipMemcpyAsync(ENC, Y, (size_t)B * Np * D * dtype_size(dte), hipMemcpyDeviceToDevice, s));
     }
     // variance adaptor (HF:1198-1218)
     predict(pitch, ENC, tok_lens, B, Np, f_pitch, s);
@@ -416,13 +435,13 @@ struct AcousticModel::Impl {
     // logd is laid out [B][Np]; durations kernel reads [B][N] rows -> compact view via stride Np
     int* dur = durations ? durations : i_dur;
     HIP_CHECK(launch_durations_strided(s, B, N, Np, tok_lens, dur_override, Tcap, dur, mel_lens));
-    HIP_CHECK(launch_var_embed_add(dt, ENC, B * Np, D, f_energy, ee_w, ee_b, f_pitch, pe_w, pe_b, s));
+    HIP_CHECK(launch_var_embed_add(dte, ENC, B * Np, D, f_energy, ee_w, ee_b, f_pitch, pe_w, pe_b, s));
     // decoder rows are laid out with stride Tp; regulate writes [B][Tcap] rows
     void* Xd = X;
     if (Tp == Tcap) {
-      HIP_CHECK(launch_regulate(dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, X, s));
+      HIP_CHECK(launch_regulate(dte, dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, X, s));
     } else {
-      HIP_CHECK(launch_regulate(dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, Y, s));
+      HIP_CHECK(launch_regulate(dte, dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, Y, s));
       HIP_CHECK(hipMemcpy2DAsync(X, (size_t)Tp * D * dtype_size(dt), Y, (size_t)Tcap * D * dtype_size(dt),
                                  (size_t)Tcap * D * dtype_size(dt), B, hipMemcpyDeviceToDevice, s));
     }
@@ -462,13 +481,15 @@ struct AcousticModel::Impl {
   }
 };
 
-void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtype, Profiler* prof) {
+void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtype, int enc_dtype, Profiler* prof) {
   if (!get("encoder.embed.weight")) {
     loaded = false;
     return;
   }
   std::unique_ptr<Impl> m(new Impl());
   m->dt = dtype;
+  m->dte = enc_dtype == DT_F32 ? DT_F32 : dtype;
+  m->bdt = m->dte;
   m->prof = prof;
   const auto es = shape("encoder.embed.weight");
   m->V = (int)es.at(0);
@@ -478,11 +499,10 @@ void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtyp
   m->PRED = (int)shape("duration_predictor.conv_layers.0.conv.weight").at(0);
   m->NMEL = (int)shape("speech_decoder_postnet.feat_out.weight").at(0);
   if (m->D % 64 || m->D > 512 || (m->D / m->H) % 16) throw TtsError(TTS_ERR_INVALID, "unsupported hidden size");
-  m->embed = m->track(upload(*get("encoder.embed.weight"), dtype));
+  // encoder side (bdt = dte): embedding, encoder layers, speaker projection, variance predictors
+  m->embed = m->track(upload(*get("encoder.embed.weight"), m->dte));
   for (int i = 0; get("encoder.conformer_layers." + std::to_string(i) + ".self_attn.pos_bias_u"); ++i)
     m->enc.push_back(m->layer(get, shape, "encoder.conformer_layers." + std::to_string(i) + "."));
-  for (int i = 0; get("decoder.conformer_layers." + std::to_string(i) + ".self_attn.pos_bias_u"); ++i)
-    m->dec.push_back(m->layer(get, shape, "decoder.conformer_layers." + std::to_string(i) + "."));
   m->pitch = m->predictor(get, shape, "pitch_predictor.");
   m->energy = m->predictor(get, shape, "energy_predictor.");
   m->duration = m->predictor(get, shape, "duration_predictor.");
@@ -497,7 +517,7 @@ void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtyp
       for (int i = 0; i < m->D; ++i) wh[(size_t)o * m->D + i] = pw[(size_t)o * din + i];
       for (int i = 0; i < m->E; ++i) we[(size_t)o * m->E + i] = pw[(size_t)o * din + m->D + i];
     }
-    m->proj_h = make_conv(wh, m->D, m->D, 1, {}, 1, 0, dtype, m->allocs);
+    m->proj_h = make_conv(wh, m->D, m->D, 1, {}, 1, 0, m->dte, m->allocs, nullptr, m->split_now());
     m->proj_we = m->upf(we);
     m->proj_b = m->upf(m->need(get, "projection.bias"));
   }
@@ -505,6 +525,10 @@ void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtyp
   m->pe_b = m->upf(m->need(get, "pitch_embed.conv.bias"));
   m->ee_w = m->upf(m->need(get, "energy_embed.conv.weight"));
   m->ee_b = m->upf(m->need(get, "energy_embed.conv.bias"));
+  // decoder side (bdt = dt): decoder layers, postnet
+  m->bdt = dtype;
+  for (int i = 0; get("decoder.conformer_layers." + std::to_string(i) + ".self_attn.pos_bias_u"); ++i)
+    m->dec.push_back(m->layer(get, shape, "decoder.conformer_layers." + std::to_string(i) + "."));
   m->feat_out = m->conv(get, shape, "speech_decoder_postnet.feat_out.weight", "speech_decoder_postnet.feat_out.bias", 0);
   for (int i = 0;; ++i) {
     const std::string p = "speech_decoder_postnet.layers." + std::to_string(i) + ".";

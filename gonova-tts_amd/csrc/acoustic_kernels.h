@@ -22,8 +22,9 @@ hipError_t launch_durations(const float* logd, const int* lens, int B, int N, co
                             int Tcap, int* dur, int* mel_lens, int* tokmap, hipStream_t s);
 hipError_t launch_var_embed_add(int dt, void* x, int rows, int D, const float* e, const float* we, const float* be,
                                 const float* p, const float* wp, const float* bp, hipStream_t s);
-hipError_t launch_regulate(int dt, const void* enc, int B, int N, int D, const int* tokmap, int Tcap, float scale,
-                           void* out, hipStream_t s);
+// enc in dt_in (dt or fp32), out in dt
+hipError_t launch_regulate(int dt_in, int dt, const void* enc, int B, int N, int D, const int* tokmap, int Tcap,
+                           float scale, void* out, hipStream_t s);
 hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, int Tcap, int C, float* out,
                           hipStream_t s);
 

@@ -457,9 +457,10 @@ __global__ void var_embed_add_kernel(T* __restrict__ x, int rows, int D, const f
   }
 }
 
-// length regulator gather (HF:82-126) fused with the decoder's input_scale (HF:763)
-template <typename T>
-__global__ void regulate_kernel(const T* __restrict__ enc, int N, int D, const int* __restrict__ tokmap, int Tcap,
+// length regulator gather (HF:82-126) fused with the decoder's input_scale (HF:763); the encoder
+// side may be fp32 (TTS_ENCODER_EXACT) while the decoder runs 16-bit: one rounding, after the scale
+template <typename T, typename TI = T>
+__global__ void regulate_kernel(const TI* __restrict__ enc, int N, int D, const int* __restrict__ tokmap, int Tcap,
                                 float scale, T* __restrict__ out) {
   const int b = blockIdx.y;
   const int f = blockIdx.x;
@@ -469,7 +470,7 @@ __global__ void regulate_kernel(const T* __restrict__ enc, int N, int D, const i
     for (int c = threadIdx.x; c < D; c += blockDim.x) o[c] = from_f32<T>(0.f);
     return;
   }
-  const T* s = enc + ((long long)b * N + tok) * D;
+  const TI* s = enc + ((long long)b * N + tok) * D;
   for (int c = threadIdx.x; c < D; c += blockDim.x) o[c] = from_f32<T>(to_f32(s[c]) * scale);
 }
 
@@ -651,8 +652,13 @@ hipError_t launch_var_embed_add(int dt, void* x, int rows, int D, const float* e
                                       (TT*)x, rows, D, e, we, be, p, wp, bp));
 }
 
-hipError_t launch_regulate(int dt, const void* enc, int B, int N, int D, const int* tokmap, int Tcap, float scale,
-                           void* out, hipStream_t s) {
+hipError_t launch_regulate(int dt_in, int dt, const void* enc, int B, int N, int D, const int* tokmap, int Tcap,
+                           float scale, void* out, hipStream_t s) {
+  if (dt_in == DT_F32 && dt != DT_F32) {
+    TTS_DISPATCH(dt, hipLaunchKernelGGL((regulate_kernel<TT, float>), dim3(Tcap, B), dim3(128), 0, s,
+                                        (const float*)enc, N, D, tokmap, Tcap, scale, (TT*)out));
+  }
+  if (dt_in != dt) return hipErrorInvalidValue;
   TTS_DISPATCH(dt, hipLaunchKernelGGL(regulate_kernel<TT>, dim3(Tcap, B), dim3(128), 0, s, (const TT*)enc, N, D,
                                       tokmap, Tcap, scale, (TT*)out));
 }

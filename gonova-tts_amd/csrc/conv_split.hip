@@ -1,0 +1,291 @@
+// fp32 implicit-GEMM conv computed as three f16 MFMAs ("split precision"), gfx950.
+//
+// gfx950 has no xf32 and its native fp32 MFMA (v_mfma_f32_32x32x2_f32) peaks at 1/16 of the
+// 16-bit rate.  An fp32 value a is split into two f16 terms,
+//     a_hi = f16(a),   a_lo = f16((a - a_hi) * 2^11)        (a ~= a_hi + a_lo * 2^-11),
+// a_hi carrying the top 11 significand bits and a_lo the next 11, and
+//     sum a*b ~= sum a_hi*b_hi  +  2^-11 * sum (a_hi*b_lo + a_lo*b_hi)
+// runs as three v_mfma_f32_32x32x16_f16 into two fp32 accumulators (the dropped a_lo*b_lo term
+// and the two representation errors are ~2^-21 relative per product: ~8x the fp32 rounding of
+// one product, 1000x below bf16).  Effective fp32 throughput is 1/3 of the f16 peak: ~5x the
+// native fp32 MFMA.  Range: |a| < 65504 (f16); the acoustic encoder's activations are O(100).
+//
+// Used for the acoustic encoder + variance predictors in "exact" encoder precision (the
+// integer durations of HF:181-183 then match the fp32 oracle, SURVEY.md §8c "durations: exact
+// integer match"; the decoder and postnet stay 16-bit).
+//
+// Layout: X fp32 [B][rows][Cin] channels-last; weights packed by frag_pack_split (runtime.h):
+// two planes of f16 fragments [M/32][taps][Cin/16][64 lanes][8] (hi, then lo * 2^11), so a
+// wave's A fragment is one contiguous 1 KiB read.  Block: 4 waves along M (128 output
+// channels), NT 32-row MFMA tiles along time.  A channel group CG of the block's X rows (every
+// tap's halo included) is split once into two LDS planes (row stride CG*2+16 bytes: an odd
+// number of 16-byte slots, conflict-free ds_read_b128 over 32 consecutive rows); the weight
+// quads (4 k-steps, hi + lo = 8 fragments) stream through a 2-deep register ring over a
+// bounds-checked buffer descriptor (a load past the group's last quad fetches nothing, so the
+// ring reloads unconditionally).  The epilogue is conv_gemm's (bias, alpha, activation,
+// residuals, scale; fp32 rows).
+#include "common.h"
+#include "conv_epilogue.h"
+#include "kernels.h"
+
+#include <cstdlib>
+
+namespace tts {
+
+constexpr float SPLIT_SCALE = 2048.f;  // 2^11: a_lo is stored scaled into f16's normal range
+constexpr int SPLIT_SU = 4;            // X staging loads (x2) in flight per thread
+
+// 8 fp32 -> (hi, lo) f16 x 8
+__device__ inline void split8(f32x4 a, f32x4 b, uint4& hi, uint4& lo) {
+  const half4 ha = __builtin_convertvector(a, half4), hb = __builtin_convertvector(b, half4);
+  const f32x4 ra = (a - __builtin_convertvector(ha, f32x4)) * SPLIT_SCALE;
+  const f32x4 rb = (b - __builtin_convertvector(hb, f32x4)) * SPLIT_SCALE;
+  const half4 la = __builtin_convertvector(ra, half4), lb = __builtin_convertvector(rb, half4);
+  const uint2 h0 = __builtin_bit_cast(uint2, ha), h1 = __builtin_bit_cast(uint2, hb);
+  const uint2 l0 = __builtin_bit_cast(uint2, la), l1 = __builtin_bit_cast(uint2, lb);
+  hi = uint4{h0.x, h0.y, h1.x, h1.y};
+  lo = uint4{l0.x, l0.y, l1.x, l1.y};
+}
+
+template <int NT, int UW>
+__global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG) {
+  typedef half8 Frag;
+  constexpr int WM = 4 / UW;  // waves along M; UW waves along utterances (same weights)
+  constexpr int BN = 32 * NT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  // XCD-aware order (cdna_hip_programming.md T1): blocks are dealt round-robin over the 8 XCDs,
+  // so work item w = (M block, utterance group, row tile), M block slowest, is given to block
+  // ids such that each XCD runs one contiguous range of w -- one or two M blocks.
+  const int ntx = (p.y_rows + BN - 1) / BN;
+  const int nbz = (p.B + UW - 1) / UW;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xq = nwg / 8, xr = nwg % 8, xcd = orig % 8;
+  const int w = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + orig / 8;
+  const int tx = w % ntx;
+  const int bz = (w / ntx) % nbz;
+  const int by = w / (ntx * nbz);
+  const int n0 = tx * BN;
+  auto ylen_of = [&](int bb) { return bb < p.B ? (p.y_len ? min(p.y_len[bb], p.y_rows) : p.y_rows) : 0; };
+  auto xlen_of = [&](int bb) { return bb < p.B ? (p.x_len ? min(p.x_len[bb], p.x_rows) : p.x_rows) : 0; };
+  {
+    int ymax = 0;
+#pragma unroll
+    for (int u = 0; u < UW; ++u) ymax = max(ymax, ylen_of(bz * UW + u));
+    if (n0 >= ymax) return;  // uniform over the block
+  }
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wu = wave / WM;
+  const int b = bz * UW + wu;  // this wave's utterance (>= B: computed, never stored)
+  const int l31 = lane & 31;
+  const int hh = lane >> 5;
+
+  const int KST = p.Cin / 16;
+  const int MB = (p.M + 31) / 32;
+  const int mb = min(by * WM + wm, MB - 1);  // a wave past M recomputes the last block (not stored)
+  const int wbytes = __builtin_amdgcn_readfirstlane(p.taps * KST * 1024);
+  const char* whi = reinterpret_cast<const char*>(p.wpk) + (long long)mb * wbytes;
+  const char* wlo = whi + (long long)MB * wbytes;
+  const auto rs_hi = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(whi), 0, wbytes, 0x00020000);
+  const auto rs_lo = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wlo), 0, wbytes, 0x00020000);
+  const int lofs = lane * 16;
+
+  const int R = BN + (p.taps - 1) * p.dil;  // staged rows per utterance
+  const int RU = UW * R;
+  const int RS = CG * 2 + 16;
+  const int PL = RU * RS;                // bytes per LDS plane
+  const int KS = CG / 16;                // k-steps per tap and group
+  const int lks = __builtin_ctz(KS);
+  const int QT = p.taps * KS / 4;        // weight quads per group (even: CG >= 128)
+  const int x_start = n0 - p.pad;
+  const char* xl = smem + (wu * R + l31) * RS + hh * 16;
+
+  f32x16 acc[NT], accx[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) { acc[j] = f32x16{}; accx[j] = f32x16{}; }
+
+  // staging: thread owns 8-channel column cc of the group and staged rows r0, r0 + rstep, ...
+  // (staged row rr = utterance u * R + local row), SPLIT_SU loads in flight per batch
+  const int VPR = CG / 8;
+  const int lvpr = __builtin_ctz(VPR);
+  const int cc = tid & (VPR - 1);
+  const int r0 = tid >> lvpr;
+  const int rstep = 256 >> lvpr;
+  auto stage = [&](int g) {
+    for (int rb = r0; rb < RU; rb += SPLIT_SU * rstep) {
+      f32x4 xa[SPLIT_SU], xb[SPLIT_SU];
+      bool ok[SPLIT_SU];
+#pragma unroll
+      for (int i = 0; i < SPLIT_SU; ++i) {  // unconditional, clamped addresses (masked below)
+        const int rr = min(rb + i * rstep, RU - 1);
+        const int u = rr / R;
+        const int bu = min(bz * UW + u, p.B - 1);
+        const int xl_ = xlen_of(bz * UW + u);
+        const int xrow = x_start + rr - u * R;
+        ok[i] = xrow >= 0 && xrow < xl_;
+        const float* src = reinterpret_cast<const float*>(p.x) + (long long)bu * p.sxb +
+                           (long long)min(max(xrow, 0), max(xl_ - 1, 0)) * p.sxr + g + cc * 8;
+        xa[i] = *reinterpret_cast<const f32x4*>(src);
+        xb[i] = *reinterpret_cast<const f32x4*>(src + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < SPLIT_SU; ++i) {
+        const int rr = rb + i * rstep;
+        f32x4 va = xa[i], vb = xb[i];
+        if (!ok[i]) { va = f32x4{}; vb = f32x4{}; }
+        if (p.in_slope != 1.0f) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { va[e] = leaky(va[e], p.in_slope); vb[e] = leaky(vb[e], p.in_slope); }
+        }
+        uint4 hi, lo;
+        split8(va, vb, hi, lo);
+        if (rr < RU) {
+          *reinterpret_cast<uint4*>(smem + rr * RS + cc * 16) = hi;
+          *reinterpret_cast<uint4*>(smem + PL + rr * RS + cc * 16) = lo;
+        }
+      }
+    }
+  };
+
+  for (int g0 = 0; g0 < p.Cin; g0 += CG) {
+    Frag a0[8], a1[8];  // quad ring: [0..3] hi, [4..7] lo
+    // quad qq of this group: k-steps 4qq .. 4qq+3 (never across a tap: KS % 4 == 0)
+#define TTS_SPLIT_LOADQ(A_, QQ_)                                                                     \
+    do {                                                                                             \
+      const int kq_ = 4 * (QQ_);                                                                     \
+      const int o_ = (((kq_ >> lks) * KST + g0 / 16 + (kq_ & (KS - 1))) * 1024) +                    \
+                     (((QT - 1 - (QQ_)) >> 31) & 0x40000000); /* out of range past the group */      \
+      _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                             \
+        A_[j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_hi, lofs + j_ * 1024, o_, 0)); \
+        A_[4 + j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_lo, lofs + j_ * 1024, o_, 0)); \
+      }                                                                                              \
+      __builtin_amdgcn_sched_barrier(0);                                                             \
+    } while (0)
+#define TTS_SPLIT_MMAQ(A_, QQ_)                                                                      \
+    do {                                                                                             \
+      const int kq_ = 4 * (QQ_);                                                                     \
+      const char* bq_ = xl + (kq_ >> lks) * p.dil * RS + (kq_ & (KS - 1)) * 32;                      \
+      _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                             \
+        Frag bh_[NT], bl_[NT];                                                                       \
+        _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_) {                                       \
+          bh_[nt_] = *reinterpret_cast<const Frag*>(bq_ + nt_ * 32 * RS + j_ * 32);                  \
+          bl_[nt_] = *reinterpret_cast<const Frag*>(bq_ + PL + nt_ * 32 * RS + j_ * 32);             \
+        }                                                                                            \
+        _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_) {                                       \
+          acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bh_[nt_], acc[nt_], 0, 0, 0);    \
+          accx[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bl_[nt_], accx[nt_], 0, 0, 0);  \
+          accx[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[4 + j_], bh_[nt_], accx[nt_], 0, 0, 0); \
+        }                                                                                            \
+      }                                                                                              \
+    } while (0)
+
+    int q = 0;
+    if constexpr (NT == 1) {
+      // 4-slot quad ring: the quad three ahead goes into the slot consumed one quad earlier (two
+      // quads of MFMAs cover its latency, and no load lands in a register an MFMA of the quad
+      // just issued still reads -- a 2-slot ring at one row tile was register-renamed by the
+      // compiler, whose copies then waited for every load at the end of each iteration)
+      Frag a2[8], a3[8];
+      TTS_SPLIT_LOADQ(a0, 0);
+      TTS_SPLIT_LOADQ(a1, 1);
+      TTS_SPLIT_LOADQ(a2, 2);
+      if (g0) __syncthreads();  // the previous group's tile is no longer read
+      stage(g0);
+      __syncthreads();
+      for (; q < QT; q += 4) {  // the quads past QT load nothing and are skipped
+        TTS_SPLIT_MMAQ(a0, q);
+        TTS_SPLIT_LOADQ(a3, q + 3);
+        TTS_SPLIT_MMAQ(a1, q + 1);
+        TTS_SPLIT_LOADQ(a0, q + 4);
+        if (q + 2 < QT) {
+          TTS_SPLIT_MMAQ(a2, q + 2);
+          TTS_SPLIT_LOADQ(a1, q + 5);
+          TTS_SPLIT_MMAQ(a3, q + 3);
+          TTS_SPLIT_LOADQ(a2, q + 6);
+        } else {
+          TTS_SPLIT_LOADQ(a1, q + 5);
+          TTS_SPLIT_LOADQ(a2, q + 6);
+        }
+      }
+    } else {
+      TTS_SPLIT_LOADQ(a0, 0);
+      TTS_SPLIT_LOADQ(a1, 1);
+      if (g0) __syncthreads();
+      stage(g0);
+      __syncthreads();
+      for (; q < QT; q += 2) {
+        TTS_SPLIT_MMAQ(a0, q);
+        TTS_SPLIT_LOADQ(a0, q + 2);
+        TTS_SPLIT_MMAQ(a1, q + 1);
+        TTS_SPLIT_LOADQ(a1, q + 3);
+      }
+    }
+#undef TTS_SPLIT_LOADQ
+#undef TTS_SPLIT_MMAQ
+  }
+
+  if (b >= p.B) return;
+  f32x16 out[1][NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) out[0][j] = acc[j] + accx[j] * (1.0f / SPLIT_SCALE);
+  conv_epilogue<float, 1, NT>(p, out, b, 0, n0, (by * WM + wm) * 32, ylen_of(b), l31, hh);
+}
+
+constexpr int SPLIT_LDS_MAX = 76 * 1024;  // two blocks per CU
+
+// channel group: largest power of two dividing Cin with both planes of UW utterances' rows within
+// SPLIT_LDS_MAX; >= 128 so a group has an even number of weight quads
+static int split_group(const ConvParams& p, int BN, int UW) {
+  const int R = BN + (p.taps - 1) * p.dil;
+  for (int cg = 512; cg >= 128; cg /= 2) {
+    if (cg > p.Cin || p.Cin % cg) continue;
+    if ((size_t)2 * UW * R * (cg * 2 + 16) <= (size_t)SPLIT_LDS_MAX) return cg;
+  }
+  return 0;
+}
+
+bool conv_split_eligible(const ConvParams& p) {
+  return p.wpk && p.Cin % 128 == 0 && p.M % 4 == 0 && p.nh == 1 && p.sxr % 4 == 0 && p.sxb % 4 == 0 &&
+         split_group(p, 64, 1) > 0 && split_group(p, 32, 1) > 0;
+}
+
+// Tile choice (TTS_SPLIT_TILE=1/2/3 forces one for A/B runs; the K order does not depend on it):
+//   2: 128 channels x 64 rows of one utterance (NT = 2) when that grid fills the chip 4x over;
+//   1: 128 channels x 32 rows of one utterance otherwise (more blocks for the encoder's
+//      batch x 144-row launches, and a 160-row cover of 144 rows instead of 192);
+//   3: 32 channels x 32 rows of 4 utterances (the 4 waves read the same weight quads).  Measured
+//      slower (B=8 FFN down-projection 109 vs 49 us): the vector L1 did not merge the four waves'
+//      weight reads, and four utterances' rows cost four times the staging.  Kept for A/B runs.
+static int split_tile(const ConvParams& p) {
+  static const int force = [] {
+    const char* e = getenv("TTS_SPLIT_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  if (force >= 1 && force <= 3) return force;
+  const long long blocks2 = (long long)((p.y_rows + 63) / 64) * ((p.M + 127) / 128) * p.B;
+  return blocks2 >= 4 * 256 ? 2 : 1;
+}
+
+template <int NT, int UW>
+static hipError_t launch_tile(const ConvParams& p, hipStream_t s) {
+  constexpr int BN = 32 * NT, WM = 4 / UW;
+  const int cg = split_group(p, BN, UW);
+  if (!cg) return hipErrorInvalidValue;
+  const size_t lds = (size_t)2 * UW * (BN + (p.taps - 1) * p.dil) * (cg * 2 + 16);
+  const int nwg = (p.y_rows + BN - 1) / BN * ((p.M + 32 * WM - 1) / (32 * WM)) * ((p.B + UW - 1) / UW);
+  hipLaunchKernelGGL((conv_split_kernel<NT, UW>), dim3(nwg), dim3(256), lds, s, p, cg);
+  return hipGetLastError();
+}
+
+hipError_t conv_split_launch(const ConvParams& p, hipStream_t s) {
+  switch (split_tile(p)) {
+    case 2: return launch_tile<2, 1>(p, s);
+    case 3: return split_group(p, 32, 4) ? launch_tile<1, 4>(p, s) : launch_tile<1, 1>(p, s);
+    default: return launch_tile<1, 1>(p, s);
+  }
+}
+
+}  // namespace tts

@@ -646,6 +646,8 @@ int tts_engine_create(int hip_device, const tts_config* cfg, tts_engine** out) {
     if (cfg) e->cfg = *cfg;
     auto okdt = [](int d) { return d == DT_F32 || d == DT_F16 || d == DT_BF16; };
     if (!okdt(e->cfg.vocoder_dtype) || !okdt(e->cfg.acoustic_dtype)) throw TtsError(TTS_ERR_INVALID, "bad dtype");
+    if (e->cfg.encoder_precision != TTS_ENCODER_EXACT && e->cfg.encoder_precision != TTS_ENCODER_FAST)
+      throw TtsError(TTS_ERR_INVALID, "bad encoder_precision");
     HIP_CHECK(hipSetDevice(hip_device));
     *out = e.release();
     return TTS_OK;
@@ -688,7 +690,8 @@ int tts_engine_finalize(tts_engine* eng) {
           auto it = eng->host.find(n);
           return it == eng->host.end() ? std::vector<int64_t>{} : it->second.shape;
         },
-        eng->cfg.acoustic_dtype, &eng->prof);
+        eng->cfg.acoustic_dtype, eng->cfg.encoder_precision == TTS_ENCODER_EXACT ? DT_F32 : eng->cfg.acoustic_dtype,
+        &eng->prof);
     if (!eng->voc.loaded && !eng->ac.loaded) throw TtsError(TTS_ERR_STATE, "no known weights were set");
     eng->host.clear();
     eng->finalized = true;

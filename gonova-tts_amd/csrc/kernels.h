@@ -40,8 +40,14 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why);
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s);
 
 // kernel family a launch runs as (live profiling buckets; tts_engine_profile_read_kinds)
-enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_MRF_FUSED = 2, PK_MRF_PAIR = 3, PK_MRF_CHAIN = 4, PK_UPSAMPLE = 5, PK_N = 6 };
+enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_MRF_FUSED = 2, PK_MRF_PAIR = 3, PK_MRF_CHAIN = 4, PK_UPSAMPLE = 5,
+                      PK_CONV_SPLIT = 6, PK_N = 7 };
 int conv_gemm_kind(int dtype, const ConvParams& p);
+
+// fp32 conv as three f16 MFMAs (conv_split.hip): an fp32 layer whose ConvParams::wpk is a
+// split-packed copy (frag_pack_split) runs here when eligible (Cin % 64 == 0, no head batching)
+bool conv_split_eligible(const ConvParams& p);
+hipError_t conv_split_launch(const ConvParams& p, hipStream_t s);
 
 // Fused MRF stage (mrf_fused.hip): all resblocks of one HiFi-GAN stage in one launch.
 constexpr int MRF_MAX_STEPS = 96;

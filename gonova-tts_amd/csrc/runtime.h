@@ -99,6 +99,32 @@ inline void* frag_pack(const std::vector<float>& w, int M, int taps, int ci, int
   return d;
 }
 
+// Split-precision packing for conv_split_kernel (fp32 layers run as three f16 MFMAs):
+// frag_pack's fragment order, two f16 planes -- hi = f16(w), then lo = f16((w - hi) * 2^11).
+inline void* frag_pack_split(const std::vector<float>& w, int M, int taps, int ci, std::vector<void*>& allocs) {
+  if (ci % 64 || M % 4) return nullptr;
+  const int MB = (M + 31) / 32, KS = ci / 16;
+  const size_t plane = (size_t)MB * 32 * taps * ci;
+  std::vector<float> p(2 * plane, 0.f);
+  size_t o = 0;
+  for (int mb = 0; mb < MB; ++mb)
+    for (int t = 0; t < taps; ++t)
+      for (int ks = 0; ks < KS; ++ks)
+        for (int l = 0; l < 64; ++l) {
+          const int m = mb * 32 + (l & 31);
+          for (int j = 0; j < 8; ++j, ++o) {
+            if (m >= M) continue;
+            const float v = w[((size_t)m * taps + t) * ci + ks * 16 + 8 * (l >> 5) + j];
+            const float hi = (float)(_Float16)v;
+            p[o] = hi;
+            p[plane + o] = (v - hi) * 2048.f;
+          }
+        }
+  void* d = upload(p, DT_F16);
+  allocs.push_back(d);
+  return d;
+}
+
 // 16x16 fragment packing for mrf_pair_kernel: nn.Conv1d weight [C][C][k] (host fp32) ->
 //   P[C/16][k][C/32][lane 0..63][8],  lane l holding output channel 16*mb + (l & 15),
 //   input channels 32*ks + 8*(l >> 4) + [0, 8)  (the A operand of v_mfma_f32_16x16x32_*).
@@ -136,9 +162,10 @@ inline void* frag_pack_up16(const std::vector<float>& w, int M, int K, int dt, s
 
 // nn.Conv1d weight [Cout][Cin][k] (host fp32) -> ConvLayer; scale[o] (optional) folds a
 // per-output-channel factor (BatchNorm) into the weights.
+// split: an fp32 layer also gets a split-packed copy (runs as three f16 MFMAs, conv_split.hip).
 inline ConvLayer make_conv(const std::vector<float>& w, int co, int ci, int k, const std::vector<float>& bias,
                            int dil, int pad, int dt, std::vector<void*>& allocs,
-                           const std::vector<float>* scale = nullptr) {
+                           const std::vector<float>* scale = nullptr, bool split = false) {
   if (w.size() != (size_t)co * ci * k) throw TtsError(TTS_ERR_INVALID, "conv weight size mismatch");
   std::vector<float> p((size_t)co * k * ci);
   for (int o = 0; o < co; ++o) {
@@ -149,7 +176,7 @@ inline ConvLayer make_conv(const std::vector<float>& w, int co, int ci, int k, c
   ConvLayer L;
   L.w = upload(p, dt);
   allocs.push_back(L.w);
-  L.wpk = frag_pack(p, co, k, ci, dt, allocs);
+  L.wpk = (dt == DT_F32 && split) ? frag_pack_split(p, co, k, ci, allocs) : frag_pack(p, co, k, ci, dt, allocs);
   std::vector<float> b = bias;
   if (b.empty()) b.assign(co, 0.f);
   if (b.size() != (size_t)co) throw TtsError(TTS_ERR_INVALID, "conv bias size mismatch");

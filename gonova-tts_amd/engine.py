@@ -29,7 +29,11 @@ TTS_ERRORS = {-1: "invalid argument", -2: "HIP error", -3: "bad state", -4: "out
 
 class TtsConfig(ctypes.Structure):
     _fields_ = [("vocoder_dtype", ctypes.c_int), ("acoustic_dtype", ctypes.c_int),
-                ("max_batch", ctypes.c_int), ("max_frames", ctypes.c_int), ("max_tokens", ctypes.c_int)]
+                ("max_batch", ctypes.c_int), ("max_frames", ctypes.c_int), ("max_tokens", ctypes.c_int),
+                ("encoder_precision", ctypes.c_int)]
+
+
+ENCODER_PRECISION = {"exact": 0, "fast": 1}
 
 
 class TtsConvDesc(ctypes.Structure):
@@ -140,7 +144,10 @@ class HipEngine:
     """Device-side TTS engine (one per HIP device)."""
 
     def __init__(self, device=0, vocoder_dtype: str = "f16", acoustic_dtype: str = "bf16",
-                 max_batch: int = 0, max_frames: int = 0, max_tokens: int = 0):
+                 max_batch: int = 0, max_frames: int = 0, max_tokens: int = 0, encoder_precision: str = "exact"):
+        """encoder_precision: "exact" (default) keeps the acoustic encoder and variance predictors in
+        fp32 (GEMMs as three f16 MFMAs) so predicted integer durations match fp32; "fast" runs them
+        in acoustic_dtype like the decoder (include/tts_hip.h, TTS_ENCODER_*)."""
         import torch
         self.lib = load_library()
         if not torch.cuda.is_available():
@@ -149,7 +156,9 @@ class HipEngine:
         self.torch_device = torch.device("cuda", self.device_index)
         self.vocoder_dtype = vocoder_dtype
         self.acoustic_dtype = acoustic_dtype
-        cfg = TtsConfig(DTYPES[vocoder_dtype], DTYPES[acoustic_dtype], max_batch, max_frames, max_tokens)
+        self.encoder_precision = encoder_precision
+        cfg = TtsConfig(DTYPES[vocoder_dtype], DTYPES[acoustic_dtype], max_batch, max_frames, max_tokens,
+                        ENCODER_PRECISION[encoder_precision])
         h = ctypes.c_void_p()
         check(self.lib.tts_engine_create(self.device_index, ctypes.byref(cfg), ctypes.byref(h)),
               "tts_engine_create")
@@ -287,7 +296,7 @@ class HipEngine:
         return ms.value, fl.value, n.value
 
     PROFILE_KINDS = ("conv_gemm_kernel", "conv_xres_kernel", "mrf_fused_kernel", "mrf_pair_kernel", "mrf_chain_kernel",
-                     "upsample_stream_kernel")
+                     "upsample_stream_kernel", "conv_split_kernel")
 
     def profile_read_kinds(self):
         """-> {kernel name: (summed ms, algorithmic FLOPs, launch count)}; resets."""

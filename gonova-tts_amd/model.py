@@ -91,7 +91,8 @@ class GonovaTTS:
     def from_pretrained(cls, device: str = "cuda", ckpt_dir: Optional[str] = None, seed: int = 0,
                         vocoder_dtype: str = "f16", acoustic_dtype: str = "bf16", fixed_duration: Optional[int] = None,
                         max_batch: int = 0, max_frames: int = 0, max_tokens: int = 0,
-                        sample_rate: Optional[int] = None, speaker_embed_dim: Optional[int] = None):
+                        sample_rate: Optional[int] = None, speaker_embed_dim: Optional[int] = None,
+                        encoder_precision: str = "exact"):
         """Mirror of `ChatterboxTTS.from_pretrained(device=...)` (synthesizer.py:185).
 
         ckpt_dir: optional directory with `acoustic.safetensors` and `vocoder.safetensors`
@@ -99,7 +100,9 @@ class GonovaTTS:
         (no checkpoint is reachable offline).  sample_rate: output rate (default 22,050 Hz;
         24,000 reproduces the rate the reference's clients assume).  speaker_embed_dim: seeded
         multi-speaker weights with a speaker-embedding projection of that size (a checkpoint
-        carrying `projection.weight` sets it by itself)."""
+        carrying `projection.weight` sets it by itself).  encoder_precision: "exact" (default: the
+        encoder and variance predictors keep fp32 activations, so predicted integer durations match
+        fp32, HF:181-183) or "fast" (all of the acoustic model in acoustic_dtype)."""
         acfg, vcfg = AcousticConfig(speaker_embed_dim=speaker_embed_dim), VocoderConfig()
         if ckpt_dir:
             aw = load_state_dict(os.path.join(ckpt_dir, "acoustic.safetensors"))
@@ -110,7 +113,8 @@ class GonovaTTS:
             aw = make_acoustic_weights(seed, acfg, fixed_duration=fixed_duration)
             vw = make_vocoder_weights(seed, vcfg)
         eng = HipEngine(device, vocoder_dtype=vocoder_dtype, acoustic_dtype=acoustic_dtype,
-                        max_batch=max_batch, max_frames=max_frames, max_tokens=max_tokens)
+                        max_batch=max_batch, max_frames=max_frames, max_tokens=max_tokens,
+                        encoder_precision=encoder_precision)
         eng.load_weights(vocoder=vw, acoustic=aw, vocoder_cfg=vcfg)
         return cls(eng, acfg, vcfg, sample_rate=sample_rate)
 

@@ -60,7 +60,16 @@ typedef struct tts_config {
   int max_batch;       /* workspace reservation hints (0 = grow on demand) */
   int max_frames;
   int max_tokens;
+  int encoder_precision; /* TTS_ENCODER_*: precision of the acoustic encoder + variance predictors */
 } tts_config;
+
+/* Acoustic encoder precision.  EXACT (the default, 0): with a 16-bit acoustic_dtype the encoder,
+ * speaker projection and variance predictors keep fp32 activations and run their GEMMs as three
+ * f16 MFMAs (~2^-21 relative per product), so the predicted integer durations
+ * clamp(round(exp(x) - 1), 0) (HF:181-183) match an fp32 evaluation; the decoder and postnet run in
+ * acoustic_dtype.  FAST (1): the whole acoustic model runs in acoustic_dtype (durations can
+ * round differently near .5).  With acoustic_dtype = F32 both are plain fp32. */
+enum { TTS_ENCODER_EXACT = 0, TTS_ENCODER_FAST = 1 };
 
 /* Number of HIP devices visible to this process. */
 int tts_device_count(void);
@@ -118,7 +127,7 @@ int tts_engine_profile(tts_engine* eng, int enable);
 int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops, int* n_launches);
 /* The same, split by kernel family into arrays of nkinds entries:
  * 0 = conv_gemm_kernel, 1 = conv_xres_kernel, 2 = mrf_fused_kernel, 3 = mrf_pair_kernel,
- * 4 = mrf_chain_kernel, 5 = upsample_stream_kernel. */
+ * 4 = mrf_chain_kernel, 5 = upsample_stream_kernel, 6 = conv_split_kernel. */
 int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, double* flops, int* n_launches);
 
 /* Rational-rate resampling of waveforms (22,050 -> 24,000 Hz for

@@ -290,3 +290,79 @@ def test_failed_reserve_leaves_a_usable_engine(aw):
     after, la, _ = run(eng, ids_list, t_cap=120, durations=durs)
     assert np.array_equal(lb, la) and np.array_equal(before, after)
     eng.close()
+
+
+def _oracle_log_durations(ids, aw):
+    """fp32 oracle encoder + duration predictor only (HF:1171-1208), the log-durations that
+    clamp(round(exp(x) - 1), 0) (HF:181-183) turns into integers."""
+    from oracle.acoustic import conformer_stack, variance_predictor
+    x = aw["encoder.embed.weight"][np.asarray(ids, np.int64)]
+    x = conformer_stack(x, aw, "encoder.", 4, 2)
+    return variance_predictor(x, aw, "duration_predictor.", 2)
+
+
+def _margin(logd):
+    """distance of the oracle's exp(x)-1 from the nearest .5 rounding boundary"""
+    return np.abs((np.exp(logd.astype(np.float32)) - 1) % 1 - 0.5)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_predicted_durations_exact_on_default_path(aw, dtype):
+    """The default 16-bit acoustic path (encoder_precision="exact": encoder, speaker projection and
+    variance predictors in fp32 with three-f16-MFMA GEMMs, conv_split.hip) predicts integer
+    durations equal to the fp32 oracle's for every token whose oracle exp(x)-1 is more than 1e-3
+    from a .5 boundary -- the same carve-out as the fp32 path above.  C3's token distribution
+    (32 x 144 ids U[1,77], 4,608 tokens), the two transformers golden utterances and a ragged tail."""
+    eng = engine(dtype, aw)
+    rng = np.random.default_rng(2000)
+    ids_list = [rng.integers(1, 78, size=144) for _ in range(32)]
+    ids_list += [G["ac_a_ids"], G["ac_b_ids"], rng.integers(1, 78, size=7), rng.integers(1, 78, size=1)]
+    _, _, dur = run(eng, ids_list, t_cap=12 * 144)
+    bad = total = carved = 0
+    for b, ids in enumerate(ids_list):
+        logd = _oracle_log_durations(ids, aw)
+        ref = np.maximum(np.round(np.exp(logd.astype(np.float32)) - np.float32(1)), 0).astype(np.int64)
+        ok = _margin(logd) > 1e-3
+        got = dur[b, :len(ids)]
+        bad += int((got[ok] != ref[ok]).sum())
+        total += int(ok.sum())
+        carved += int((~ok).sum())
+    print(f"[parity] durations {dtype} exact-encoder: {bad} of {total} tokens differ "
+          f"({carved} within 1e-3 of a .5 boundary not compared)")
+    assert bad == 0
+    for tag in ("ac_a", "ac_b"):  # the transformers goldens themselves
+        b = len(ids_list) - 4 + (tag == "ac_b")
+        np.testing.assert_array_equal(dur[b, :len(G[f"{tag}_ids"])], G[f"{tag}_dur"])
+
+
+def test_predicted_durations_bf16_mel_matches_oracle(aw):
+    """Predicted (not forced) durations on the default bf16 path end to end: the frame counts
+    equal the oracle's, so the mel is comparable frame for frame (tests/parity.py ac_bf16)."""
+    eng = engine("bf16", aw)
+    rng = np.random.default_rng(31)
+    ids_list = [rng.integers(1, 78, size=n) for n in (48, 21)]
+    mel, mel_lens, dur = run(eng, ids_list, t_cap=12 * 48)
+    for b, ids in enumerate(ids_list):
+        ref = acoustic_forward(ids, aw)
+        np.testing.assert_array_equal(dur[b, :len(ids)], ref["durations"])
+        L = int(mel_lens[b])
+        assert L == ref["mel"].shape[0]
+        check(f"acoustic bf16 predicted-dur b={b}", mel[b, :L], ref["mel"], kind="ac_bf16")
+        assert np.all(mel[b, L:] == 0)
+
+
+def test_fast_encoder_precision_bounded():
+    """encoder_precision="fast" (the whole acoustic model in bf16) stays available: its durations
+    may round differently near .5 (measured 131 of 4,608 C3 tokens, all within 0.1 of a boundary);
+    bounded here at 5 % of tokens, none off by more than one frame."""
+    aw = make_acoustic_weights(seed=0)
+    e = HipEngine(DEV, vocoder_dtype="f32", acoustic_dtype="bf16", encoder_precision="fast")
+    e.load_weights(acoustic=aw)
+    rng = np.random.default_rng(2000)
+    ids_list = [rng.integers(1, 78, size=144) for _ in range(8)]
+    _, _, dur = run(e, ids_list, t_cap=12 * 144)
+    diff = np.concatenate([dur[b, :144] - np.maximum(np.round(np.exp(
+        _oracle_log_durations(ids, aw).astype(np.float32)) - 1), 0) for b, ids in enumerate(ids_list)])
+    print(f"[parity] durations bf16 fast-encoder: {int((diff != 0).sum())} of {diff.size} tokens differ")
+    assert (diff != 0).mean() < 0.05 and np.abs(diff).max() <= 1
+    e.close()

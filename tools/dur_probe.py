@@ -43,15 +43,15 @@ def main():
                       "frac_margin_lt_1e-3": float((margin < 1e-3).mean()),
                       "frac_margin_lt_1e-2": float((margin < 1e-2).mean()),
                       "frac_margin_lt_3e-2": float((margin < 3e-2).mean())}), flush=True)
-    for dt in ("f32", "f16", "bf16"):
-        eng = HipEngine("cuda:0", vocoder_dtype="f32", acoustic_dtype=dt)
+    for dt, prec in (("f32", "exact"), ("f16", "exact"), ("bf16", "exact"), ("f16", "fast"), ("bf16", "fast")):
+        eng = HipEngine("cuda:0", vocoder_dtype="f32", acoustic_dtype=dt, encoder_precision=prec)
         eng.load_weights(acoustic=aw)
         mel, ml, dur = eng.acoustic(torch.from_numpy(tok).cuda(), torch.from_numpy(lens), 12 * N,
                                     return_durations=True)
         torch.cuda.synchronize()
         d = dur.cpu().numpy()
         bad = d != ref_dur
-        print(json.dumps({"dtype": dt, "mismatch_tokens": int(bad.sum()), "tokens": int(bad.size),
+        print(json.dumps({"dtype": dt, "encoder": prec, "mismatch_tokens": int(bad.sum()), "tokens": int(bad.size),
                           "utts_with_mismatch": int(bad.any(axis=1).sum()),
                           "max_margin_of_mismatch": float(margin[bad].max()) if bad.any() else None,
                           "median_margin_of_mismatch": float(np.median(margin[bad])) if bad.any() else None}),
@@ -69,7 +69,7 @@ def main():
                     for _ in range(10):
                         eng.acoustic(tk, tl, N * fr, durations=dd)
                     torch.cuda.synchronize()
-                    print(json.dumps({"dtype": dt, "B": Bt, "frames_per_token": fr,
+                    print(json.dumps({"dtype": dt, "encoder": prec, "B": Bt, "frames_per_token": fr,
                                       "acoustic_ms": round((time.perf_counter() - t) * 100, 3)}), flush=True)
         eng.close()
 

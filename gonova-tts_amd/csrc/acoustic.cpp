@@ -69,6 +69,19 @@ struct AcousticModel::Impl {
   // fp32 layers of a 16-bit model get split-packed weights (three f16 MFMAs, conv_split.hip)
   bool split_now() const { return bdt == DT_F32 && dt != DT_F32; }
   size_t esz() const { return std::max(dtype_size(dt), dtype_size(dte)); }
+  // encoder row stride: at least ENC_PAD masked rows after every utterance, so the split-precision
+  // GEMMs run packed 128-row tiles across utterances (ConvParams::rows_pad; k <= 5 convs)
+  static constexpr int ENC_PAD = 2;
+  static int enc_rows(int N) { return rup(N + ENC_PAD, 32); }
+  int cur_rpad = 0;            // rows_pad of the convs being launched (encoder side only)
+  float* split_ws = nullptr;   // split-K partial sums of the packed split GEMMs
+  long long split_ws_bytes = 0;
+  void run(const ConvLayer& L, const void* x, int x_rows, const int* lens, void* y, int y_rows, int B, int d,
+           hipStream_t s, Profiler* pr, float in_slope = 1.f, int act = ACT_NONE, float alpha = 1.f,
+           const void* r1 = nullptr) {
+    run_layer(L, x, x_rows, lens, y, y_rows, B, d, s, pr, in_slope, act, alpha, r1, nullptr, 1.f, 0, 0, cur_rpad,
+              split_ws, split_ws_bytes);
+  }
   Profiler* prof = nullptr;
   int D = 384, H = 2, V = 78, NMEL = 80, FFN = 1536, PRED = 256;
   float eps = 1e-5f;
@@ -245,6 +258,8 @@ struct AcousticModel::Impl {
     X = Y = O = G = Qu = Qv = H1 = QKV = A = Vt = ENC = SPK = PB1 = PB2 = BEF = PN1 = PN2 = MELT = nullptr;
     f_pitch = f_energy = f_logd = nullptr;
     i_dur = i_tokmap = nullptr;
+    split_ws = nullptr;
+    split_ws_bytes = 0;
     std::vector<void*> old;
     old.swap(ws);
     for (void* p : old) hipFree(p);
@@ -290,7 +305,7 @@ struct AcousticModel::Impl {
   void reserve_fresh(int B, int N, int T) {
     const size_t e = esz();
     const int Tm = std::max(N, T);
-    const int Tp = rup(Tm, 32);
+    const int Tp = std::max(rup(Tm, 32), enc_rows(N));
     const int dk = D / H;
     const size_t rows = (size_t)B * Tp;
     X = alloc_ws(rows * D, e); Y = alloc_ws(rows * D, e); O = alloc_ws(rows * D, e); G = alloc_ws(rows * D, e);
@@ -298,7 +313,7 @@ struct AcousticModel::Impl {
     H1 = alloc_ws(rows * FFN, e); QKV = alloc_ws(rows * 3 * D, e); A = alloc_ws(rows * 2 * D, e);
     const int Sk = rup(Tm, 16);
     Vt = alloc_ws((size_t)B * H * dk * Sk, e);
-    const size_t nrows = (size_t)B * rup(N, 32);
+    const size_t nrows = (size_t)B * enc_rows(N);
     ENC = alloc_ws(nrows * D, e);
     SPK = alloc_ws((size_t)B * D, e);
     PB1 = alloc_ws(nrows * PRED, e); PB2 = alloc_ws(nrows * PRED, e);
@@ -308,6 +323,18 @@ struct AcousticModel::Impl {
     f_pitch = (float*)alloc_ws(nrows, 4); f_energy = (float*)alloc_ws(nrows, 4); f_logd = (float*)alloc_ws(nrows, 4);
     i_dur = (int*)alloc_ws((size_t)B * N, 4);
     i_tokmap = (int*)alloc_ws((size_t)B * T, 4);
+    // split-K partials of the encoder's packed split GEMMs (fp32 encoder of a 16-bit model)
+    long long wsb = 0;
+    if (dte == DT_F32 && dt != DT_F32) {
+      const int F = B * enc_rows(N);
+      for (auto& L : enc)
+        for (const ConvLayer* c : {&L.ffm1, &L.ffm2, &L.ff1, &L.ff2, &L.qkv, &L.out, &L.pw1, &L.pw2})
+          wsb = std::max(wsb, conv_split_ws_bytes(c->taps, c->Cin, c->M, F));
+      for (const Predictor* pr : {&pitch, &energy, &duration})
+        for (const ConvLayer& c : pr->convs) wsb = std::max(wsb, conv_split_ws_bytes(c.taps, c.Cin, c.M, F));
+    }
+    split_ws = wsb ? (float*)alloc_ws((size_t)wsb, 1) : nullptr;
+    split_ws_bytes = wsb;
     cap_B = B; cap_N = N; cap_T = T;
   }
 
@@ -330,8 +357,8 @@ struct AcousticModel::Impl {
     launch_conv_checked(p, d, s, prof, 2.0 * M * (double)K * x_rows * B * H);
   }
 
-  void stack(std::vector<ConformerLayer>& layers, void* Xb, const int* lens, int B, int Tm, hipStream_t s) {
-    const int Tp = rup(Tm, 32);
+  // Tm: longest utterance (attention extent); Tp: row stride of Xb and the workspace
+  void stack(std::vector<ConformerLayer>& layers, void* Xb, const int* lens, int B, int Tm, int Tp, hipStream_t s) {
     const int dk = D / H;
     const int rows = B * Tp;
     const int Sk = rup(Tm, 16), Sac = rup(Tm, 16), Sbd = rup(2 * Tm, 16);
@@ -340,18 +367,18 @@ struct AcousticModel::Impl {
     for (auto& L : layers) {
       const int dt = L.dt;
       // macaron FFN: x = LN(x + 0.5 * ffn(x))
-      run_layer(L.ffm1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
-      run_layer(L.ffm2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
+      run(L.ffm1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
+      run(L.ffm2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
       ln_rows(dt, Y, Xb, rows, D, L.ln_mac, nullptr, s);
       // relative-position MHSA: x = LN(x + mhsa(x))
-      run_layer(L.qkv, Xb, Tp, lens, QKV, Tp, B, dt, s, prof);
+      run(L.qkv, Xb, Tp, lens, QKV, Tp, B, dt, s, prof);
       const bool fused_attn = rel_attn_enabled() && rel_attn_supported(dt, D, H);
       if (!fused_attn) HIP_CHECK(launch_pos_bias(dt, QKV, rows, D, L.pos_u, L.pos_v, Qu, Qv, s));
       HIP_CHECK(launch_transpose_v(dt, QKV, lens, B, Tp, D, H, Sk, Vt, s));
       if (fused_attn) {
         // fused flash-style relative-position attention (attention.hip); Qu / Qv formed in it
         HIP_CHECK(launch_rel_attn(dt, L.pos_u, L.pos_v, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale, O, s));
-        run_layer(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
+        run(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
         ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s);
         conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
         continue;
@@ -367,7 +394,7 @@ struct AcousticModel::Impl {
       // O[b][i][h*dk + d] = sum_j P[b,h][i][j] * Vt[b,h][d][j]
       attn_gemm(dt, P, (long long)H * Tm * Sk, (long long)Tm * Sk, Sk, lens, Tm, Vt, (long long)H * dk * Sk,
                 (long long)dk * Sk, Sk, dk, Sk, O, (long long)Tp * D, dk, D, B, s);
-      run_layer(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
+      run(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
       ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s);
       conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
     }
@@ -376,13 +403,13 @@ struct AcousticModel::Impl {
   void conv_module_and_ffn(ConformerLayer& L, void* Xb, const int* lens, int B, int Tp, int rows, hipStream_t s) {
     const int dt = L.dt;
     // conv module: x = LN(x + pw2(silu(bn(dw(glu(pw1(x)))))))
-    run_layer(L.pw1, Xb, Tp, lens, A, Tp, B, dt, s, prof);
+    run(L.pw1, Xb, Tp, lens, A, Tp, B, dt, s, prof);
     HIP_CHECK(launch_glu_dwconv(dt, A, lens, B, Tp, D, L.dw_w, L.dw_k, L.dw_b, G, s));
-    run_layer(L.pw2, G, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
+    run(L.pw2, G, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
     ln_rows(dt, Y, Xb, rows, D, L.ln_conv, nullptr, s);
     // FFN: x = final_LN(LN(x + 0.5 * ffn(x)))
-    run_layer(L.ff1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
-    run_layer(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
+    run(L.ff1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
+    run(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
     ln_rows(dt, Y, Xb, rows, D, L.ln_ff, &L.ln_final, s);
   }
 
@@ -393,7 +420,7 @@ struct AcousticModel::Impl {
     const int n = (int)Pr.convs.size();
     for (int i = 0; i < n; ++i) {
       void* o = bufs[i & 1];
-      run_layer(Pr.convs[i], h, Np, lens, o, Np, B, dt, s, prof, 1.f, ACT_RELU);
+      run(Pr.convs[i], h, Np, lens, o, Np, B, dt, s, prof, 1.f, ACT_RELU);
       if (i + 1 < n) ln_rows(dt, o, o, B * Np, PRED, Pr.lns[i], nullptr, s);
       else HIP_CHECK(launch_ln_linear1(dt, o, B * Np, PRED, Pr.lns[i].g, Pr.lns[i].b, eps, Pr.lin_w, Pr.lin_b, out, s));
       h = o;
@@ -412,10 +439,11 @@ struct AcousticModel::Impl {
     }
     if (Tm > rmax) build_ptabs(rup(Tm, 256), s);
     const float xscale = std::sqrt((float)D);
-    const int Np = rup(N, 32), Tp = rup(Tcap, 32);
+    const int Np = enc_rows(N), Tp = rup(Tcap, 32);
     // encoder
     HIP_CHECK(launch_embed(dte, tokens, tok_lens, B, N, Np, embed, V, D, xscale, ENC, s));
-    stack(enc, ENC, tok_lens, B, N, s);
+    cur_rpad = Np - N;  // encoder side: packed-row split GEMMs
+    stack(enc, ENC, tok_lens, B, N, Np, s);
     if (spk && E) {  // speaker embedding (HF:1192-1196); without one HF skips the projection
       HIP_CHECK(launch_spk_bias(dte, spk, B, E, proj_we, proj_b, D, SPK, s));
       ConvParams p = conv_params_default();
@@ -425,6 +453,7 @@ struct AcousticModel::Impl {
       p.r1 = SPK; p.srb = D; p.srr = 0;  // the utterance's term broadcast over its frames
       p.y_len = tok_lens; p.y_rows = Np;
       p.M = D; p.Cin = D; p.B = B;
+      p.rows_pad = cur_rpad; p.ws = split_ws; p.ws_bytes = split_ws_bytes;
       launch_conv_checked(p, dte, s, prof, 2.0 * D * (double)D * B * Np);
       HIP_CHECK(hipMemcpyAsync(ENC, Y, (size_t)B * Np * D * dtype_size(dte), hipMemcpyDeviceToDevice, s));
     }
@@ -432,6 +461,7 @@ struct AcousticModel::Impl {
     predict(pitch, ENC, tok_lens, B, Np, f_pitch, s);
     predict(energy, ENC, tok_lens, B, Np, f_energy, s);
     predict(duration, ENC, tok_lens, B, Np, f_logd, s);
+    cur_rpad = 0;
     // logd is laid out [B][Np]; durations kernel reads [B][N] rows -> compact view via stride Np
     int* dur = durations ? durations : i_dur;
     HIP_CHECK(launch_durations_strided(s, B, N, Np, tok_lens, dur_override, Tcap, dur, mel_lens));
@@ -445,16 +475,16 @@ struct AcousticModel::Impl {
       HIP_CHECK(hipMemcpy2DAsync(X, (size_t)Tp * D * dtype_size(dt), Y, (size_t)Tcap * D * dtype_size(dt),
                                  (size_t)Tcap * D * dtype_size(dt), B, hipMemcpyDeviceToDevice, s));
     }
-    stack(dec, Xd, mel_lens, B, Tcap, s);
+    stack(dec, Xd, mel_lens, B, Tcap, Tp, s);
     // postnet (HF:238-244), BatchNorm folded
-    run_layer(feat_out, Xd, Tp, mel_lens, BEF, Tp, B, dt, s, prof);
+    run(feat_out, Xd, Tp, mel_lens, BEF, Tp, B, dt, s, prof);
     const void* h = BEF;
     void* bufs[2] = {PN1, PN2};
     const int n = (int)postnet.size();
     for (int i = 0; i < n; ++i) {
       const bool last = i == n - 1;
       void* o = last ? MELT : bufs[i & 1];
-      run_layer(postnet[i], h, Tp, mel_lens, o, Tp, B, dt, s, prof, 1.f, last ? ACT_NONE : ACT_TANH, 1.f,
+      run(postnet[i], h, Tp, mel_lens, o, Tp, B, dt, s, prof, 1.f, last ? ACT_NONE : ACT_TANH, 1.f,
                 last ? BEF : nullptr);
       h = o;
     }

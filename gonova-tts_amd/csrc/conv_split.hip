@@ -28,6 +28,7 @@
 #include "conv_epilogue.h"
 #include "kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace tts {
@@ -234,6 +235,261 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
   conv_epilogue<float, 1, NT>(p, out, b, 0, n0, (by * WM + wm) * 32, ylen_of(b), l31, hh);
 }
 
+// ---------------------------------------------------------------------------------------
+// Packed-row form (ConvParams::rows_pad): the batch is one flat sequence of B * x_rows rows, an
+// utterance's rows followed by >= rows_pad masked rows, so a 128-row tile may hold the end of
+// one utterance and the start of the next (every staged row is masked by its own utterance's
+// length; a conv tap never reaches past the masked gap).  Block: 4 waves along M (128 output
+// channels) x 128 rows (each wave 4 MFMA row tiles; each weight quad feeds 12 MFMAs, a quarter
+// of the per-CU weight stream of 32-row tiles, with no row cover beyond the 32-row padding).
+// K is optionally split into S slices of whole channel groups (S from the layer shape only, so a
+// row's accumulation order never depends on the batch): each slice writes fp32 partial sums to
+// ConvParams::ws and split_reduce_kernel adds them in slice order and applies the epilogue.
+constexpr int SPK_NT = 2;  // 32-row MFMA tiles per wave: 64-row blocks
+constexpr int SPK_SU = 9;  // X prefetch registers (16 B each) per thread: 66-72 rows x 128 channels
+
+__device__ inline int packed_valid(const ConvParams& p, const int* lens, int f, int F) {
+  if (f < 0 || f >= F) return 0;
+  const int b = f / p.x_rows;
+  const int r = f - b * p.x_rows;
+  return r < (lens ? min(lens[b], p.x_rows) : p.x_rows);
+}
+
+__global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int CG, int S, int gps) {
+  typedef half8 Frag;
+  constexpr int NT = SPK_NT, BN = 32 * NT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int F = p.B * p.x_rows;  // flat rows
+  const int ntx = (F + BN - 1) / BN;
+  const int nmb = (p.M + 127) / 128;
+  // XCD-aware order (T1): work w = (slice, M block, row tile), row tile fastest, contiguous per XCD
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xq = nwg / 8, xr = nwg % 8, xcd = orig % 8;
+  const int w = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + orig / 8;
+  const int tx = w % ntx;
+  const int by = (w / ntx) % nmb;
+  const int sl = w / (ntx * nmb);
+  const int f0 = tx * BN;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l31 = lane & 31;
+  const int hh = lane >> 5;
+
+  const int KST = p.Cin / 16;
+  const int MB = (p.M + 31) / 32;
+  const int mb = min(by * 4 + wave, MB - 1);
+  const int wbytes = __builtin_amdgcn_readfirstlane(p.taps * KST * 1024);
+  const char* whi = reinterpret_cast<const char*>(p.wpk) + (long long)mb * wbytes;
+  const char* wlo = whi + (long long)MB * wbytes;
+  const auto rs_hi = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(whi), 0, wbytes, 0x00020000);
+  const auto rs_lo = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wlo), 0, wbytes, 0x00020000);
+  const int lofs = lane * 16;
+
+  const int R = BN + (p.taps - 1) * p.dil;
+  const int RS = CG * 2 + 16;
+  const int PL = R * RS;
+  const int KS = CG / 16;
+  const int lks = __builtin_ctz(KS);
+  const int QT = p.taps * KS / 4;  // even (CG >= 128)
+  const int x_start = f0 - p.pad;
+  const char* xl = smem + l31 * RS + hh * 16;
+  const float* X = reinterpret_cast<const float*>(p.x);
+
+  f32x16 acc[NT], accx[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) { acc[j] = f32x16{}; accx[j] = f32x16{}; }
+
+  // X staging: thread owns 4-channel column c4 of the group and staged rows r0, r0 + rstep, ...
+  // (at most SPK_SU: split_group sizes CG for that).  The next group's rows are loaded into
+  // registers while the current group's MFMAs run (issued two weight quads into the group, so
+  // the first wait on a younger weight load finds them landed) and split into LDS after them.
+  const int VPR = CG / 4;
+  const int lvpr = __builtin_ctz(VPR);
+  const int c4 = tid & (VPR - 1);
+  const int r0 = tid >> lvpr;
+  const int rstep = 256 >> lvpr;
+  f32x4 xv[SPK_SU];
+  auto load_x = [&](int g) {
+#pragma unroll
+    for (int i = 0; i < SPK_SU; ++i) {
+      const int f = x_start + min(r0 + i * rstep, R - 1);
+      xv[i] = *reinterpret_cast<const f32x4*>(X + (long long)min(max(f, 0), F - 1) * p.sxr + g + c4 * 4);
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int i = 0; i < SPK_SU; ++i) {
+      const int rr = r0 + i * rstep;
+      f32x4 v = xv[i];
+      if (!packed_valid(p, p.x_len, x_start + rr, F)) v = f32x4{};
+      if (p.in_slope != 1.0f) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = leaky(v[e], p.in_slope);
+      }
+      const half4 h = __builtin_convertvector(v, half4);
+      const half4 l = __builtin_convertvector((v - __builtin_convertvector(h, f32x4)) * SPLIT_SCALE, half4);
+      if (rr < R) {
+        *reinterpret_cast<uint2*>(smem + rr * RS + c4 * 8) = __builtin_bit_cast(uint2, h);
+        *reinterpret_cast<uint2*>(smem + PL + rr * RS + c4 * 8) = __builtin_bit_cast(uint2, l);
+      }
+    }
+  };
+
+  const int gbeg = sl * gps * CG, gend = min(p.Cin, (sl + 1) * gps * CG);
+  load_x(gbeg);
+  store_x();
+  __syncthreads();
+  for (int g0 = gbeg; g0 < gend; g0 += CG) {
+    Frag a0[8], a1[8];
+#define TTS_SPLIT_LOADQ(A_, QQ_)                                                                     \
+    do {                                                                                             \
+      const int kq_ = 4 * (QQ_);                                                                     \
+      const int o_ = (((kq_ >> lks) * KST + g0 / 16 + (kq_ & (KS - 1))) * 1024) +                    \
+                     (((QT - 1 - (QQ_)) >> 31) & 0x40000000);                                        \
+      _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                             \
+        A_[j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_hi, lofs + j_ * 1024, o_, 0)); \
+        A_[4 + j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_lo, lofs + j_ * 1024, o_, 0)); \
+      }                                                                                              \
+      __builtin_amdgcn_sched_barrier(0);                                                             \
+    } while (0)
+#define TTS_SPLIT_MMAQ(A_, QQ_)                                                                      \
+    do {                                                                                             \
+      const int kq_ = 4 * (QQ_);                                                                     \
+      const char* bq_ = xl + (kq_ >> lks) * p.dil * RS + (kq_ & (KS - 1)) * 32;                      \
+      _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                             \
+        _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_) {                                       \
+          const Frag bh_ = *reinterpret_cast<const Frag*>(bq_ + nt_ * 32 * RS + j_ * 32);            \
+          const Frag bl_ = *reinterpret_cast<const Frag*>(bq_ + PL + nt_ * 32 * RS + j_ * 32);       \
+          acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bh_, acc[nt_], 0, 0, 0);         \
+          accx[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bl_, accx[nt_], 0, 0, 0);       \
+          accx[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[4 + j_], bh_, accx[nt_], 0, 0, 0);   \
+        }                                                                                            \
+      }                                                                                              \
+    } while (0)
+    const bool more = g0 + CG < gend;
+    TTS_SPLIT_LOADQ(a0, 0);
+    TTS_SPLIT_LOADQ(a1, 1);
+    TTS_SPLIT_MMAQ(a0, 0);
+    TTS_SPLIT_LOADQ(a0, 2);
+    load_x(more ? g0 + CG : g0);  // unconditional (a load under a branch is waited on at once)
+    TTS_SPLIT_MMAQ(a1, 1);
+    TTS_SPLIT_LOADQ(a1, 3);
+    for (int q = 2; q < QT; q += 2) {
+      TTS_SPLIT_MMAQ(a0, q);
+      TTS_SPLIT_LOADQ(a0, q + 2);
+      TTS_SPLIT_MMAQ(a1, q + 1);
+      TTS_SPLIT_LOADQ(a1, q + 3);
+    }
+#undef TTS_SPLIT_LOADQ
+#undef TTS_SPLIT_MMAQ
+    if (more) {
+      __syncthreads();  // every wave is done with this group's tile
+      store_x();
+      __syncthreads();
+    }
+  }
+
+  const int m_w0 = (by * 4 + wave) * 32;
+  if (S == 1) {
+    // epilogue through LDS: fp32 tile [BN rows][128 channels] (row stride 528 B), then a row pass
+    // of 16-byte pieces -- bias, alpha, activation, residuals (prefetched before the staging
+    // barrier), scale -- with coalesced row stores (fragment-shaped stores were ~1/3 of a small
+    // launch's time)
+    constexpr int OSR = 128 * 4 + 16;
+    constexpr int NIT = BN * 32 / 256;  // 4-channel pieces per thread
+    const int pc = tid & 31;            // piece: channels by*128 + 4*pc .. +3
+    const int m4 = by * 128 + pc * 4;
+    const bool mok = m4 < p.M;
+    f32x4 res[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int rl = (tid >> 5) + it * 8;
+      const int f = min(f0 + rl, F - 1);
+      const int b = f / p.x_rows, r = f - b * p.x_rows;
+      res[it] = f32x4{};
+      if (p.r1 && mok) res[it] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.r1) +
+                                                                 (long long)b * p.srb + (long long)r * p.srr + m4);
+    }
+    __syncthreads();  // X tile no longer read
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const f32x16 v = acc[nt] + accx[nt] * (1.0f / SPLIT_SCALE);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(smem + (nt * 32 + l31) * OSR + (wave * 32 + 8 * g + 4 * hh) * 4) =
+            f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+    }
+    __syncthreads();
+    const f32x4 bias = (p.bias && mok) ? *reinterpret_cast<const f32x4*>(p.bias + m4) : f32x4{};
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int rl = (tid >> 5) + it * 8;
+      const int f = f0 + rl;
+      if (f >= F || !mok) continue;
+      const int b = f / p.x_rows, r = f - b * p.x_rows;
+      if (r >= (p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows)) continue;
+      f32x4 v = *reinterpret_cast<const f32x4*>(smem + rl * OSR + pc * 16) + bias;
+      if (p.alpha != 1.0f) v *= p.alpha;
+      if (p.act_out) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act_out, p.out_slope);
+      }
+      const long long ro = (long long)b * p.srb + (long long)r * p.srr + m4;
+      v += res[it];
+      if (p.r2) v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.r2) + ro);
+      if (p.out_scale != 1.0f) v *= p.out_scale;
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.y) + (long long)b * p.syb + (long long)r * p.syr + m4) = v;
+    }
+    return;
+  }
+  // partial sums of slice sl: ws[sl][f][M] (rows past F and channels past M are not stored)
+  float* P = p.ws + (long long)sl * F * p.M;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int f = f0 + nt * 32 + l31;
+    if (f >= F) continue;
+    const f32x16 v = acc[nt] + accx[nt] * (1.0f / SPLIT_SCALE);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int m = m_w0 + 8 * g + 4 * hh;
+      if (m < p.M)
+        *reinterpret_cast<f32x4*>(P + (long long)f * p.M + m) = f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+    }
+  }
+}
+
+// y[f][m] = epilogue(sum over slices of ws[s][f][m]) for every valid flat row (conv_epilogue's
+// arithmetic: ((alpha * (acc + bias)) -> act) + r1 + r2, times out_scale)
+__global__ __launch_bounds__(256) void split_reduce_kernel(ConvParams p, int S) {
+  const int F = p.B * p.x_rows;
+  const int M4 = p.M / 4;
+  const long long n = (long long)F * M4;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const int f = (int)(i / M4);
+    const int m = (int)(i - (long long)f * M4) * 4;
+    const int b = f / p.x_rows;
+    const int r = f - b * p.x_rows;
+    const int ylen = p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows;
+    if (r >= ylen) continue;
+    f32x4 v = *reinterpret_cast<const f32x4*>(p.ws + (long long)f * p.M + m);
+    for (int s = 1; s < S; ++s) v += *reinterpret_cast<const f32x4*>(p.ws + ((long long)s * F + f) * p.M + m);
+    if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + m);
+    if (p.alpha != 1.0f) v *= p.alpha;
+    if (p.act_out) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act_out, p.out_slope);
+    }
+    const long long ro = (long long)b * p.srb + (long long)r * p.srr + m;
+    if (p.r1) v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.r1) + ro);
+    if (p.r2) v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.r2) + ro);
+    if (p.out_scale != 1.0f) v *= p.out_scale;
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.y) + (long long)b * p.syb + (long long)r * p.syr + m) = v;
+  }
+}
+
 constexpr int SPLIT_LDS_MAX = 76 * 1024;  // two blocks per CU
 
 // channel group: largest power of two dividing Cin with both planes of UW utterances' rows within
@@ -252,40 +508,86 @@ bool conv_split_eligible(const ConvParams& p) {
          split_group(p, 64, 1) > 0 && split_group(p, 32, 1) > 0;
 }
 
-// Tile choice (TTS_SPLIT_TILE=1/2/3 forces one for A/B runs; the K order does not depend on it):
-//   2: 128 channels x 64 rows of one utterance (NT = 2) when that grid fills the chip 4x over;
-//   1: 128 channels x 32 rows of one utterance otherwise (more blocks for the encoder's
-//      batch x 144-row launches, and a 160-row cover of 144 rows instead of 192);
-//   3: 32 channels x 32 rows of 4 utterances (the 4 waves read the same weight quads).  Measured
-//      slower (B=8 FFN down-projection 109 vs 49 us): the vector L1 did not merge the four waves'
-//      weight reads, and four utterances' rows cost four times the staging.  Kept for A/B runs.
+// Per-utterance form (callers without the packed-row promise): 128 channels x 64 rows of one
+// utterance (NT = 2) when that grid fills the chip 4x over, else 32 rows (more blocks, a 160-row
+// cover of 144 rows instead of 192).  TTS_SPLIT_TILE=1/2 forces one; the K order is the same.
 static int split_tile(const ConvParams& p) {
   static const int force = [] {
     const char* e = getenv("TTS_SPLIT_TILE");
     return e ? atoi(e) : 0;
   }();
-  if (force >= 1 && force <= 3) return force;
+  if (force == 1 || force == 2) return force;
   const long long blocks2 = (long long)((p.y_rows + 63) / 64) * ((p.M + 127) / 128) * p.B;
   return blocks2 >= 4 * 256 ? 2 : 1;
 }
 
-template <int NT, int UW>
+template <int NT>
 static hipError_t launch_tile(const ConvParams& p, hipStream_t s) {
-  constexpr int BN = 32 * NT, WM = 4 / UW;
-  const int cg = split_group(p, BN, UW);
+  constexpr int BN = 32 * NT;
+  const int cg = split_group(p, BN, 1);
   if (!cg) return hipErrorInvalidValue;
-  const size_t lds = (size_t)2 * UW * (BN + (p.taps - 1) * p.dil) * (cg * 2 + 16);
-  const int nwg = (p.y_rows + BN - 1) / BN * ((p.M + 32 * WM - 1) / (32 * WM)) * ((p.B + UW - 1) / UW);
-  hipLaunchKernelGGL((conv_split_kernel<NT, UW>), dim3(nwg), dim3(256), lds, s, p, cg);
+  const size_t lds = (size_t)2 * (BN + (p.taps - 1) * p.dil) * (cg * 2 + 16);
+  const int nwg = (p.y_rows + BN - 1) / BN * ((p.M + 127) / 128) * p.B;
+  hipLaunchKernelGGL((conv_split_kernel<NT, 1>), dim3(nwg), dim3(256), lds, s, p, cg);
   return hipGetLastError();
 }
 
+// packed-row channel group: 128 when every thread's share of the (128 + halo)-row tile fits its
+// SPK_SU prefetch registers and both planes fit LDS at one block per CU
+static int packed_group(const ConvParams& p) {
+  const int R = 32 * SPK_NT + (p.taps - 1) * p.dil;
+  const int cg = 128, rstep = 256 / (cg / 4);
+  if (p.Cin % cg || (R + rstep - 1) / rstep > SPK_SU || (size_t)2 * R * (cg * 2 + 16) > SPLIT_LDS_MAX) return 0;
+  return cg;
+}
+
+// packed-row form: usable when the caller promises enough masked rows after every utterance for
+// this conv's taps, the row stride is a multiple of 32 rows, and the buffers are contiguous
+static bool packed_ok(const ConvParams& p) {
+  const int right = (p.taps - 1) * p.dil - p.pad;
+  return p.rows_pad > 0 && p.rows_pad >= p.pad && p.rows_pad >= right && p.x_rows == p.y_rows &&
+         p.x_rows % 32 == 0 && p.sxb == (long long)p.x_rows * p.sxr && p.syb == (long long)p.y_rows * p.syr &&
+         (!(p.r1 || p.r2) || p.srb == (long long)p.y_rows * p.srr) && !p.up_s && p.M % 4 == 0;
+}
+
+// split-K slices from the layer shape only (batch-independent accumulation order): one slice per
+// ~1152 of K (taps * Cin), whole channel groups each, while the workspace holds the partials
+static int split_slices(const ConvParams& p, int cg) {
+  const int groups = p.Cin / cg;
+  int S = std::max(1, std::min(groups, p.taps * p.Cin / 1152));
+  while (S > 1 && groups % S) --S;
+  const long long need = (long long)S * p.B * p.x_rows * p.M * 4;
+  return (S > 1 && p.ws && need <= p.ws_bytes) ? S : 1;
+}
+
+long long conv_split_ws_bytes(int taps, int Cin, int M, int rows) {
+  ConvParams q = conv_params_default();
+  q.taps = taps; q.Cin = Cin; q.M = M; q.B = 1; q.x_rows = rows; q.ws = reinterpret_cast<float*>(16);
+  q.ws_bytes = 1LL << 62;
+  const int cg = packed_group(q);
+  return cg ? (long long)split_slices(q, cg) * rows * M * 4 : 0;
+}
+
 hipError_t conv_split_launch(const ConvParams& p, hipStream_t s) {
-  switch (split_tile(p)) {
-    case 2: return launch_tile<2, 1>(p, s);
-    case 3: return split_group(p, 32, 4) ? launch_tile<1, 4>(p, s) : launch_tile<1, 1>(p, s);
-    default: return launch_tile<1, 1>(p, s);
+  if (packed_ok(p)) {
+    const int cg = packed_group(p);
+    if (cg) {
+      const int S = split_slices(p, cg);
+      const int gps = p.Cin / cg / S;
+      const int F = p.B * p.x_rows;
+      const int nwg = (F + 32 * SPK_NT - 1) / (32 * SPK_NT) * ((p.M + 127) / 128) * S;
+      const size_t lds = std::max((size_t)2 * (32 * SPK_NT + (p.taps - 1) * p.dil) * (cg * 2 + 16),
+                                  (size_t)32 * SPK_NT * (128 * 4 + 16));  // X planes / epilogue tile
+      hipLaunchKernelGGL(conv_splitp_kernel, dim3(nwg), dim3(256), lds, s, p, cg, S, gps);
+      if (S > 1) {
+        const long long n = (long long)F * (p.M / 4);
+        const unsigned g = (unsigned)std::min<long long>((n + 255) / 256, 4096);
+        hipLaunchKernelGGL(split_reduce_kernel, dim3(g), dim3(256), 0, s, p, S);
+      }
+      return hipGetLastError();
+    }
   }
+  return split_tile(p) == 2 ? launch_tile<2>(p, s) : launch_tile<1>(p, s);
 }
 
 }  // namespace tts

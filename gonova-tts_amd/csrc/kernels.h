@@ -27,6 +27,13 @@ struct ConvParams {
   // optional fragment-packed copy of w (frag_pack in runtime.h): enables the X-resident
   // kernel, whose weight loads are then contiguous 1 KiB wave reads
   const void* wpk;
+  // Packed-row hint (split-precision fp32 GEMMs, conv_split.hip): rows_pad > 0 promises that every
+  // utterance is followed by at least rows_pad masked rows (x_rows - len[b] >= rows_pad, X / Y /
+  // residuals contiguous [B][x_rows][C]), so row tiles may run across utterance boundaries; the
+  // optional split-K workspace ws (ws_bytes) holds fp32 partial sums.
+  int rows_pad;
+  float* ws;
+  long long ws_bytes;
 };
 
 inline ConvParams conv_params_default() {
@@ -48,6 +55,8 @@ int conv_gemm_kind(int dtype, const ConvParams& p);
 // split-packed copy (frag_pack_split) runs here when eligible (Cin % 64 == 0, no head batching)
 bool conv_split_eligible(const ConvParams& p);
 hipError_t conv_split_launch(const ConvParams& p, hipStream_t s);
+// split-K workspace bytes a packed-row launch of this shape over `rows` flat rows can use (0: none)
+long long conv_split_ws_bytes(int taps, int Cin, int M, int rows);
 
 // Fused MRF stage (mrf_fused.hip): all resblocks of one HiFi-GAN stage in one launch.
 constexpr int MRF_MAX_STEPS = 96;

@@ -26,8 +26,8 @@ the timed region; strong scaling over N).
 `roofline` is for the dominant kernel family (largest summed time per step: today the
 fused ResBlock-pair kernel of all four stages), timed live with hipEvents around every launch
 on the stream it runs on; `roofline.kernels` lists every family the same way
-(conv_gemm_kernel, conv_xres_kernel, mrf_fused_kernel, mrf_pair_kernel, mrf_chain_kernel,
-upsample_stream_kernel).  `cpu_baseline` (rank 0, N=1 only) is the torch-CPU fp32
+(conv_gemm_kernel, conv_xres_kernel, mrf_pair_kernel, mrf_chain_kernel, upsample_stream_kernel,
+conv_split_kernel).  `cpu_baseline` (rank 0, N=1 only) is the torch-CPU fp32
 restatement (oracle/torch_cpu.py) timed on the host cores on a bounded
 sample of C2 (4 utterances) and C3 (2 utterances).
 """

@@ -22,16 +22,14 @@
 
 #include "acoustic_kernels.h"
 #include "runtime.h"
+#include "switches.h"
 
 namespace tts {
 
 namespace {
 
 // TTS_REL_ATTN=0: the unfused attention path (four launches) for A/B and parity tests
-bool rel_attn_enabled() {
-  const char* e = getenv("TTS_REL_ATTN");
-  return !e || atoi(e) != 0;
-}
+bool rel_attn_enabled() { return sw(SW_REL_ATTN) != 0; }
 
 inline int rup(int x, int m) { return (x + m - 1) / m * m; }
 

@@ -28,6 +28,7 @@
 #include "common.h"
 #include "conv_epilogue.h"
 #include "kernels.h"
+#include "switches.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -219,9 +220,6 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
 // stride CG*2+16 bytes (an odd number of 16-byte slots: conflict-free ds_read_b128 of 32
 // consecutive rows).
 constexpr int XRES_HR = 64;            // output rows per N-wave staged per half
-#ifndef TTS_XRES_PROBE
-#define TTS_XRES_PROBE 0               // timing-only probes for A/B builds (results invalid)
-#endif
 #ifndef TTS_XRES_STORE
 #define TTS_XRES_STORE 2               // output store cache policy (store16 in common.h)
 #endif
@@ -346,12 +344,7 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
 #pragma unroll
       for (int i = 0; i < XRES_SU; ++i) {
         const int xr = min(max(x_start + min(rb + i * rstep, R - 1), 0), xlast);
-#if TTS_XRES_PROBE & 1  // timing-only: no X staging loads
-        { const unsigned z = (unsigned)(xr * 977 + cc + g0) * 2654435761u;
-          r[i] = uint4{z & 0xB7FF37FFu, (z >> 3) & 0x37FFB7FFu, (z >> 5) & 0xB7FF37FFu, (z >> 7) & 0x37FFB7FFu}; }
-#else
         r[i] = *reinterpret_cast<const uint4*>(xg + xr * p.sxr);
-#endif
       }
 #pragma unroll
       for (int i = 0; i < XRES_SU; ++i) {
@@ -381,15 +374,6 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
 
   // ---- epilogue through LDS: fragments -> fp32 rows -> 8-channel row pieces ----
   T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.syb + (long long)hd * p.syh;
-#if TTS_XRES_PROBE & 2  // timing-only: no epilogue (accumulators kept live)
-  {
-    float z = 0.f;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) z += acc[j][0] + acc[j][15];
-    if (z == 1234.5f) Y[tid] = (T)z;
-    return;
-  }
-#endif
   const T* R1 = p.r1 ? reinterpret_cast<const T*>(p.r1) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const T* R2 = p.r2 ? reinterpret_cast<const T*>(p.r2) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const int tlen = p.up_len ? min(p.up_len[b], (p.y_rows - 1) * p.up_s) : 0;
@@ -468,9 +452,6 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
       if (p.out_scale != 1.0f) { v0 *= p.out_scale; v1 *= p.out_scale; }
       y = pack8<T>(v0, v1);
     }
-#if TTS_XRES_PROBE & 4  // timing-only: row pass without its global stores
-    if (y.x == 0x12345678u)
-#endif
     store16<TTS_XRES_STORE>(Y, (int)(((long long)row * p.syr + col) * (long long)sizeof(T)), y);
   }
 #else
@@ -532,20 +513,9 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
       if (R1) { f32x4 a, c; ld8<T>(reinterpret_cast<const T*>(&res1[half][it]), a, c); v0 += a; v1 += c; }
       if (R2) { f32x4 a, c; ld8<T>(R2 + (long long)row * p.srr + col, a, c); v0 += a; v1 += c; }
       if (p.out_scale != 1.0f) { v0 *= p.out_scale; v1 *= p.out_scale; }
-#if TTS_XRES_PROBE & 4  // timing-only: row pass without its global stores
-      if (v0[0] == 1234.5f)
-#endif
       {
         const uint4 e8 = pack8<T>(v0, v1);
-#if TTS_XRES_PROBE & 8  // timing-only: every block stores into the same 32 KB (L2-resident, no HBM writes)
-        store16<TTS_XRES_STORE>(Y, (int)((((rl & 127) * 16 + cl) * 16) & 0x7fff), e8);
-#elif TTS_XRES_PROBE & 16  // timing-only: each block writes its own contiguous 32 KB (same bytes, block-linear)
-        store16<TTS_XRES_STORE>(Y, (int)((blockIdx.x * gridDim.y + blockIdx.y) * 32768 + (((half * 64 + (rl & 63)) * 16 + cl) * 16) % 32768),
-                                e8);
-#else
-        store16<TTS_XRES_STORE>(Y, (int)(((long long)row * p.syr + col) * (long long)sizeof(T)),
-                                e8);
-#endif
+        store16<TTS_XRES_STORE>(Y, (int)(((long long)row * p.syr + col) * (long long)sizeof(T)), e8);
       }
     }
   }
@@ -573,13 +543,7 @@ static int xres_group(const ConvParams& p, int BN, int lds_max = XRES_LDS_MAX) {
   return 0;
 }
 
-static int xres_mode() {  // TTS_CONV_XRES=0 disables the X-resident kernel (A/B runs)
-  static int m = [] {
-    const char* e = getenv("TTS_CONV_XRES");
-    return e ? atoi(e) : 1;
-  }();
-  return m;
-}
+static int xres_mode() { return sw(SW_CONV_XRES) != 0; }  // TTS_CONV_XRES=0 disables the X-resident kernel
 
 // 128-channel blocks (4 x 1 waves, BN = 128) for M >= 128; 64-channel blocks (2 x 2 waves,
 // BN = 256) for M = 64 (the last upsampler)
@@ -599,8 +563,7 @@ static int xres_wm(const ConvParams& p) { return p.M >= 128 ? 4 : 2; }
 // forces it off / on where eligible (A/B runs and tests).
 static bool xres_narrow(const ConvParams& p, int nt) {
   if (p.M % 64 || !TTS_XRES_EPI16) return false;
-  const char* e = getenv("TTS_XRES_NARROW");
-  if (e) return atoi(e) != 0;
+  if (sw(SW_XRES_NARROW) >= 0) return sw(SW_XRES_NARROW) != 0;
   const long long blocks = (long long)((p.y_rows + 32 * nt - 1) / (32 * nt)) * ((p.M + 127) / 128) * p.B * p.nh;
   if (blocks < TTS_XRES_NARROW_MAXBLK) return true;
   // long-K launches (the encoder's FFN down-projection, K = 4608) up to twice that many blocks
@@ -613,9 +576,9 @@ static bool xres_narrow(const ConvParams& p, int nt) {
 // 64-row tiles (NT = 2) where 128-row tiles would leave much of the last tile of every
 // utterance empty (the encoder's 144 rows: 3 x 64 = 192 rows of work instead of 2 x 128)
 static int xres_nt(const ConvParams& p, int wm) {
-  const char* e = getenv("TTS_XRES_NT");  // 2 / 4 force a tile height (tests), else automatic
+  const int force = sw(SW_XRES_NT);  // 2 / 4 force a tile height (tests), else automatic
   if (wm != 4) return 4;
-  if (e && (atoi(e) == 2 || atoi(e) == 4)) return atoi(e);
+  if (force == 2 || force == 4) return force;
   if (!TTS_XRES_SMALL_TILES) return 4;
   const int r4 = (p.y_rows + 127) / 128 * 128, r2 = (p.y_rows + 63) / 64 * 64;
   return 8 * r2 <= 7 * r4 ? 2 : 4;
@@ -672,13 +635,7 @@ static hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-static int wide_mode() {
-  static int m = [] {
-    const char* e = getenv("TTS_CONV_WIDE");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
+static int wide_mode() { return sw(SW_CONV_WIDE) > 0; }
 
 template <typename T>
 static hipError_t launch_t(const ConvParams& p, hipStream_t s) {

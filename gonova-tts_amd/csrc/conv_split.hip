@@ -27,6 +27,7 @@
 #include "common.h"
 #include "conv_epilogue.h"
 #include "kernels.h"
+#include "switches.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -512,10 +513,7 @@ bool conv_split_eligible(const ConvParams& p) {
 // utterance (NT = 2) when that grid fills the chip 4x over, else 32 rows (more blocks, a 160-row
 // cover of 144 rows instead of 192).  TTS_SPLIT_TILE=1/2 forces one; the K order is the same.
 static int split_tile(const ConvParams& p) {
-  static const int force = [] {
-    const char* e = getenv("TTS_SPLIT_TILE");
-    return e ? atoi(e) : 0;
-  }();
+  const int force = sw(SW_SPLIT_TILE);
   if (force == 1 || force == 2) return force;
   const long long blocks2 = (long long)((p.y_rows + 63) / 64) * ((p.M + 127) / 128) * p.B;
   return blocks2 >= 4 * 256 ? 2 : 1;

@@ -19,6 +19,7 @@
 
 #include "../../include/tts_hip.h"
 #include "acoustic.h"
+#include "switches.h"
 #include "common.h"
 #include "kernels.h"
 #include "runtime.h"
@@ -52,46 +53,16 @@ struct VocoderWeights {
   float post_b = 0.f;
   int post_k = 7, post_c = 32;
   int hop = 256;
-  // fused MRF launch templates per stage (x/s/len/T/B filled per forward); empty = unfused
-  std::vector<MrfParams> fused;
-  std::vector<MrfTable> fused_tab;  // host copy (FLOP accounting)
-  std::vector<bool> has_fused;
 };
 
-// TTS_MRF_FUSED=0 selects the unfused per-conv path (A/B and parity tests); read per forward.
-static bool mrf_fused_enabled() {
-  const char* e = getenv("TTS_MRF_FUSED");
-  return e ? atoi(e) != 0 : true;
-}
+// TTS_MRF_FUSED=0 selects the unfused per-conv path (A/B and parity tests)
+static bool mrf_fused_enabled() { return sw(SW_MRF_FUSED) != 0; }
 // resblock chain kernel for the HBM-bound resblocks (default on; TTS_MRF_CHAIN=0: pairs only)
-#ifndef TTS_MRF_CHAIN_DEFAULT
-#define TTS_MRF_CHAIN_DEFAULT 1
-#endif
-static bool mrf_chain_enabled() {
-  const char* e = getenv("TTS_MRF_CHAIN");
-  return e ? atoi(e) != 0 : TTS_MRF_CHAIN_DEFAULT != 0;
-}
+static bool mrf_chain_enabled() { return sw(SW_MRF_CHAIN) != 0; }
 // conv_post inside the vocoder's last pair launch (default on; TTS_POST_FUSE=0: separate launch)
-#ifndef TTS_POST_FUSE_DEFAULT
-#define TTS_POST_FUSE_DEFAULT 1
-#endif
-static bool post_fuse_enabled() {
-  const char* e = getenv("TTS_POST_FUSE");
-  return e ? atoi(e) != 0 : TTS_POST_FUSE_DEFAULT != 0;
-}
+static bool post_fuse_enabled() { return sw(SW_POST_FUSE) != 0; }
 // streaming upsampler for the small stages (default on; TTS_UP_STREAM=0: conv_xres)
-#ifndef TTS_UP_STREAM_DEFAULT
-#define TTS_UP_STREAM_DEFAULT 1
-#endif
-static bool up_stream_enabled() {
-  const char* e = getenv("TTS_UP_STREAM");
-  return e ? atoi(e) != 0 : TTS_UP_STREAM_DEFAULT != 0;
-}
-// fused MRF flavour: pair kernels (default) or the whole-stage kernel (TTS_MRF_PAIR=0)
-static bool mrf_pair_enabled() {
-  const char* e = getenv("TTS_MRF_PAIR");
-  return e ? atoi(e) != 0 : true;
-}
+static bool up_stream_enabled() { return sw(SW_UP_STREAM) != 0; }
 
 struct tts_engine {
   int device = 0;
@@ -195,83 +166,6 @@ struct tts_engine {
     return L;
   }
 
-  // Fused-MRF weights: every conv of the stage as [k][Cout][Cin] slabs, and the step table
-  // (one step per tap group of each conv) consumed by mrf_fused_kernel.
-  void prepare_fused_stage(int i, int nk, int dt) {
-    VocoderWeights& v = voc;
-    v.fused.resize(i + 1);
-    v.has_fused.resize(i + 1, false);
-    const int C = v.stage_ch[i];
-    if (dt == DT_F32 || (C != 32 && C != 64) || nk > 4) return;
-    MrfTable mp{};
-    MrfParams pp{};
-    mp.nblk = nk;
-    mp.npair = (int)v.mrf[i][0].size();
-    if (mp.npair > 4) return;
-    pp.slope = 0.1f;
-    pp.out_scale = 1.0f / (float)nk;
-    const int G = mrf_fused_taps_per_group(C);
-    const int BN = mrf_fused_bn(C);
-    int hmax = 0, n = 0;
-    std::vector<float> biases;
-    for (int j = 0; j < nk; ++j) {
-      if ((int)v.mrf[i][j].size() != mp.npair) return;
-      const int k = v.mrf[i][j][0][0].taps;
-      const int hk = (k - 1) / 2;
-      mp.k[j] = k;
-      int h = 0;
-      for (int q = 0; q < mp.npair; ++q) {
-        mp.dil[j][q] = v.mrf[i][j][q][0].dil;
-        h += hk * mp.dil[j][q] + hk;
-      }
-      mp.halo[j] = h;
-      hmax = std::max(hmax, h);
-      const std::string pre = "resblocks." + std::to_string(i * nk + j) + ".";
-      int lo = 0;  // first LDS row of the pair's input range
-      for (int q = 0; q < mp.npair; ++q)
-        for (int cv = 0; cv < 2; ++cv) {
-          const std::string cname = pre + (cv ? "convs2." : "convs1.") + std::to_string(q);
-          const int conv_idx = (j * mp.npair + q) * 2 + cv;
-          const auto& bh = get(cname + ".bias").data;
-          biases.insert(biases.end(), bh.begin(), bh.end());
-          const int dq = mp.dil[j][q];
-          const int a = cv == 0 ? hk * dq : hk;
-          const int olo = lo + (cv == 0 ? a : hk * dq + hk);
-          const int nt = (BN + 2 * h - 2 * olo + 31) / 32;
-          const int fin = (cv == 1 && q == mp.npair - 1) ? 1 : 0;
-          if (cv == 1) lo += hk * dq + hk;
-          const HostTensor& w = get(cname + ".weight");
-          std::vector<float> slab((size_t)k * C * C);
-          for (int t = 0; t < k; ++t)
-            for (int m = 0; m < C; ++m)
-              for (int c = 0; c < C; ++c) slab[((size_t)t * C + m) * C + c] = w.data[((size_t)m * C + c) * k + t];
-          char* dptr = (char*)track(upload(slab, dt));
-          for (int t0 = 0; t0 < k; t0 += G) {
-            if (n >= MRF_MAX_STEPS) return;
-            const int ntp = std::min(G, k - t0);
-            const int last = (t0 + ntp == k) ? 1 : 0;
-            mp.step[n] = make_int4(j | (q << 4) | (cv << 8) | (last << 12) | (fin << 13), t0, ntp, conv_idx);
-            mp.geo[n] = make_int4(olo, a, cv == 0 ? dq : 1, nt);
-            mp.step_w[n] = dptr + (size_t)t0 * C * C * dtype_size(dt);
-            ++n;
-          }
-        }
-    }
-    mp.nsteps = n;
-    mp.nconv = nk * mp.npair * 2;
-    mp.bias = (const float*)track(upload_f32(biases));
-    pp.rp = BN + 2 * hmax + 32;
-    void* dtab = nullptr;
-    HIP_CHECK(hipMalloc(&dtab, sizeof(MrfTable)));
-    HIP_CHECK(hipMemcpy(dtab, &mp, sizeof(MrfTable), hipMemcpyHostToDevice));
-    track(dtab);
-    pp.tab = (const MrfTable*)dtab;
-    v.fused[i] = pp;
-    v.fused_tab.resize(i + 1);
-    v.fused_tab[i] = mp;
-    v.has_fused[i] = true;
-  }
-
   void finalize_vocoder() {
     if (!has("conv_pre.weight")) return;
     const int dt = cfg.vocoder_dtype;
@@ -327,7 +221,6 @@ struct tts_engine {
           }
         }
       }
-      prepare_fused_stage(i, nk, dt);
     }
     const HostTensor& pw = get("conv_post.weight");  // [1][C][k]
     v.post_c = (int)pw.shape[1];
@@ -497,7 +390,7 @@ struct tts_engine {
         return ok;
       };
       bool pair_ok = false;
-      if (mrf_fused_enabled() && mrf_pair_enabled())
+      if (mrf_fused_enabled())
         for (int j = 0; j < nk; ++j) pair_ok = pair_ok || pair_capable(j);
       if (pair_ok) {
         // 9 pair launches: X -> HA -> HB -> S per resblock; S accumulates over resblocks.  A resblock
@@ -566,25 +459,6 @@ struct tts_engine {
             }
             h = pp.y;
           }
-        }
-        Tin = Tout;
-        cin = ch;
-        continue;
-      }
-      if (mrf_fused_enabled() && i < (int)v.has_fused.size() && v.has_fused[i]) {
-        MrfParams mp = v.fused[i];
-        mp.x = XS; mp.s = S; mp.len = Lp(i + 1); mp.T = Tout; mp.B = B;
-        const MrfTable& tab = v.fused_tab[i];
-        const double fl = 2.0 * ch * (double)ch * (double)B * Tout * 2.0 * tab.npair *
-                          [&] { double k = 0; for (int j = 0; j < nk; ++j) k += tab.k[j]; return k; }();
-        if (prof.on) {
-          Profiler::Rec r{prof.get(), prof.get(), fl, PK_MRF_FUSED};
-          HIP_CHECK(hipEventRecord(r.a, s));
-          HIP_CHECK(mrf_fused_launch(dt, ch, mp, s));
-          HIP_CHECK(hipEventRecord(r.b, s));
-          prof.recs.push_back(r);
-        } else {
-          HIP_CHECK(mrf_fused_launch(dt, ch, mp, s));
         }
         Tin = Tout;
         cin = ch;
@@ -781,6 +655,14 @@ int tts_engine_profile(tts_engine* eng, int enable) {
 
 int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops, int* n_launches) {
   return guarded(eng, [&] { eng->prof.read(gemm_ms, gemm_flops, n_launches); });
+}
+
+int tts_set_switch(const char* name, int value) {
+  if (tts::sw_set(name, value)) {
+    g_last_error = std::string("unknown switch: ") + (name ? name : "(null)");
+    return TTS_ERR_INVALID;
+  }
+  return TTS_OK;
 }
 
 int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, double* flops, int* n_launches) {

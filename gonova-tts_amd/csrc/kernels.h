@@ -47,7 +47,7 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why);
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s);
 
 // kernel family a launch runs as (live profiling buckets; tts_engine_profile_read_kinds)
-enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_MRF_FUSED = 2, PK_MRF_PAIR = 3, PK_MRF_CHAIN = 4, PK_UPSAMPLE = 5,
+enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_RETIRED = 2 /* mrf_fused, removed */, PK_MRF_PAIR = 3, PK_MRF_CHAIN = 4, PK_UPSAMPLE = 5,
                       PK_CONV_SPLIT = 6, PK_N = 7 };
 int conv_gemm_kind(int dtype, const ConvParams& p);
 
@@ -58,28 +58,6 @@ hipError_t conv_split_launch(const ConvParams& p, hipStream_t s);
 // split-K workspace bytes a packed-row launch of this shape over `rows` flat rows can use (0: none)
 long long conv_split_ws_bytes(int taps, int Cin, int M, int rows);
 
-// Fused MRF stage (mrf_fused.hip): all resblocks of one HiFi-GAN stage in one launch.
-constexpr int MRF_MAX_STEPS = 96;
-// Device-resident schedule of one stage (uploaded once; read with uniform indices -> scalar loads).
-struct MrfTable {
-  int nblk, npair, nsteps, nconv;
-  int k[4];
-  int dil[4][4];
-  int halo[4];        // receptive-field half-width of each resblock
-  int4 step[MRF_MAX_STEPS];             // {blk | pair<<4 | conv<<8 | last<<12 | final<<13, tap0, ntaps, conv index}
-  int4 geo[MRF_MAX_STEPS];              // {olo (first output row in LDS), a (half-width), d (dilation), nt (tiles)}
-  const void* step_w[MRF_MAX_STEPS];    // [ntaps][C][C] weight slab of the step
-  const float* bias;                    // [nconv][C] biases of every conv of the stage, fp32
-};
-struct MrfParams {
-  const void* x;      // [B][T][C] stage input (upsampler output), compute dtype
-  void* s;            // [B][T][C] output: mean over resblocks
-  const int* len;     // per-utterance valid rows
-  const MrfTable* tab;
-  int T, B;
-  float slope, out_scale;
-  int rp;             // LDS rows per activation buffer
-};
 // Fused ResBlock pair (mrf_pair.hip): t = lrelu(conv_{k,d}(lrelu(h)) + b1);
 // h' = conv_{k,1}(t) + b2 + h;  y = ((accum ? y : 0) + h') * scale.
 struct MrfPairParams {
@@ -141,10 +119,6 @@ struct MrfChainParams {
 };
 bool mrf_chain_supported(int dtype, int C, int k, const int* dil, int npair);
 hipError_t mrf_chain_launch(int dtype, int C, int k, const MrfChainParams& p, hipStream_t s);
-
-int mrf_fused_taps_per_group(int C);
-int mrf_fused_bn(int C);
-hipError_t mrf_fused_launch(int dtype, int C, const MrfParams& p, hipStream_t s);
 
 // resample.hip: scipy.signal.resample_poly's default filter (padded taps, n_pre_remove)
 int resample_design(int up, int down, std::vector<double>& h, int& n_pre_remove);

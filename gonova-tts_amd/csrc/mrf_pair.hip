@@ -14,7 +14,7 @@
 // the last pair of a resblock, the running MRF sum.  HBM traffic per pair: read h once
 // (+ halo, mostly L2), write h' once (S: read + write).
 //
-// Why pairs, not whole stages (mrf_fused.hip) or single convs (conv_xres): a whole-stage
+// Why pairs, not whole stages (round 1's mrf_fused kernel, removed) or single convs (conv_xres): a whole-stage
 // tile must carry the receptive-field halo of all three pairs of a resblock (60 rows per
 // side at k=11) and recompute it in every conv -- 55 % (C=64) / 71 % (C=32) of its issued
 // MFMA work was useful; a pair recomputes only conv1's 2*a2 <= 10 extra rows.  Against two
@@ -35,15 +35,13 @@
 #include "common.h"
 #include "kernels.h"
 #include "mrf_tile.h"
+#include "switches.h"
 
 #ifndef TTS_PAIR_C256
 #define TTS_PAIR_C256 1  // stage 0 (C = 256) as pair launches; 0: single convs (conv_xres)
 #endif
 #ifndef TTS_PAIR_MTO_MIN
 #define TTS_PAIR_MTO_MIN 64  // pair_conv's M-tile-outer MFMA order from this channel count up
-#endif
-#ifndef TTS_PAIR_PROBE
-#define TTS_PAIR_PROBE 0  // timing-only probes for A/B builds (results invalid): 1 no staging loads, 2 no weight reloads
 #endif
 
 #include <algorithm>
@@ -150,12 +148,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
         uint4 v[PAIR_SU];
 #pragma unroll
         for (int i = 0; i < PAIR_SU; ++i)
-#if TTS_PAIR_PROBE & 1  // timing-only probe: no staging loads (pseudo-random f16 payload)
-          { const unsigned z = (unsigned)(rb + i * rstep + cc * 977 + n0) * 2654435761u;
-            v[i] = uint4{z & 0xB7FF37FFu, (z >> 3) & 0x37FFB7FFu, (z >> 5) & 0xB7FF37FFu, (z >> 7) & 0x37FFB7FFu}; }
-#else
           v[i] = *reinterpret_cast<const uint4*>(xc + (long long)(gs + min(rb + i * rstep, RG - 1)) * C);
-#endif
 #pragma unroll
         for (int i = 0; i < PAIR_SU; ++i) {
           const int r = rb + i * rstep;
@@ -333,13 +326,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
     if (gr >= len) continue;
     T* dst = Y + (long long)gr * C + c8 * 8;
     const uint4 y = *reinterpret_cast<const uint4*>(smem + o * YS16 + c8 * 16);
-#if TTS_PAIR_PROBE & 4  // timing-only: every block stores into the same 32 KB (no HBM writes)
-    (void)dst;
-    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(p.y) + ((idx * 16) & 0x7fff)) =
-        epi_row<T>(y, xin[it], p.accum, sin[it], p.scale);
-#else
     store16<TTS_ROW_STORE>(Y, (int)((dst - Y) * (long long)sizeof(T)), epi_row<T>(y, xin[it], p.accum, sin[it], p.scale));
-#endif
   }
 }
 
@@ -356,8 +343,8 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
 // TTS_PAIR_DIV=1 / any other value forces full-height / short tiles (tests).
 static int pair_div(int C, const MrfPairParams& p, bool post) {
   if (post) return 1;
-  const char* e = getenv("TTS_PAIR_DIV");
-  if (e) return atoi(e) == 1 ? 1 : TTS_PAIR_SHORT_DIV;
+  const int force = sw(SW_PAIR_DIV);
+  if (force >= 0) return force == 1 ? 1 : TTS_PAIR_SHORT_DIV;
   const int bn = C == 32 ? PairGeom<32>::BN : C == 64 ? PairGeom<64>::BN : C == 128 ? PairGeom<128>::BN : PairGeom<256>::BN;
   return (long long)((p.T + bn - 1) / bn) * p.B < TTS_PAIR_SHORT ? TTS_PAIR_SHORT_DIV : 1;
 }

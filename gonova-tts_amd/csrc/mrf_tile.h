@@ -233,11 +233,7 @@ __device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][MT], typename Mfma<T>
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[u][mt] = MF::mma(ring[slot][mt], bf[u], acc[u][mt]);
     }
-#if defined(TTS_PAIR_PROBE) && (TTS_PAIR_PROBE & 2)
-    if (false) {
-#else
     if (reload) {
-#endif
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
         ring[slot][mt] = *reinterpret_cast<const Frag*>(wp + ((long long)mt * S + s + D) * 1024);

@@ -1,0 +1,27 @@
+// Runtime switches selecting alternative kernel paths (A/B runs and the parity tests' reference
+// paths).  Each is read from its TTS_* environment variable once, on first use, and can be set
+// at run time through tts_set_switch (include/tts_hip.h); nothing on the forward path calls
+// getenv.  -1 = not set: the path's built-in default.
+#pragma once
+
+namespace tts {
+
+enum Sw : int {
+  SW_REL_ATTN,     // TTS_REL_ATTN=0: unfused four-launch attention (16-bit)
+  SW_MRF_FUSED,    // TTS_MRF_FUSED=0: the per-conv MRF path
+  SW_MRF_CHAIN,    // TTS_MRF_CHAIN=0/1: resblock chain kernel off / on
+  SW_POST_FUSE,    // TTS_POST_FUSE=0: conv_post as its own launch
+  SW_UP_STREAM,    // TTS_UP_STREAM=0: stages 2-3 upsamplers on conv_xres
+  SW_CONV_XRES,    // TTS_CONV_XRES=0: no X-resident conv kernel
+  SW_XRES_NARROW,  // TTS_XRES_NARROW=0/1: force conv_xres narrow tiles off / on
+  SW_XRES_NT,      // TTS_XRES_NT=2/4: force conv_xres tile height
+  SW_CONV_WIDE,    // TTS_CONV_WIDE=1: 128-byte channel chunks in conv_gemm
+  SW_SPLIT_TILE,   // TTS_SPLIT_TILE=1/2: force the per-utterance split GEMM tile
+  SW_PAIR_DIV,     // TTS_PAIR_DIV=1: full-height pair tiles; any other value: short tiles
+  SW_N
+};
+
+int sw(Sw s);                              // current value, -1 = not set
+int sw_set(const char* name, int value);   // 0, or -1 for an unknown name
+
+}  // namespace tts

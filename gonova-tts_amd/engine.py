@@ -11,6 +11,7 @@ visible, construction raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -76,6 +77,7 @@ C_API = [
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     ("tts_resample_poly", _I, [_VP, _VP, ctypes.c_int64, _VP, _I, _I, _I, _VP, ctypes.c_int64, _I, _VP, _VP]),
     ("tts_resample_filter", _I, [_I, _I, ctypes.POINTER(ctypes.c_double), _I, ctypes.POINTER(ctypes.c_int)]),
+    ("tts_set_switch", _I, [ctypes.c_char_p, _I]),
     ("tts_last_error", ctypes.c_char_p, []),
     ("tts_op_conv1d", _I, [_I, ctypes.POINTER(TtsConvDesc), _VP]),
 ]
@@ -113,6 +115,26 @@ def resample_filter(up: int, down: int):
     lib.tts_resample_filter(up, down, h, n, ctypes.byref(npr))
     import numpy as _np
     return _np.frombuffer(h, dtype=_np.float64).copy(), npr.value
+
+
+def set_switch(name: str, value: int = -1):
+    """Select an alternative kernel path process-wide (include/tts_hip.h tts_set_switch):
+    e.g. set_switch("TTS_REL_ATTN", 0) for the unfused attention; -1 restores the default."""
+    lib = load_library()
+    check(lib.tts_set_switch(name.encode(), int(value)), "tts_set_switch")
+
+
+@contextlib.contextmanager
+def switches(**values):
+    """Context manager form of set_switch: `with switches(TTS_MRF_CHAIN=0): ...`; every named
+    switch goes back to its default on exit."""
+    try:
+        for k, v in values.items():
+            set_switch(k, v)
+        yield
+    finally:
+        for k in values:
+            set_switch(k, -1)
 
 
 def check(rc: int, what: str = ""):
@@ -295,7 +317,7 @@ class HipEngine:
               "profile_read")
         return ms.value, fl.value, n.value
 
-    PROFILE_KINDS = ("conv_gemm_kernel", "conv_xres_kernel", "mrf_fused_kernel", "mrf_pair_kernel", "mrf_chain_kernel",
+    PROFILE_KINDS = ("conv_gemm_kernel", "conv_xres_kernel", "retired", "mrf_pair_kernel", "mrf_chain_kernel",
                      "upsample_stream_kernel", "conv_split_kernel")
 
     def profile_read_kinds(self):

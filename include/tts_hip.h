@@ -126,9 +126,16 @@ int tts_acoustic_speaker_dim(tts_engine* eng, int* dim);
 int tts_engine_profile(tts_engine* eng, int enable);
 int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops, int* n_launches);
 /* The same, split by kernel family into arrays of nkinds entries:
- * 0 = conv_gemm_kernel, 1 = conv_xres_kernel, 2 = mrf_fused_kernel, 3 = mrf_pair_kernel,
+ * 0 = conv_gemm_kernel, 1 = conv_xres_kernel, 2 = (retired: round 1's whole-stage kernel), 3 = mrf_pair_kernel,
  * 4 = mrf_chain_kernel, 5 = upsample_stream_kernel, 6 = conv_split_kernel. */
 int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, double* flops, int* n_launches);
+
+/* Process-wide switch selecting an alternative kernel path (A/B runs, the parity tests'
+ * reference paths): TTS_REL_ATTN, TTS_MRF_FUSED, TTS_MRF_CHAIN, TTS_POST_FUSE, TTS_UP_STREAM,
+ * TTS_CONV_XRES, TTS_XRES_NARROW, TTS_XRES_NT, TTS_CONV_WIDE, TTS_SPLIT_TILE, TTS_PAIR_DIV.  Each
+ * starts from its environment variable, read once; value -1 restores the built-in default.
+ * Applies to launches enqueued after the call (use from one thread while no forward runs). */
+int tts_set_switch(const char* name, int value);
 
 /* Rational-rate resampling of waveforms (22,050 -> 24,000 Hz for
  * clients that assume the reference's hard-coded 24 kHz, synthesizer.py:119 /

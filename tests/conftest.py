@@ -35,3 +35,19 @@ def pytest_sessionfinish(session, exitstatus):
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         with open(path, "w") as f:
             json.dump(recs, f, indent=1)
+
+
+@pytest.fixture
+def switch():
+    """set_switch(name, value) for one test (gonova_tts_amd.engine.set_switch: the process-wide
+    kernel-path switches of include/tts_hip.h); every switch it touched is reset afterwards."""
+    from gonova_tts_amd.engine import set_switch
+    touched = set()
+
+    def setter(name, value):
+        touched.add(name)
+        set_switch(name, -1 if value is None else int(value))
+
+    yield setter
+    for name in touched:
+        set_switch(name, -1)

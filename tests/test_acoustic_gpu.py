@@ -219,7 +219,7 @@ def test_generate_batch_mixed_voices_equals_single(spk_engine, tmp_path):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
-def test_fused_rel_attention_matches_unfused_and_oracle(aw, dtype, monkeypatch):
+def test_fused_rel_attention_matches_unfused_and_oracle(aw, dtype, switch):
     """The fused relative-position attention (attention.hip, default for 16-bit dtypes)
     against the four-launch path (TTS_REL_ATTN=0) and the oracle, on a ragged batch whose
     lengths cross the 64-query / 32-key tile edges (durations forced: predicted durations
@@ -228,9 +228,9 @@ def test_fused_rel_attention_matches_unfused_and_oracle(aw, dtype, monkeypatch):
     rng = np.random.default_rng(11)
     ids_list = [rng.integers(1, 78, size=n) for n in (40, 1, 17, 33)]
     durs = [np.full(len(x), 5) for x in ids_list]
-    monkeypatch.setenv("TTS_REL_ATTN", "1")
+    switch("TTS_REL_ATTN", 1)
     fused, lf, _ = run(eng, ids_list, t_cap=200, durations=durs)
-    monkeypatch.setenv("TTS_REL_ATTN", "0")
+    switch("TTS_REL_ATTN", 0)
     unfused, lu, _ = run(eng, ids_list, t_cap=200, durations=durs)
     tol = 2.5e-2 if dtype == "bf16" else 5e-3
     for b, ids in enumerate(ids_list):
@@ -244,7 +244,7 @@ def test_fused_rel_attention_matches_unfused_and_oracle(aw, dtype, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
-def test_short_row_tiles_bit_identical(aw, dtype, monkeypatch):
+def test_short_row_tiles_bit_identical(aw, dtype, switch):
     """conv_xres picks 64-row tiles where 128-row tiles would leave much of each utterance's
     last tile empty (the encoder's short token rows).  The channel group, and so the K order
     of the accumulation, is the same for both tile heights, so the mel matches the 128-row
@@ -256,15 +256,15 @@ def test_short_row_tiles_bit_identical(aw, dtype, monkeypatch):
     rng = np.random.default_rng(12)
     ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70)]
     durs = [np.full(len(x), 3) for x in ids_list]
-    monkeypatch.setenv("TTS_XRES_NARROW", "0")   # 128-channel tiles: the tile-height pair
-    monkeypatch.setenv("TTS_XRES_NT", "4")
+    switch("TTS_XRES_NARROW", 0)   # 128-channel tiles: the tile-height pair
+    switch("TTS_XRES_NT", 4)
     big, lb, _ = run(eng, ids_list, t_cap=432, durations=durs)
-    monkeypatch.setenv("TTS_XRES_NT", "2")
+    switch("TTS_XRES_NT", 2)
     small, ls, _ = run(eng, ids_list, t_cap=432, durations=durs)
-    monkeypatch.delenv("TTS_XRES_NT")
-    monkeypatch.setenv("TTS_XRES_NARROW", "1")   # 64 x 64 tiles wherever eligible
+    switch("TTS_XRES_NT", None)
+    switch("TTS_XRES_NARROW", 1)   # 64 x 64 tiles wherever eligible
     narrow, ln, _ = run(eng, ids_list, t_cap=432, durations=durs)
-    monkeypatch.delenv("TTS_XRES_NARROW")
+    switch("TTS_XRES_NARROW", None)
     auto, la, _ = run(eng, ids_list, t_cap=432, durations=durs)
     for b, ids in enumerate(ids_list):
         L = int(la[b])

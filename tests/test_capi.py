@@ -36,3 +36,14 @@ def test_parse_device():
     assert engine.parse_device("cuda") == 0
     with pytest.raises(ValueError):
         engine.parse_device("cpu")
+
+
+def test_switches_set_and_reset_without_gpu():
+    """tts_set_switch needs no device: known switches accept a value and -1 (default); an
+    unknown name is an error with a message."""
+    engine.set_switch("TTS_MRF_CHAIN", 0)
+    engine.set_switch("TTS_MRF_CHAIN", -1)
+    with engine.switches(TTS_PAIR_DIV=1, TTS_REL_ATTN=0):
+        pass
+    with pytest.raises(RuntimeError, match="unknown switch"):
+        engine.set_switch("TTS_NO_SUCH_SWITCH", 1)

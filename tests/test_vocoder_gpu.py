@@ -155,20 +155,18 @@ def test_vocoder_full_size_batch_invariance(vw):
     check("C2 full-size f16 utt 0 frames 100-300", wav[0, w0 * 256:w1 * 256].cpu().numpy(), ref, kind="voc_f16")
 
 
-@pytest.mark.parametrize("pair", ["1", "0"], ids=["pair", "stage"])
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-def test_fused_mrf_matches_unfused_path(vw, dtype, pair, monkeypatch):
-    """The fused MRF kernels of the C=64/32 stages -- ResBlock-pair kernels (default) and the
-    whole-stage kernel (TTS_MRF_PAIR=0) -- against the per-conv path on ragged input."""
+def test_fused_mrf_matches_unfused_path(vw, dtype, switch):
+    """The fused MRF kernels (ResBlock-pair and resblock-chain launches, the default) against
+    the per-conv path (TTS_MRF_FUSED=0) on ragged input."""
     eng = engine_for(dtype, vw)
     rng = np.random.default_rng(21)
     lens = [70, 3, 41, 66]
     mel = torch.from_numpy(rng.standard_normal((4, 70, 80)).astype(np.float32)).to(DEV)
     ln = torch.tensor(lens, dtype=torch.int32)
-    monkeypatch.setenv("TTS_MRF_FUSED", "1")
-    monkeypatch.setenv("TTS_MRF_PAIR", pair)
+    switch("TTS_MRF_FUSED", 1)
     fused = eng.vocoder(mel, ln).cpu().numpy()
-    monkeypatch.setenv("TTS_MRF_FUSED", "0")
+    switch("TTS_MRF_FUSED", 0)
     unfused = eng.vocoder(mel, ln).cpu().numpy()
     for b, L in enumerate(lens):
         e = rel_rms(fused[b, :L * 256], unfused[b, :L * 256])
@@ -177,7 +175,7 @@ def test_fused_mrf_matches_unfused_path(vw, dtype, pair, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-def test_resblock_chain_bit_identical_to_pairs(vw, dtype, monkeypatch):
+def test_resblock_chain_bit_identical_to_pairs(vw, dtype, switch):
     """The resblock chain kernel (three pairs in one launch: k=3 at C=32/64, k=7 at C=32)
     reproduces the three pair launches bit for bit, ragged utterances and tile edges included
     (first / last blocks of an utterance, one block shorter than the halo)."""
@@ -186,11 +184,10 @@ def test_resblock_chain_bit_identical_to_pairs(vw, dtype, monkeypatch):
     lens = [70, 1, 33, 64, 5]
     mel = torch.from_numpy(rng.standard_normal((5, 70, 80)).astype(np.float32)).to(DEV)
     ln = torch.tensor(lens, dtype=torch.int32)
-    monkeypatch.setenv("TTS_MRF_FUSED", "1")
-    monkeypatch.setenv("TTS_MRF_PAIR", "1")
-    monkeypatch.setenv("TTS_MRF_CHAIN", "1")
+    switch("TTS_MRF_FUSED", 1)
+    switch("TTS_MRF_CHAIN", 1)
     chain = eng.vocoder(mel, ln).cpu().numpy()
-    monkeypatch.setenv("TTS_MRF_CHAIN", "0")
+    switch("TTS_MRF_CHAIN", 0)
     pairs = eng.vocoder(mel, ln).cpu().numpy()
     for b, L in enumerate(lens):
         assert np.array_equal(chain[b], pairs[b]), (b, float(np.abs(chain[b] - pairs[b]).max()))
@@ -198,7 +195,7 @@ def test_resblock_chain_bit_identical_to_pairs(vw, dtype, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-def test_fused_conv_post_bit_identical(vw, dtype, monkeypatch):
+def test_fused_conv_post_bit_identical(vw, dtype, switch):
     """conv_post inside the last pair launch (its halo rows computed in the block, the final
     MRF sum never written) reproduces the separate conv_post launch bit for bit: ragged and
     empty utterances, a batch length that is not a whole number of 512-row tiles, utterances
@@ -208,9 +205,9 @@ def test_fused_conv_post_bit_identical(vw, dtype, monkeypatch):
     lens = [71, 1, 2, 0, 33, 64]
     mel = torch.from_numpy(rng.standard_normal((6, 71, 80)).astype(np.float32)).to(DEV)
     ln = torch.tensor(lens, dtype=torch.int32)
-    monkeypatch.setenv("TTS_POST_FUSE", "1")
+    switch("TTS_POST_FUSE", 1)
     fused = eng.vocoder(mel, ln).cpu().numpy()
-    monkeypatch.setenv("TTS_POST_FUSE", "0")
+    switch("TTS_POST_FUSE", 0)
     sep = eng.vocoder(mel, ln).cpu().numpy()
     for b, L in enumerate(lens):
         assert np.array_equal(fused[b], sep[b]), (b, float(np.abs(fused[b] - sep[b]).max()))
@@ -218,7 +215,7 @@ def test_fused_conv_post_bit_identical(vw, dtype, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-def test_short_pair_tiles_bit_identical(vw, dtype, monkeypatch):
+def test_short_pair_tiles_bit_identical(vw, dtype, switch):
     """Short pair tiles (picked for grids that leave most CUs idle, e.g. the streamed vocoder's
     stage 0) reproduce the full-height tiles bit for bit at every C (forced), ragged and empty
     utterances and tile edges included; the automatic choice agrees too."""
@@ -227,14 +224,14 @@ def test_short_pair_tiles_bit_identical(vw, dtype, monkeypatch):
     lens = [71, 1, 0, 33, 64]
     mel = torch.from_numpy(rng.standard_normal((5, 71, 80)).astype(np.float32)).to(DEV)
     ln = torch.tensor(lens, dtype=torch.int32)
-    monkeypatch.setenv("TTS_MRF_CHAIN", "0")     # every resblock as pair launches
-    monkeypatch.setenv("TTS_PAIR_DIV", "short")
+    switch("TTS_MRF_CHAIN", 0)     # every resblock as pair launches
+    switch("TTS_PAIR_DIV", 0)
     short = eng.vocoder(mel, ln).cpu().numpy()
-    monkeypatch.setenv("TTS_PAIR_DIV", "1")
+    switch("TTS_PAIR_DIV", 1)
     full = eng.vocoder(mel, ln).cpu().numpy()
-    monkeypatch.delenv("TTS_MRF_CHAIN")
+    switch("TTS_MRF_CHAIN", None)
     default_full = eng.vocoder(mel, ln).cpu().numpy()
-    monkeypatch.delenv("TTS_PAIR_DIV")
+    switch("TTS_PAIR_DIV", None)
     auto = eng.vocoder(mel, ln).cpu().numpy()
     for b, L in enumerate(lens):
         assert np.array_equal(short[b], full[b]), (b, float(np.abs(short[b] - full[b]).max()))
@@ -243,7 +240,7 @@ def test_short_pair_tiles_bit_identical(vw, dtype, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-def test_streaming_upsampler_matches_conv_path(vw, dtype, monkeypatch):
+def test_streaming_upsampler_matches_conv_path(vw, dtype, switch):
     """The streaming transposed-conv kernel of stages 2-3 (weights in LDS, B fragments straight
     from HBM, zero rows outside each utterance through the buffer descriptor) against the
     conv_xres polyphase path and the oracle: ragged and empty utterances, lengths that end
@@ -253,9 +250,9 @@ def test_streaming_upsampler_matches_conv_path(vw, dtype, monkeypatch):
     lens = [45, 1, 0, 17, 32]
     mel = torch.from_numpy(rng.standard_normal((5, 45, 80)).astype(np.float32)).to(DEV)
     ln = torch.tensor(lens, dtype=torch.int32)
-    monkeypatch.setenv("TTS_UP_STREAM", "1")
+    switch("TTS_UP_STREAM", 1)
     st = eng.vocoder(mel, ln).cpu().numpy()
-    monkeypatch.setenv("TTS_UP_STREAM", "0")
+    switch("TTS_UP_STREAM", 0)
     cv = eng.vocoder(mel, ln).cpu().numpy()
     tol = 2e-3 if dtype == "f16" else 1.5e-2
     for b, L in enumerate(lens):

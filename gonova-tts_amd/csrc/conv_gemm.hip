@@ -642,6 +642,14 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
   constexpr int CKW = 64 / (int)sizeof(T);   // 32 x 16-bit / 16 x f32 (64-byte rows)
   constexpr int CKWW = 128 / (int)sizeof(T); // 64 x 16-bit / 32 x f32 (128-byte rows)
   const bool wide = wide_mode() && p.Cin % CKWW == 0 && p.Cin >= 2 * CKWW;
+  // fp32 head-batched attention products of the exact-duration encoder (M = 144-288 keys /
+  // 192 channels, K = 144-192, 144 query rows, batch x heads): when the 128 x 128 grid would
+  // fill under half the CUs (batch 8: 64 blocks), 64 x 64 tiles with 128-byte channel chunks,
+  // one 32 x 32 MFMA tile per wave.  Measured at batch 8: the 12 launches 443 -> 289 us; at
+  // batch 32 (256 blocks) the small tiles were slower (522 -> 585 us), so the rule.
+  if constexpr (sizeof(T) == 4)
+    if (p.nh > 1 && (long long)((p.y_rows + 127) / 128) * ((p.M + 127) / 128) * p.B * p.nh < 128)
+      return p.Cin % 32 == 0 ? launch_cfg<T, 1, 1, 2, 2, 32>(p, s) : launch_cfg<T, 1, 1, 2, 2, CKW>(p, s);
   if (p.M <= 32) {
     if (wide) return launch_cfg<T, 1, 2, 1, 4, CKWW>(p, s);
     return launch_cfg<T, 1, 2, 1, 4, CKW>(p, s);

@@ -84,6 +84,18 @@ struct ChainGeom<64, 3> { static constexpr int BN = TTS_CHAIN_BN64_3, OCC = TTS_
 template <>
 struct ChainGeom<64, 7> { static constexpr int BN = TTS_CHAIN_BN64_7, OCC = TTS_CHAIN_OCC64_7; };
 
+#ifndef TTS_CHAIN_C128K3
+#define TTS_CHAIN_C128K3 0         // chain the k = 3 resblock at C = 128 too
+#endif
+#ifndef TTS_CHAIN_BN128_3
+#define TTS_CHAIN_BN128_3 96
+#endif
+#ifndef TTS_CHAIN_OCC128_3
+#define TTS_CHAIN_OCC128_3 2
+#endif
+template <>
+struct ChainGeom<128, 3> { static constexpr int BN = TTS_CHAIN_BN128_3, OCC = TTS_CHAIN_OCC128_3; };
+
 constexpr int CHAIN_D0 = 1, CHAIN_D1 = 3, CHAIN_D2 = 5;  // HiFi-GAN V1/V2 dilations
 
 template <int C, int K>
@@ -339,7 +351,7 @@ bool mrf_chain_supported(int dtype, int C, int k, const int* dil, int npair) {
   if (!(dtype == DT_F16 || dtype == DT_BF16) || npair != 3) return false;
   if (dil[0] != CHAIN_D0 || dil[1] != CHAIN_D1 || dil[2] != CHAIN_D2) return false;
   return (C == 32 && (k == 3 || k == 7 || (TTS_CHAIN_C32K11 && k == 11))) ||
-         (C == 64 && (k == 3 || (TTS_CHAIN_C64K7 && k == 7)));
+         (C == 64 && (k == 3 || (TTS_CHAIN_C64K7 && k == 7))) || (TTS_CHAIN_C128K3 && C == 128 && k == 3);
 }
 
 hipError_t mrf_chain_launch(int dtype, int C, int k, const MrfChainParams& p, hipStream_t s) {
@@ -351,6 +363,9 @@ hipError_t mrf_chain_launch(int dtype, int C, int k, const MrfChainParams& p, hi
   if (C == 32 && k == 11) return f16 ? launch_chain_t<half_t, 32, 11>(p, s) : launch_chain_t<bf16_t, 32, 11>(p, s);
 #endif
   if (C == 64 && k == 3) return f16 ? launch_chain_t<half_t, 64, 3>(p, s) : launch_chain_t<bf16_t, 64, 3>(p, s);
+#if TTS_CHAIN_C128K3
+  if (C == 128 && k == 3) return f16 ? launch_chain_t<half_t, 128, 3>(p, s) : launch_chain_t<bf16_t, 128, 3>(p, s);
+#endif
 #if TTS_CHAIN_C64K7
   if (C == 64 && k == 7) return f16 ? launch_chain_t<half_t, 64, 7>(p, s) : launch_chain_t<bf16_t, 64, 7>(p, s);
 #endif

@@ -88,13 +88,16 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
   // (block slot sb <-> m = i0 - j0 - 31 + sb, 96 rows) lives in a 96-row ring indexed by
   // m mod 96: a step shifts the window by 32, so only the 32 rows entering it are loaded,
   // into the slots of the 32 that left.  Loads for step s+1 are issued before step s's
-  // MFMAs (registers) and written to LDS after the barrier that ends step s.
+  // MFMAs (registers, pinned there by a scheduling barrier) and written to LDS after the
+  // barrier that ends step s -- on every step, the last one included, so the loads are
+  // consumed unconditionally (consumed only under a branch, they were sunk into it and
+  // their latency was exposed once per step)
   constexpr int KP = AT_BK * (DK / 8) / 256;   // 16-byte pieces per thread: K, Vt, new R rows
   static_assert(AT_BK * (DK / 8) % 256 == 0 && DK * (AT_BK / 8) % 256 == 0, "staging split");
   auto rslot = [](int m) { const int r = m % AT_RW; return r < 0 ? r + AT_RW : r; };
   auto rrow = [&](int m) { return min(max(rmax - 1 - m, 0), 2 * rmax - 1); };
-  uint4 pkv[KP], pvt[KP], prr[KP];
-  auto stage_load = [&](int j0, bool first) __attribute__((always_inline)) {
+  u32x4 pkv[KP], pvt[KP], prr[KP];
+  auto load_kv = [&](int j0) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
       const int p = tid + 256 * i;
@@ -103,29 +106,41 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
       // addresses clamped into the buffers and the loads consumed unconditionally (a load under
       // a branch or consumed only under a mask makes the waitcnt pass drain vmcnt); keys past
       // len are masked out of the softmax, so their K / Vt only have to be finite
-      const uint4 kv = *reinterpret_cast<const uint4*>(qkv + ((long long)b * Tp + min(j, Tp - 1)) * 3 * rowD + D + h * DK + c * 8);
-      pkv[i] = j < len ? kv : uint4{0u, 0u, 0u, 0u};
+      pkv[i] = *reinterpret_cast<const u32x4*>(qkv + ((long long)b * Tp + min(j, Tp - 1)) * 3 * rowD + D + h * DK + c * 8);
       const int d = p / (AT_BK / 8), cv = p - d * (AT_BK / 8);
       const int jv = j0 + cv * 8;  // Vt is zero past len (transpose_v) and padded to Sk
-      const uint4 vv = *reinterpret_cast<const uint4*>(vt + (((long long)b * H + h) * DK + d) * Sk + min(jv, Sk - 8));
-      pvt[i] = jv < Sk ? vv : uint4{0u, 0u, 0u, 0u};
-      // R rows entering the window: m = i0 - j0 - 31 + [0, 32) (the first step loads all 96 below)
-      const int m = i0 - j0 - (AT_BK - 1) + r;
-      if (!first) prr[i] = *reinterpret_cast<const uint4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 8);
+      pvt[i] = *reinterpret_cast<const u32x4*>(vt + (((long long)b * H + h) * DK + d) * Sk + min(jv, Sk - 8));
     }
   };
-  auto stage_write = [&](int j0, bool first) __attribute__((always_inline)) {
+  auto load_r = [&](int j0) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
       const int p = tid + 256 * i;
       const int r = p / (DK / 8), c = p - r * (DK / 8);
-      *reinterpret_cast<uint4*>(Ks + r * KR + c * 16) = pkv[i];
+      // R rows entering the window: m = i0 - j0 - 31 + [0, 32)
+      const int m = i0 - j0 - (AT_BK - 1) + r;
+      prr[i] = *reinterpret_cast<const u32x4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 8);
+    }
+  };
+  // the zero masks are applied here, after the step's MFMAs (applied at the loads, they pulled
+  // the loads' waits into the step)
+  auto write_kv = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int p = tid + 256 * i;
+      const int r = p / (DK / 8), c = p - r * (DK / 8);
+      *reinterpret_cast<u32x4*>(Ks + r * KR + c * 16) = j0 + r < len ? pkv[i] : u32x4{};
       const int d = p / (AT_BK / 8), cv = p - d * (AT_BK / 8);
-      *reinterpret_cast<uint4*>(Vs + d * VR + cv * 16) = pvt[i];
-      if (!first) {
-        const int m = i0 - j0 - (AT_BK - 1) + r;
-        *reinterpret_cast<uint4*>(Rs + rslot(m) * KR + c * 16) = prr[i];
-      }
+      *reinterpret_cast<u32x4*>(Vs + d * VR + cv * 16) = j0 + cv * 8 < Sk ? pvt[i] : u32x4{};
+    }
+  };
+  auto write_r = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int p = tid + 256 * i;
+      const int r = p / (DK / 8), c = p - r * (DK / 8);
+      const int m = i0 - j0 - (AT_BK - 1) + r;
+      *reinterpret_cast<u32x4*>(Rs + rslot(m) * KR + c * 16) = prr[i];
     }
   };
   // first step: the whole 96-row R window
@@ -135,13 +150,14 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
     *reinterpret_cast<uint4*>(Rs + rslot(m) * KR + c * 16) =
         *reinterpret_cast<const uint4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 8);
   }
-  stage_load(0, true);
-  stage_write(0, true);
+  load_kv(0);
+  write_kv(0);
   __syncthreads();
 
   for (int j0 = 0; j0 < len; j0 += AT_BK) {
-    const bool more = j0 + AT_BK < len;
-    stage_load(j0 + AT_BK, false);  // in flight during this step's MFMAs (the last step's is unused)
+    load_kv(j0 + AT_BK);  // in flight during this step's MFMAs (the last step's are written, unused)
+    load_r(j0 + AT_BK);
+    __builtin_amdgcn_sched_barrier(0);
     const int mbw = i0w - j0 - (AT_BK - 1);  // m of this wave's G slot 0
     // S^T tiles (keys 16 kt + 4g + e, query q) and G^T tiles (slots 16 t + 4g + e)
     f32x4 sacc[2] = {f32x4{}, f32x4{}};
@@ -186,18 +202,22 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
     const float m_new = fmaxf(m_run, mloc);
     const float alpha = exp2f(m_run - m_new);  // m_run = -inf on the first step: alpha = 0
     float lsum = 0.f;
-    T pk[8];
+    f32x4 pe0, pe1;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float pe = exp2f(sv[e] - m_new);
-      pk[e] = (T)pe;
-      lsum += (float)pk[e];  // normalise with the rounded probabilities P.V uses
+    for (int e = 0; e < 4; ++e) {
+      pe0[e] = exp2f(sv[e] - m_new);
+      pe1[e] = exp2f(sv[4 + e] - m_new);
     }
+    // normalise with the rounded probabilities P.V uses (keys in the order e = 0 .. 7)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lsum += (float)(T)pe0[e];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lsum += (float)(T)pe1[e];
     lsum += __shfl_xor(lsum, 16);
     lsum += __shfl_xor(lsum, 32);
     l_run = l_run * alpha + lsum;
     m_run = m_new;
-    const Frag bp = *reinterpret_cast<const Frag*>(pk);
+    const Frag bp = __builtin_bit_cast(Frag, pack8<T>(pe0, pe1));
     // O^T += Vt . P^T with the permuted key order of bp
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
@@ -207,11 +227,10 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
       const uint4 av = uint4{lo.x, lo.y, hi.x, hi.y};
       oacc[t] = MF::mma(*reinterpret_cast<const Frag*>(&av), bp, oacc[t] * alpha);
     }
-    if (more) {
-      __syncthreads();  // every wave is done with this step's K / Vt and the leaving R rows
-      stage_write(j0 + AT_BK, false);
-      __syncthreads();
-    }
+    __syncthreads();  // every wave is done with this step's K / Vt and the leaving R rows
+    write_kv(j0 + AT_BK);
+    write_r(j0 + AT_BK);
+    __syncthreads();
   }
   // O[i][h*dk + d] = O^T[d][i] / l
   const int i = i0w + q;
@@ -227,6 +246,201 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
   }
 }
 
+// fp32 form (the exact-duration encoder, acoustic.cpp): the same flash schedule and index map
+// on v_mfma_f32_16x16x4_f32 (exact f32 products, fp32 accumulation -- the unfused fp32 path's
+// arithmetic up to summation order), P kept in fp32.  The dk index of each 4-deep k-step is
+// permuted (lane group g holds d = 16u + 4g + e for k-step 4u + e) so every A fragment of four
+// k-steps is one 16-byte LDS read and every Q fragment one 16-byte global load.  LDS holds fp32
+// K / Vt / R (140 KB): one block per CU.
+template <int DK>
+__global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __restrict__ pu, const float* __restrict__ pv,
+                                                             const float* __restrict__ qkv, const float* __restrict__ vt,
+                                                             const float* __restrict__ ptab, const int* __restrict__ lens,
+                                                             int Tp, int D, int H, int Sk, int rmax, float scale,
+                                                             float* __restrict__ out, int nqb, int nbatch) {
+  constexpr int KU = DK / 16;         // 16-wide dk chunks (4 k-steps each); also O^T tiles
+  constexpr int KR = DK * 4 + 16;     // K / R row stride in LDS (bytes; odd 16-byte slots)
+  constexpr int VR = AT_BK * 4 + 16;  // Vt row stride (144 B)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Ks = smem;                                  // [32 keys][DK]
+  char* Vs = Ks + AT_BK * KR;                       // [DK][32 keys]
+  char* Rs = Vs + DK * VR;                          // [96 slots][DK]
+  float* Gs = reinterpret_cast<float*>(Rs + AT_RW * KR);  // [4 waves][48 slots][16 q]
+
+  int bh, qb;
+  if (!xcd_tile(nqb, H * nbatch, bh, qb)) return;
+  const int b = bh / H, h = bh - b * H;
+  const int i0 = qb * AT_BQ;
+  const int len = lens[b];
+  if (i0 >= len) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane & 15, g = lane >> 4;
+  const int i0w = i0 + 16 * w;
+  const long long rowD = D;
+  const int iq = min(i0w + q, Tp - 1);
+  // Qu = q + pos_bias_u, Qv = q + pos_bias_v (HF:420-423) in fp32, as pos_bias_kernel<float>
+  f32x4 bu[KU], bv[KU];
+#pragma unroll
+  for (int u = 0; u < KU; ++u) {
+    const int c = h * DK + 16 * u + 4 * g;
+    const f32x4 qv = *reinterpret_cast<const f32x4*>(qkv + ((long long)b * Tp + iq) * 3 * rowD + c);
+    bu[u] = qv + *reinterpret_cast<const f32x4*>(pu + c);
+    bv[u] = qv + *reinterpret_cast<const f32x4*>(pv + c);
+  }
+  f32x4 oacc[KU];
+#pragma unroll
+  for (int t = 0; t < KU; ++t) oacc[t] = f32x4{};
+  float m_run = -INFINITY, l_run = 0.f;
+  const float sl2 = scale * 1.4426950408889634f;
+  float* gw = Gs + w * 48 * 16;
+
+  // staging as the 16-bit kernel: loads for step s+1 in flight during step s, written after
+  // the barrier that ends it (every step), masks applied at the write
+  constexpr int KP = AT_BK * (DK / 4) / 256;  // 16-byte pieces per thread: K, Vt, new R rows
+  static_assert(AT_BK * (DK / 4) % 256 == 0 && DK * (AT_BK / 4) % 256 == 0, "staging split");
+  auto rslot = [](int m) { const int r = m % AT_RW; return r < 0 ? r + AT_RW : r; };
+  auto rrow = [&](int m) { return min(max(rmax - 1 - m, 0), 2 * rmax - 1); };
+  f32x4 pkv[KP], pvt[KP], prr[KP];
+  auto load_kv = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int p = tid + 256 * i;
+      const int r = p / (DK / 4), c = p - r * (DK / 4);
+      pkv[i] = *reinterpret_cast<const f32x4*>(qkv + ((long long)b * Tp + min(j0 + r, Tp - 1)) * 3 * rowD + D + h * DK + c * 4);
+      const int d = p / (AT_BK / 4), cv = p - d * (AT_BK / 4);
+      pvt[i] = *reinterpret_cast<const f32x4*>(vt + (((long long)b * H + h) * DK + d) * Sk + min(j0 + cv * 4, Sk - 4));
+    }
+  };
+  auto load_r = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int p = tid + 256 * i;
+      const int r = p / (DK / 4), c = p - r * (DK / 4);
+      prr[i] = *reinterpret_cast<const f32x4*>(ptab + (long long)rrow(i0 - j0 - (AT_BK - 1) + r) * rowD + h * DK + c * 4);
+    }
+  };
+  auto write_kv = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int p = tid + 256 * i;
+      const int r = p / (DK / 4), c = p - r * (DK / 4);
+      *reinterpret_cast<f32x4*>(Ks + r * KR + c * 16) = j0 + r < len ? pkv[i] : f32x4{};
+      const int d = p / (AT_BK / 4), cv = p - d * (AT_BK / 4);
+      *reinterpret_cast<f32x4*>(Vs + d * VR + cv * 16) = j0 + cv * 4 < Sk ? pvt[i] : f32x4{};
+    }
+  };
+  auto write_r = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int p = tid + 256 * i;
+      const int r = p / (DK / 4), c = p - r * (DK / 4);
+      *reinterpret_cast<f32x4*>(Rs + rslot(i0 - j0 - (AT_BK - 1) + r) * KR + c * 16) = prr[i];
+    }
+  };
+  for (int p = tid; p < AT_RW * (DK / 4); p += 256) {
+    const int sb = p / (DK / 4), c = p - sb * (DK / 4);
+    const int m = i0 - (AT_BK - 1) + sb;
+    *reinterpret_cast<f32x4*>(Rs + rslot(m) * KR + c * 16) =
+        *reinterpret_cast<const f32x4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 4);
+  }
+  load_kv(0);
+  write_kv(0);
+  __syncthreads();
+
+  for (int j0 = 0; j0 < len; j0 += AT_BK) {
+    load_kv(j0 + AT_BK);
+    load_r(j0 + AT_BK);
+    __builtin_amdgcn_sched_barrier(0);
+    const int mbw = i0w - j0 - (AT_BK - 1);
+    f32x4 sacc[2] = {f32x4{}, f32x4{}};
+    f32x4 gacc[3] = {f32x4{}, f32x4{}, f32x4{}};
+    int rs[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) rs[t] = rslot(mbw + 16 * t + q) * KR;
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      f32x4 a[5];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) a[kt] = *reinterpret_cast<const f32x4*>(Ks + (16 * kt + q) * KR + (16 * u + 4 * g) * 4);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) a[2 + t] = *reinterpret_cast<const f32x4*>(Rs + rs[t] + (16 * u + 4 * g) * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) sacc[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kt][e], bu[u][e], sacc[kt], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) gacc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2 + t][e], bv[u][e], gacc[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gw[(16 * t + 4 * g + e) * 16 + q] = gacc[t][e];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's scratch writes landed
+    __builtin_amdgcn_wave_barrier();
+    float sv[8];
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kk = 16 * kt + 4 * g + e;
+        const float bd = gw[(q - kk + AT_BK - 1) * 16 + q];
+        float sc = (sacc[kt][e] + bd) * sl2;
+        if (j0 + kk >= len) sc = -INFINITY;
+        sv[4 * kt + e] = sc;
+        mloc = fmaxf(mloc, sc);
+      }
+    __builtin_amdgcn_wave_barrier();
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+    const float m_new = fmaxf(m_run, mloc);
+    const float alpha = exp2f(m_run - m_new);
+    f32x4 pe[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pe[kt][e] = exp2f(sv[4 * kt + e] - m_new);
+    float lsum = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) lsum += pe[e >> 2][e & 3];
+    lsum += __shfl_xor(lsum, 16);
+    lsum += __shfl_xor(lsum, 32);
+    l_run = l_run * alpha + lsum;
+    m_run = m_new;
+    // O^T += Vt . P^T: k-step (kt, e) has lane group g on key 16 kt + 4 g + e, the lane's own pe
+#pragma unroll
+    for (int t = 0; t < KU; ++t) {
+      f32x4 o = oacc[t] * alpha;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(Vs + (16 * t + q) * VR + (16 * kt + 4 * g) * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], pe[kt][e], o, 0, 0, 0);
+      }
+      oacc[t] = o;
+    }
+    __syncthreads();
+    write_kv(j0 + AT_BK);
+    write_r(j0 + AT_BK);
+    __syncthreads();
+  }
+  const int i = i0w + q;
+  if (i < len) {
+    const float inv = 1.f / l_run;
+    float* orow = out + ((long long)b * Tp + i) * rowD + h * DK;
+#pragma unroll
+    for (int t = 0; t < KU; ++t) *reinterpret_cast<f32x4*>(orow + 16 * t + 4 * g) = oacc[t] * inv;
+  }
+}
+
+template <int DK>
+size_t rel_attn_f32_lds() {
+  return (size_t)AT_BK * (DK * 4 + 16) + (size_t)DK * (AT_BK * 4 + 16) + (size_t)AT_RW * (DK * 4 + 16) +
+         (size_t)4 * 48 * 16 * 4;
+}
+
 template <int DK>
 size_t rel_attn_lds() {
   return (size_t)AT_BK * (DK * 2 + 16) + (size_t)DK * (AT_BK * 2 + 16) + (size_t)AT_RW * (DK * 2 + 16) +
@@ -236,7 +450,7 @@ size_t rel_attn_lds() {
 }  // namespace
 
 bool rel_attn_supported(int dt, int D, int H) {
-  return (dt == DT_F16 || dt == DT_BF16) && H > 0 && D % H == 0 && D / H == 192;
+  return (dt == DT_F16 || dt == DT_BF16 || dt == DT_F32) && H > 0 && D % H == 0 && D / H == 192;
 }
 
 hipError_t launch_rel_attn(int dt, const float* pos_u, const float* pos_v, const void* qkv, const void* vt, const void* ptab,
@@ -245,6 +459,12 @@ hipError_t launch_rel_attn(int dt, const float* pos_u, const float* pos_v, const
   if (!rel_attn_supported(dt, D, H) || Tm > rmax || Sk % 8) return hipErrorInvalidValue;
   const int nqb = (Tm + AT_BQ - 1) / AT_BQ;
   dim3 grid(xcd_grid(nqb, H * B));
+  if (dt == DT_F32) {
+    hipLaunchKernelGGL((rel_attn_f32_kernel<192>), grid, dim3(256), rel_attn_f32_lds<192>(), s, pos_u, pos_v,
+                       (const float*)qkv, (const float*)vt, (const float*)ptab, lens, Tp, D, H, Sk, rmax, scale,
+                       (float*)out, nqb, B);
+    return hipGetLastError();
+  }
   const size_t lds = rel_attn_lds<192>();
   if (dt == DT_F16)
     hipLaunchKernelGGL((rel_attn_kernel<half_t, 192>), grid, dim3(256), lds, s, pos_u, pos_v,

@@ -22,6 +22,9 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// 16-byte staging registers: a native vector, so a global -> register -> LDS copy is a plain
+// load / store pair (a uint4 struct copy becomes a memcpy that can land in scratch)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
 // MFMA traits: one 32x32 output tile per wave-instruction.

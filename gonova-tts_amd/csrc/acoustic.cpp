@@ -393,7 +393,10 @@ struct AcousticModel::Impl {
       HIP_CHECK(launch_transpose_v(dt, QKV, lens, B, Tp, D, H, Sk, Vt, s));
       if (fused_attn) {
         // fused flash-style relative-position attention (attention.hip); Qu / Qv formed in it
-        HIP_CHECK(launch_rel_attn(dt, L.pos_u, L.pos_v, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale, O, s));
+        // fp32 layers of a 16-bit model (the exact-duration encoder) in split precision, like their GEMMs
+        const bool split = dt == DT_F32 && this->dt != DT_F32 && sw(SW_ATTN_SPLIT) != 0;
+        HIP_CHECK(launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale,
+                                  O, s));
         run(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
         ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s);
         conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);

@@ -31,10 +31,11 @@ hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, in
 hipError_t launch_spk_bias(int dt, const float* e, int B, int E, const float* We, const float* bias, int D, void* out,
                            hipStream_t s);
 
-// attention.hip: fused relative-position attention (16-bit dtypes, dk = 192)
+// attention.hip: fused relative-position attention (dk = 192): 16-bit dtypes, fp32 (exact f32
+// MFMA) and, with split set, fp32 in split precision (three f16 MFMAs per product)
 bool rel_attn_supported(int dt, int D, int H);
-hipError_t launch_rel_attn(int dt, const float* pos_u, const float* pos_v, const void* qkv, const void* vt, const void* ptab,
-                           const int* lens, int B, int Tm, int Tp, int D, int H, int Sk, int rmax, float scale,
-                           void* out, hipStream_t s);
+hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* pos_v, const void* qkv, const void* vt,
+                           const void* ptab, const int* lens, int B, int Tm, int Tp, int D, int H, int Sk, int rmax,
+                           float scale, void* out, hipStream_t s);
 
 }  // namespace tts

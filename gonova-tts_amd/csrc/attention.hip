@@ -435,6 +435,243 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
   }
 }
 
+// Split-precision form (the fp32 encoder of a 16-bit model, acoustic.cpp): every fp32 operand
+// x is staged as two f16 planes, x_hi = f16(x) and x_lo = f16((x - x_hi) * 2^11), and each
+// product runs as three v_mfma_f32_16x16x32_f16 (hi.hi into one accumulator, hi.lo + lo.hi
+// into a second, scaled by 2^-11 when read) -- conv_split.hip's scheme, ~2^-21 relative per
+// product, at 126 MFMA issues of 16 cycles per 32-key step where the f32 form needs 336 of 32.
+// P is split the same way (P.V keeps fp32 accuracy); the softmax statistics are fp32.  Same
+// schedule, index map and operand layouts as the 16-bit kernel; LDS holds both planes of K /
+// Vt / R (142 KB): one block per CU.
+constexpr float AT_SPLIT = 2048.f;  // 2^11
+
+__device__ inline void at_split4(f32x4 v, uint2& hi, uint2& lo) {
+  const half4 h = __builtin_convertvector(v, half4);
+  const half4 l = __builtin_convertvector((v - __builtin_convertvector(h, f32x4)) * AT_SPLIT, half4);
+  hi = __builtin_bit_cast(uint2, h);
+  lo = __builtin_bit_cast(uint2, l);
+}
+
+__device__ inline void at_split8(f32x4 a, f32x4 b, half8& hi, half8& lo) {
+  uint2 h0, l0, h1, l1;
+  at_split4(a, h0, l0);
+  at_split4(b, h1, l1);
+  hi = __builtin_bit_cast(half8, uint4{h0.x, h0.y, h1.x, h1.y});
+  lo = __builtin_bit_cast(half8, uint4{l0.x, l0.y, l1.x, l1.y});
+}
+
+template <int DK>
+__global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __restrict__ pu, const float* __restrict__ pv,
+                                                               const float* __restrict__ qkv, const float* __restrict__ vt,
+                                                               const float* __restrict__ ptab, const int* __restrict__ lens,
+                                                               int Tp, int D, int H, int Sk, int rmax, float scale,
+                                                               float* __restrict__ out, int nqb, int nbatch) {
+  using MF = Mfma16<half_t>;
+  typedef half8 Frag;
+  constexpr int KS = DK / 32;         // k-steps over dk
+  constexpr int DT = DK / 16;         // 16-row tiles of dk (O^T)
+  constexpr int KR = DK * 2 + 16;     // K / R plane row stride (bytes; odd 16-byte slots)
+  constexpr int VR = AT_BK * 2 + 16;  // Vt plane row stride (80 B)
+  constexpr int KPL = AT_BK * KR, VPL = DK * VR, RPL = AT_RW * KR;  // plane sizes (lo = hi + size)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Ks = smem;                                        // 2 x [32 keys][DK]
+  char* Vs = Ks + 2 * KPL;                                // 2 x [DK][32 keys]
+  char* Rs = Vs + 2 * VPL;                                // 2 x [96 slots][DK]
+  float* Gs = reinterpret_cast<float*>(Rs + 2 * RPL);     // [4 waves][48 slots][16 q]
+
+  int bh, qb;
+  if (!xcd_tile(nqb, H * nbatch, bh, qb)) return;
+  const int b = bh / H, h = bh - b * H;
+  const int i0 = qb * AT_BQ;
+  const int len = lens[b];
+  if (i0 >= len) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane & 15, g = lane >> 4;
+  const int i0w = i0 + 16 * w;
+  const long long rowD = D;
+  const int iq = min(i0w + q, Tp - 1);
+  // Qu = q + pos_bias_u, Qv = q + pos_bias_v (HF:420-423) in fp32, then split
+  Frag bu[KS], bul[KS], bv[KS], bvl[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int c = h * DK + ks * 32 + 8 * g;
+    const float* qr = qkv + ((long long)b * Tp + iq) * 3 * rowD + c;
+    const f32x4 q0 = *reinterpret_cast<const f32x4*>(qr), q1 = *reinterpret_cast<const f32x4*>(qr + 4);
+    at_split8(q0 + *reinterpret_cast<const f32x4*>(pu + c), q1 + *reinterpret_cast<const f32x4*>(pu + c + 4), bu[ks], bul[ks]);
+    at_split8(q0 + *reinterpret_cast<const f32x4*>(pv + c), q1 + *reinterpret_cast<const f32x4*>(pv + c + 4), bv[ks], bvl[ks]);
+  }
+  f32x4 oacc[DT], oaccx[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) { oacc[t] = f32x4{}; oaccx[t] = f32x4{}; }
+  float m_run = -INFINITY, l_run = 0.f;
+  const float sl2 = scale * 1.4426950408889634f;
+  float* gw = Gs + w * 48 * 16;
+
+  // staging: fp32 pieces loaded for step s+1 during step s, split into the two planes after
+  // the barrier that ends it (every step), masks applied there
+  constexpr int KP = AT_BK * (DK / 4) / 256;
+  static_assert(AT_BK * (DK / 4) % 256 == 0 && DK * (AT_BK / 4) % 256 == 0, "staging split");
+  auto rslot = [](int m) { const int r = m % AT_RW; return r < 0 ? r + AT_RW : r; };
+  auto rrow = [&](int m) { return min(max(rmax - 1 - m, 0), 2 * rmax - 1); };
+  auto put = [](char* plane_hi, int plane, int off, f32x4 v) __attribute__((always_inline)) {
+    uint2 hi, lo;
+    at_split4(v, hi, lo);
+    *reinterpret_cast<uint2*>(plane_hi + off) = hi;
+    *reinterpret_cast<uint2*>(plane_hi + plane + off) = lo;
+  };
+  f32x4 pkv[KP], pvt[KP], prr[KP];
+  auto load_kv = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int p = tid + 256 * i;
+      const int r = p / (DK / 4), c = p - r * (DK / 4);
+      pkv[i] = *reinterpret_cast<const f32x4*>(qkv + ((long long)b * Tp + min(j0 + r, Tp - 1)) * 3 * rowD + D + h * DK + c * 4);
+      const int d = p / (AT_BK / 4), cv = p - d * (AT_BK / 4);
+      pvt[i] = *reinterpret_cast<const f32x4*>(vt + (((long long)b * H + h) * DK + d) * Sk + min(j0 + cv * 4, Sk - 4));
+    }
+  };
+  auto load_r = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int p = tid + 256 * i;
+      const int r = p / (DK / 4), c = p - r * (DK / 4);
+      prr[i] = *reinterpret_cast<const f32x4*>(ptab + (long long)rrow(i0 - j0 - (AT_BK - 1) + r) * rowD + h * DK + c * 4);
+    }
+  };
+  auto write_kv = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int p = tid + 256 * i;
+      const int r = p / (DK / 4), c = p - r * (DK / 4);
+      put(Ks, KPL, r * KR + c * 8, j0 + r < len ? pkv[i] : f32x4{});
+      const int d = p / (AT_BK / 4), cv = p - d * (AT_BK / 4);
+      put(Vs, VPL, d * VR + cv * 8, j0 + cv * 4 < Sk ? pvt[i] : f32x4{});
+    }
+  };
+  auto write_r = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int p = tid + 256 * i;
+      const int r = p / (DK / 4), c = p - r * (DK / 4);
+      put(Rs, RPL, rslot(i0 - j0 - (AT_BK - 1) + r) * KR + c * 8, prr[i]);
+    }
+  };
+  for (int p = tid; p < AT_RW * (DK / 4); p += 256) {
+    const int sb = p / (DK / 4), c = p - sb * (DK / 4);
+    const int m = i0 - (AT_BK - 1) + sb;
+    put(Rs, RPL, rslot(m) * KR + c * 8, *reinterpret_cast<const f32x4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 4));
+  }
+  load_kv(0);
+  write_kv(0);
+  __syncthreads();
+
+  for (int j0 = 0; j0 < len; j0 += AT_BK) {
+    load_kv(j0 + AT_BK);
+    load_r(j0 + AT_BK);
+    __builtin_amdgcn_sched_barrier(0);
+    const int mbw = i0w - j0 - (AT_BK - 1);
+    f32x4 sacc[2] = {f32x4{}, f32x4{}}, saccx[2] = {f32x4{}, f32x4{}};
+    f32x4 gacc[3] = {f32x4{}, f32x4{}, f32x4{}}, gaccx[3] = {f32x4{}, f32x4{}, f32x4{}};
+    int rs[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) rs[t] = rslot(mbw + 16 * t + q) * KR;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int co = (ks * 32 + 8 * g) * 2;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const char* kr = Ks + (16 * kt + q) * KR + co;
+        const Frag ah = *reinterpret_cast<const Frag*>(kr), al = *reinterpret_cast<const Frag*>(kr + KPL);
+        sacc[kt] = MF::mma(ah, bu[ks], sacc[kt]);
+        saccx[kt] = MF::mma(ah, bul[ks], saccx[kt]);
+        saccx[kt] = MF::mma(al, bu[ks], saccx[kt]);
+      }
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const char* rr = Rs + rs[t] + co;
+        const Frag ah = *reinterpret_cast<const Frag*>(rr), al = *reinterpret_cast<const Frag*>(rr + RPL);
+        gacc[t] = MF::mma(ah, bv[ks], gacc[t]);
+        gaccx[t] = MF::mma(ah, bvl[ks], gaccx[t]);
+        gaccx[t] = MF::mma(al, bv[ks], gaccx[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const f32x4 gv = gacc[t] + gaccx[t] * (1.f / AT_SPLIT);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gw[(16 * t + 4 * g + e) * 16 + q] = gv[e];
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's scratch writes landed
+    __builtin_amdgcn_wave_barrier();
+    float sv[8];
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const f32x4 s4 = sacc[kt] + saccx[kt] * (1.f / AT_SPLIT);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kk = 16 * kt + 4 * g + e;
+        const float bd = gw[(q - kk + AT_BK - 1) * 16 + q];
+        float sc = (s4[e] + bd) * sl2;
+        if (j0 + kk >= len) sc = -INFINITY;
+        sv[4 * kt + e] = sc;
+        mloc = fmaxf(mloc, sc);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+    const float m_new = fmaxf(m_run, mloc);
+    const float alpha = exp2f(m_run - m_new);
+    f32x4 pe0, pe1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      pe0[e] = exp2f(sv[e] - m_new);
+      pe1[e] = exp2f(sv[4 + e] - m_new);
+    }
+    float lsum = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lsum += pe0[e];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lsum += pe1[e];
+    lsum += __shfl_xor(lsum, 16);
+    lsum += __shfl_xor(lsum, 32);
+    l_run = l_run * alpha + lsum;
+    m_run = m_new;
+    Frag bp, bpl;
+    at_split8(pe0, pe1, bp, bpl);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const char* vr = Vs + (16 * t + q) * VR + 8 * g;
+      const uint2 h0 = *reinterpret_cast<const uint2*>(vr), h1 = *reinterpret_cast<const uint2*>(vr + 32);
+      const uint2 l0 = *reinterpret_cast<const uint2*>(vr + VPL), l1 = *reinterpret_cast<const uint2*>(vr + VPL + 32);
+      const Frag ah = __builtin_bit_cast(Frag, uint4{h0.x, h0.y, h1.x, h1.y});
+      const Frag al = __builtin_bit_cast(Frag, uint4{l0.x, l0.y, l1.x, l1.y});
+      oacc[t] = MF::mma(ah, bp, oacc[t] * alpha);
+      f32x4 ox = MF::mma(ah, bpl, oaccx[t] * alpha);
+      oaccx[t] = MF::mma(al, bp, ox);
+    }
+    __syncthreads();
+    write_kv(j0 + AT_BK);
+    write_r(j0 + AT_BK);
+    __syncthreads();
+  }
+  const int i = i0w + q;
+  if (i < len) {
+    const float inv = 1.f / l_run;
+    float* orow = out + ((long long)b * Tp + i) * rowD + h * DK;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+      *reinterpret_cast<f32x4*>(orow + 16 * t + 4 * g) = (oacc[t] + oaccx[t] * (1.f / AT_SPLIT)) * inv;
+  }
+}
+
+template <int DK>
+size_t rel_attn_split_lds() {
+  return (size_t)2 * (AT_BK * (DK * 2 + 16) + DK * (AT_BK * 2 + 16) + AT_RW * (DK * 2 + 16)) + (size_t)4 * 48 * 16 * 4;
+}
+
 template <int DK>
 size_t rel_attn_f32_lds() {
   return (size_t)AT_BK * (DK * 4 + 16) + (size_t)DK * (AT_BK * 4 + 16) + (size_t)AT_RW * (DK * 4 + 16) +
@@ -453,12 +690,18 @@ bool rel_attn_supported(int dt, int D, int H) {
   return (dt == DT_F16 || dt == DT_BF16 || dt == DT_F32) && H > 0 && D % H == 0 && D / H == 192;
 }
 
-hipError_t launch_rel_attn(int dt, const float* pos_u, const float* pos_v, const void* qkv, const void* vt, const void* ptab,
-                           const int* lens, int B, int Tm, int Tp, int D, int H, int Sk, int rmax, float scale,
-                           void* out, hipStream_t s) {
+hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* pos_v, const void* qkv, const void* vt,
+                           const void* ptab, const int* lens, int B, int Tm, int Tp, int D, int H, int Sk, int rmax,
+                           float scale, void* out, hipStream_t s) {
   if (!rel_attn_supported(dt, D, H) || Tm > rmax || Sk % 8) return hipErrorInvalidValue;
   const int nqb = (Tm + AT_BQ - 1) / AT_BQ;
   dim3 grid(xcd_grid(nqb, H * B));
+  if (dt == DT_F32 && split) {
+    hipLaunchKernelGGL((rel_attn_split_kernel<192>), grid, dim3(256), rel_attn_split_lds<192>(), s, pos_u, pos_v,
+                       (const float*)qkv, (const float*)vt, (const float*)ptab, lens, Tp, D, H, Sk, rmax, scale,
+                       (float*)out, nqb, B);
+    return hipGetLastError();
+  }
   if (dt == DT_F32) {
     hipLaunchKernelGGL((rel_attn_f32_kernel<192>), grid, dim3(256), rel_attn_f32_lds<192>(), s, pos_u, pos_v,
                        (const float*)qkv, (const float*)vt, (const float*)ptab, lens, Tp, D, H, Sk, rmax, scale,

@@ -18,6 +18,7 @@ enum Sw : int {
   SW_CONV_WIDE,    // TTS_CONV_WIDE=1: 128-byte channel chunks in conv_gemm
   SW_SPLIT_TILE,   // TTS_SPLIT_TILE=1/2: force the per-utterance split GEMM tile
   SW_PAIR_DIV,     // TTS_PAIR_DIV=1: full-height pair tiles; any other value: short tiles
+  SW_ATTN_SPLIT,   // TTS_ATTN_SPLIT=0: the exact encoder's fused attention on f32 MFMA, not split
   SW_N
 };
 

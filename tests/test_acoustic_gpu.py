@@ -314,7 +314,8 @@ def _margin(logd):
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_predicted_durations_exact_on_default_path(aw, dtype):
     """The default 16-bit acoustic path (encoder_precision="exact": encoder, speaker projection and
-    variance predictors in fp32 with three-f16-MFMA GEMMs, conv_split.hip) predicts integer
+    variance predictors in fp32 with three-f16-MFMA GEMMs, conv_split.hip, and the split-precision
+    fused attention, attention.hip) predicts integer
     durations equal to the fp32 oracle's for every token whose oracle exp(x)-1 is more than 1e-3
     from a .5 boundary -- the same carve-out as the fp32 path above.  C3's token distribution
     (32 x 144 ids U[1,77], 4,608 tokens), the two transformers golden utterances and a ragged tail."""

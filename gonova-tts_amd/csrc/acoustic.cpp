@@ -108,18 +108,7 @@ struct AcousticModel::Impl {
   float *f_pitch = nullptr, *f_energy = nullptr, *f_logd = nullptr;
   int *i_dur = nullptr, *i_tokmap = nullptr;
 
-  // the three variance predictors read the same encoder output and write disjoint buffers
-  // (HF:1198-1210), so pitch and energy run on two side streams beside duration: at small
-  // batches each predictor conv fills a fraction of the chip
-  hipStream_t side[2] = {nullptr, nullptr};
-  hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
-  void *PBv[3][2] = {};         // per-predictor ping-pong buffers (duration's are PB1 / PB2)
-  float* pws[3] = {};           // per-predictor split-K partials
-  long long pws_bytes[3] = {};
-
   ~Impl() {
-    for (hipStream_t& q : side) if (q) hipStreamDestroy(q);
-    for (hipEvent_t e : {ev_fork, ev_join[0], ev_join[1]}) if (e) hipEventDestroy(e);
     for (void* p : allocs) hipFree(p);
     for (void* p : ws) hipFree(p);
     for (void* p : score_ws) hipFree(p);
@@ -269,7 +258,6 @@ struct AcousticModel::Impl {
     i_dur = i_tokmap = nullptr;
     split_ws = nullptr;
     split_ws_bytes = 0;
-    for (int i = 0; i < 3; ++i) { PBv[i][0] = PBv[i][1] = nullptr; pws[i] = nullptr; pws_bytes[i] = 0; }
     std::vector<void*> old;
     old.swap(ws);
     for (void* p : old) hipFree(p);
@@ -326,8 +314,7 @@ struct AcousticModel::Impl {
     const size_t nrows = (size_t)B * enc_rows(N);
     ENC = alloc_ws(nrows * D, e);
     SPK = alloc_ws((size_t)B * D, e);
-    for (int i = 0; i < 3; ++i) { PBv[i][0] = alloc_ws(nrows * PRED, e); PBv[i][1] = alloc_ws(nrows * PRED, e); }
-    PB1 = PBv[2][0]; PB2 = PBv[2][1];
+    PB1 = alloc_ws(nrows * PRED, e); PB2 = alloc_ws(nrows * PRED, e);
     const size_t trows = (size_t)B * rup(T, 32);
     BEF = alloc_ws(trows * NMEL, e); MELT = alloc_ws(trows * NMEL, e);
     PN1 = alloc_ws(trows * PRED, e); PN2 = alloc_ws(trows * PRED, e);
@@ -341,13 +328,8 @@ struct AcousticModel::Impl {
       for (auto& L : enc)
         for (const ConvLayer* c : {&L.ffm1, &L.ffm2, &L.ff1, &L.ff2, &L.qkv, &L.out, &L.pw1, &L.pw2})
           wsb = std::max(wsb, conv_split_ws_bytes(c->taps, c->Cin, c->M, F));
-      int i = 0;
-      for (const Predictor* pr : {&pitch, &energy, &duration}) {
-        long long pb = 0;
-        for (const ConvLayer& c : pr->convs) pb = std::max(pb, conv_split_ws_bytes(c.taps, c.Cin, c.M, F));
-        pws[i] = pb ? (float*)alloc_ws((size_t)pb, 1) : nullptr;
-        pws_bytes[i++] = pb;
-      }
+      for (const Predictor* pr : {&pitch, &energy, &duration})
+        for (const ConvLayer& c : pr->convs) wsb = std::max(wsb, conv_split_ws_bytes(c.taps, c.Cin, c.M, F));
     }
     split_ws = wsb ? (float*)alloc_ws((size_t)wsb, 1) : nullptr;
     split_ws_bytes = wsb;
@@ -432,16 +414,18 @@ struct AcousticModel::Impl {
     ln_rows(dt, Y, Xb, rows, D, L.ln_ff, &L.ln_final, s);
   }
 
-  // predictor k (0 pitch, 1 energy, 2 duration) with its own buffers and split-K workspace
-  void predict(Predictor& Pr, int k, const void* x, const int* lens, int B, int Np, float* out, hipStream_t s) {
+  // The three predictors run in sequence on one stream: pitch and energy on two side streams
+  // (they read the same encoder output, HF:1198-1210) shortened the predictor span in kernel
+  // traces (batch 8: 270 -> 149 us) but cost 0.1-0.3 ms end to end in the C3 / C5 measurements
+  // (fork / join across hardware queues), so they stay sequential.
+  void predict(Predictor& Pr, const void* x, const int* lens, int B, int Np, float* out, hipStream_t s) {
     const int dt = Pr.dt;
     const void* h = x;
-    void* const* bufs = PBv[k];
+    void* bufs[2] = {PB1, PB2};
     const int n = (int)Pr.convs.size();
     for (int i = 0; i < n; ++i) {
       void* o = bufs[i & 1];
-      run_layer(Pr.convs[i], h, Np, lens, o, Np, B, dt, s, prof, 1.f, ACT_RELU, 1.f, nullptr, nullptr, 1.f, 0, 0,
-                cur_rpad, pws[k], pws_bytes[k]);
+      run(Pr.convs[i], h, Np, lens, o, Np, B, dt, s, prof, 1.f, ACT_RELU);
       if (i + 1 < n) ln_rows(dt, o, o, B * Np, PRED, Pr.lns[i], nullptr, s);
       else HIP_CHECK(launch_ln_linear1(dt, o, B * Np, PRED, Pr.lns[i].g, Pr.lns[i].b, eps, Pr.lin_w, Pr.lin_b, out, s));
       h = o;
@@ -479,24 +463,13 @@ struct AcousticModel::Impl {
       HIP_CHECK(hipMemcpyAsync(ENC, Y, (size_t)B * Np * D * dtype_size(dte), hipMemcpyDeviceToDevice, s));
     }
     // variance adaptor (HF:1198-1218)
-    if (!side[0]) {
-      for (hipStream_t& q : side) HIP_CHECK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
-      for (hipEvent_t* e : {&ev_fork, &ev_join[0], &ev_join[1]})
-        HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    }
-    HIP_CHECK(hipEventRecord(ev_fork, s));
-    for (hipStream_t q : side) HIP_CHECK(hipStreamWaitEvent(q, ev_fork, 0));
-    predict(duration, 2, ENC, tok_lens, B, Np, f_logd, s);  // first: the durations wait on it
-    predict(pitch, 0, ENC, tok_lens, B, Np, f_pitch, side[0]);
-    predict(energy, 1, ENC, tok_lens, B, Np, f_energy, side[1]);
+    predict(pitch, ENC, tok_lens, B, Np, f_pitch, s);
+    predict(energy, ENC, tok_lens, B, Np, f_energy, s);
+    predict(duration, ENC, tok_lens, B, Np, f_logd, s);
     cur_rpad = 0;
     // logd is laid out [B][Np]; durations kernel reads [B][N] rows -> compact view via stride Np
     int* dur = durations ? durations : i_dur;
     HIP_CHECK(launch_durations_strided(s, B, N, Np, tok_lens, dur_override, Tcap, dur, mel_lens));
-    for (int i = 0; i < 2; ++i) {  // pitch and energy join before their embeddings are added
-      HIP_CHECK(hipEventRecord(ev_join[i], side[i]));
-      HIP_CHECK(hipStreamWaitEvent(s, ev_join[i], 0));
-    }
     HIP_CHECK(launch_var_embed_add(dte, ENC, B * Np, D, f_energy, ee_w, ee_b, f_pitch, pe_w, pe_b, s));
     // decoder rows are laid out with stride Tp; regulate writes [B][Tcap] rows
     void* Xd = X;

@@ -26,6 +26,29 @@ namespace tts {
 
 namespace {
 
+// Row statistics over the 4 lanes of a query (q, q+16, q+32, q+48) with gfx950's VALU lane
+// swaps instead of LDS-routed ds_bpermute: each swap returns the lane's own value in one result
+// and its partner's in the other, so max / sum of the two is the xor-16 / xor-32 reduction (the
+// same operands, so bit-identical to the shuffle form)
+__device__ inline float at_xor16_max(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ inline float at_xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ inline float at_xor16_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ inline float at_xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// 2^x on v_exp_f32 (arguments <= 0 here; -inf -> 0), without exp2f's denormal-range fixup
+__device__ inline float at_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 constexpr int AT_BQ = 64;   // queries per block
 constexpr int AT_BK = 32;   // keys per step
 constexpr int AT_RW = AT_BQ + AT_BK;  // R window rows per block (95 used)
@@ -196,25 +219,22 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
         mloc = fmaxf(mloc, sc);
       }
     __builtin_amdgcn_wave_barrier();
-    // row statistics over the 4 lanes of query q (lanes q, q+16, q+32, q+48)
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+        mloc = at_xor32_max(at_xor16_max(mloc));
     const float m_new = fmaxf(m_run, mloc);
-    const float alpha = exp2f(m_run - m_new);  // m_run = -inf on the first step: alpha = 0
+    const float alpha = at_exp2(m_run - m_new);  // m_run = -inf on the first step: alpha = 0
     float lsum = 0.f;
     f32x4 pe0, pe1;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      pe0[e] = exp2f(sv[e] - m_new);
-      pe1[e] = exp2f(sv[4 + e] - m_new);
+      pe0[e] = at_exp2(sv[e] - m_new);
+      pe1[e] = at_exp2(sv[4 + e] - m_new);
     }
     // normalise with the rounded probabilities P.V uses (keys in the order e = 0 .. 7)
 #pragma unroll
     for (int e = 0; e < 4; ++e) lsum += (float)(T)pe0[e];
 #pragma unroll
     for (int e = 0; e < 4; ++e) lsum += (float)(T)pe1[e];
-    lsum += __shfl_xor(lsum, 16);
-    lsum += __shfl_xor(lsum, 32);
+    lsum = at_xor32_sum(at_xor16_sum(lsum));
     l_run = l_run * alpha + lsum;
     m_run = m_new;
     const Frag bp = __builtin_bit_cast(Frag, pack8<T>(pe0, pe1));
@@ -393,20 +413,18 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
         mloc = fmaxf(mloc, sc);
       }
     __builtin_amdgcn_wave_barrier();
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+    mloc = at_xor32_max(at_xor16_max(mloc));
     const float m_new = fmaxf(m_run, mloc);
-    const float alpha = exp2f(m_run - m_new);
+    const float alpha = at_exp2(m_run - m_new);
     f32x4 pe[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) pe[kt][e] = exp2f(sv[4 * kt + e] - m_new);
+      for (int e = 0; e < 4; ++e) pe[kt][e] = at_exp2(sv[4 * kt + e] - m_new);
     float lsum = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) lsum += pe[e >> 2][e & 3];
-    lsum += __shfl_xor(lsum, 16);
-    lsum += __shfl_xor(lsum, 32);
+    lsum = at_xor32_sum(at_xor16_sum(lsum));
     l_run = l_run * alpha + lsum;
     m_run = m_new;
     // O^T += Vt . P^T: k-step (kt, e) has lane group g on key 16 kt + 4 g + e, the lane's own pe
@@ -620,23 +638,21 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
       }
     }
     __builtin_amdgcn_wave_barrier();
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+    mloc = at_xor32_max(at_xor16_max(mloc));
     const float m_new = fmaxf(m_run, mloc);
-    const float alpha = exp2f(m_run - m_new);
+    const float alpha = at_exp2(m_run - m_new);
     f32x4 pe0, pe1;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      pe0[e] = exp2f(sv[e] - m_new);
-      pe1[e] = exp2f(sv[4 + e] - m_new);
+      pe0[e] = at_exp2(sv[e] - m_new);
+      pe1[e] = at_exp2(sv[4 + e] - m_new);
     }
     float lsum = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) lsum += pe0[e];
 #pragma unroll
     for (int e = 0; e < 4; ++e) lsum += pe1[e];
-    lsum += __shfl_xor(lsum, 16);
-    lsum += __shfl_xor(lsum, 32);
+    lsum = at_xor32_sum(at_xor16_sum(lsum));
     l_run = l_run * alpha + lsum;
     m_run = m_new;
     Frag bp, bpl;

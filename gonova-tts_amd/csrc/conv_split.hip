@@ -340,16 +340,18 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
   };
 
   const int gbeg = sl * gps * CG, gend = min(p.Cin, (sl + 1) * gps * CG);
-  load_x(gbeg);
-  store_x();
-  __syncthreads();
-  for (int g0 = gbeg; g0 < gend; g0 += CG) {
-    Frag a0[8], a1[8];
+  // Weight quads form one ring over the slice: the two quads past a group's last are the next
+  // group's first two (issued before the group-change barriers, so their latency overlaps the
+  // X restaging); past the slice's last group they fall outside the descriptor and fetch nothing.
+  Frag a0[8], a1[8];
+  int g0 = gbeg;
 #define TTS_SPLIT_LOADQ(A_, QQ_)                                                                     \
     do {                                                                                             \
-      const int kq_ = 4 * (QQ_);                                                                     \
-      const int o_ = (((kq_ >> lks) * KST + g0 / 16 + (kq_ & (KS - 1))) * 1024) +                    \
-                     (((QT - 1 - (QQ_)) >> 31) & 0x40000000);                                        \
+      const int nx_ = (QQ_) >= QT;                                                                   \
+      const int kq_ = 4 * ((QQ_) - nx_ * QT);                                                        \
+      const int gg_ = g0 + nx_ * CG;                                                                 \
+      const int o_ = (((kq_ >> lks) * KST + gg_ / 16 + (kq_ & (KS - 1))) * 1024) +                   \
+                     (gg_ < gend ? 0 : 0x40000000);                                                  \
       _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                             \
         A_[j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_hi, lofs + j_ * 1024, o_, 0)); \
         A_[4 + j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_lo, lofs + j_ * 1024, o_, 0)); \
@@ -370,9 +372,13 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
         }                                                                                            \
       }                                                                                              \
     } while (0)
+  TTS_SPLIT_LOADQ(a0, 0);
+  TTS_SPLIT_LOADQ(a1, 1);
+  load_x(gbeg);
+  store_x();
+  __syncthreads();
+  for (; g0 < gend; g0 += CG) {
     const bool more = g0 + CG < gend;
-    TTS_SPLIT_LOADQ(a0, 0);
-    TTS_SPLIT_LOADQ(a1, 1);
     TTS_SPLIT_MMAQ(a0, 0);
     TTS_SPLIT_LOADQ(a0, 2);
     load_x(more ? g0 + CG : g0);  // unconditional (a load under a branch is waited on at once)

@@ -21,6 +21,7 @@
 #include "acoustic_kernels.h"
 #include "common.h"
 #include "mrf_tile.h"
+#include "switches.h"
 
 namespace tts {
 
@@ -53,8 +54,12 @@ constexpr int AT_BQ = 64;   // queries per block
 constexpr int AT_BK = 32;   // keys per step
 constexpr int AT_RW = AT_BQ + AT_BK;  // R window rows per block (95 used)
 
-template <typename T, int DK>
-__global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restrict__ pu, const float* __restrict__ pv,
+// KH = 2: 8 waves, the block's keys split into two groups of whole 32-key steps, one per 4
+// waves (each group with its own K / Vt / R staging), merged through LDS at the end -- twice
+// the waves per SIMD where the grid has about one block per CU.  The split point depends only
+// on the utterance's length, so a row's result does not depend on the batch.
+template <typename T, int DK, int KH>
+__global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(const float* __restrict__ pu, const float* __restrict__ pv,
                                                          const T* __restrict__ qkv, const T* __restrict__ vt,
                                                          const T* __restrict__ ptab, const int* __restrict__ lens,
                                                          int Tp, int D, int H, int Sk, int rmax, float scale,
@@ -65,11 +70,13 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
   constexpr int DT = DK / 16;         // 16-row tiles of dk (O^T)
   constexpr int KR = DK * 2 + 16;     // K / R row stride in LDS (bytes; odd 16-byte slots)
   constexpr int VR = AT_BK * 2 + 16;  // Vt row stride (80 B)
+  constexpr int HALF = AT_BK * KR + DK * VR + AT_RW * KR;  // one key group's staging bytes
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Ks = smem;                                  // [32 keys][DK]
+  const int kh = KH > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) : 0;  // key group
+  char* Ks = smem + kh * HALF;                      // [32 keys][DK]
   char* Vs = Ks + AT_BK * KR;                       // [DK][32 keys]
   char* Rs = Vs + DK * VR;                          // [96 slots][DK]
-  float* Gs = reinterpret_cast<float*>(Rs + AT_RW * KR);  // [4 waves][48 slots][16 q]
+  float* Gs = reinterpret_cast<float*>(smem + KH * HALF);  // [KH][4 waves][48 slots][16 q]
 
   // 1-D grid, XCD-grouped: the query blocks of one (utterance, head) -- which all stream the
   // same K / Vt / R rows -- run on one XCD, so those rows come from its L2 after the first
@@ -79,11 +86,14 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
   const int i0 = qb * AT_BQ;
   const int len = lens[b];
   if (i0 >= len) return;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x & 255, lane = tid & 63;  // thread / wave within the key group
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane & 15, g = lane >> 4;
   const int i0w = i0 + 16 * w;
   const long long rowD = D;
+  // this group's keys: whole 32-key steps, the same step count for both groups
+  const int khalf = KH > 1 ? (len + 2 * AT_BK - 1) / (2 * AT_BK) * AT_BK : len;
+  const int kbeg = kh * khalf, kend = min(len, kbeg + khalf);
   // this lane's query row (clamped into the buffer; rows >= len are computed, not stored)
   const int iq = min(i0w + q, Tp - 1);
   // Qu = q + pos_bias_u, Qv = q + pos_bias_v (HF:420-423), formed here from the q slice of
@@ -105,7 +115,7 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
   for (int t = 0; t < DT; ++t) oacc[t] = f32x4{};
   float m_run = -INFINITY, l_run = 0.f;
   const float sl2 = scale * 1.4426950408889634f;  // scores in log2 units
-  float* gw = Gs + w * 48 * 16;
+  float* gw = Gs + (kh * 4 + w) * 48 * 16;
 
   // Staging.  K[j0 .. j0+32) (zero past len) and Vt[:, j0 .. j0+32) per step; the R window
   // (block slot sb <-> m = i0 - j0 - 31 + sb, 96 rows) lives in a 96-row ring indexed by
@@ -169,15 +179,15 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
   // first step: the whole 96-row R window
   for (int p = tid; p < AT_RW * (DK / 8); p += 256) {
     const int sb = p / (DK / 8), c = p - sb * (DK / 8);
-    const int m = i0 - (AT_BK - 1) + sb;
+    const int m = i0 - kbeg - (AT_BK - 1) + sb;
     *reinterpret_cast<uint4*>(Rs + rslot(m) * KR + c * 16) =
         *reinterpret_cast<const uint4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 8);
   }
-  load_kv(0);
-  write_kv(0);
+  load_kv(kbeg);
+  write_kv(kbeg);
   __syncthreads();
 
-  for (int j0 = 0; j0 < len; j0 += AT_BK) {
+  for (int j0 = kbeg; j0 < kbeg + khalf; j0 += AT_BK) {
     load_kv(j0 + AT_BK);  // in flight during this step's MFMAs (the last step's are written, unused)
     load_r(j0 + AT_BK);
     __builtin_amdgcn_sched_barrier(0);
@@ -214,20 +224,23 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
         const int kk = 16 * kt + 4 * g + e;
         const float bd = gw[(q - kk + AT_BK - 1) * 16 + q];
         float sc = (sacc[kt][e] + bd) * sl2;
-        if (j0 + kk >= len) sc = -INFINITY;
+        if (j0 + kk >= kend) sc = -INFINITY;
         sv[4 * kt + e] = sc;
         mloc = fmaxf(mloc, sc);
       }
     __builtin_amdgcn_wave_barrier();
-        mloc = at_xor32_max(at_xor16_max(mloc));
+    mloc = at_xor32_max(at_xor16_max(mloc));
     const float m_new = fmaxf(m_run, mloc);
-    const float alpha = at_exp2(m_run - m_new);  // m_run = -inf on the first step: alpha = 0
+    // a step with every key masked (the second key group of a short utterance) keeps m = -inf:
+    // exponents are then taken against 0, so alpha and P stay 0 instead of NaN
+    const float m_ref = KH > 1 && m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = at_exp2(m_run - m_ref);  // m_run = -inf on the first step: alpha = 0
     float lsum = 0.f;
     f32x4 pe0, pe1;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      pe0[e] = at_exp2(sv[e] - m_new);
-      pe1[e] = at_exp2(sv[4 + e] - m_new);
+      pe0[e] = at_exp2(sv[e] - m_ref);
+      pe1[e] = at_exp2(sv[4 + e] - m_ref);
     }
     // normalise with the rounded probabilities P.V uses (keys in the order e = 0 .. 7)
 #pragma unroll
@@ -251,6 +264,31 @@ __global__ __launch_bounds__(256, 2) void rel_attn_kernel(const float* __restric
     write_kv(j0 + AT_BK);
     write_r(j0 + AT_BK);
     __syncthreads();
+  }
+  if constexpr (KH > 1) {
+    // merge the two key groups: group 1 leaves (m, l, O^T) in LDS, group 0 rescales both
+    constexpr int MS = 2 + 4 * DT + 2;  // floats per lane (padded)
+    float* mg = reinterpret_cast<float*>(smem) + (w * 64 + lane) * MS;
+    __syncthreads();  // staging tiles no longer read
+    if (kh == 1) {
+      mg[0] = m_run;
+      mg[1] = l_run;
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mg[2 + 4 * t + e] = oacc[t][e];
+    }
+    __syncthreads();
+    if (kh == 1) return;
+    const float mb = mg[0], lb = mg[1];
+    const float mm = fmaxf(m_run, mb);
+    const float sa = m_run == -INFINITY ? 0.f : at_exp2(m_run - mm);
+    const float sb = mb == -INFINITY ? 0.f : at_exp2(mb - mm);
+    l_run = l_run * sa + lb * sb;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) oacc[t][e] = oacc[t][e] * sa + mg[2 + 4 * t + e] * sb;
   }
   // O[i][h*dk + d] = O^T[d][i] / l
   const int i = i0w + q;
@@ -695,9 +733,9 @@ size_t rel_attn_f32_lds() {
 }
 
 template <int DK>
-size_t rel_attn_lds() {
-  return (size_t)AT_BK * (DK * 2 + 16) + (size_t)DK * (AT_BK * 2 + 16) + (size_t)AT_RW * (DK * 2 + 16) +
-         (size_t)4 * 48 * 16 * 4;
+size_t rel_attn_lds(int kh) {
+  return (size_t)kh * (AT_BK * (DK * 2 + 16) + (size_t)DK * (AT_BK * 2 + 16) + (size_t)AT_RW * (DK * 2 + 16) +
+                       (size_t)4 * 48 * 16 * 4);
 }
 
 }  // namespace
@@ -724,15 +762,21 @@ hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* 
                        (float*)out, nqb, B);
     return hipGetLastError();
   }
-  const size_t lds = rel_attn_lds<192>();
-  if (dt == DT_F16)
-    hipLaunchKernelGGL((rel_attn_kernel<half_t, 192>), grid, dim3(256), lds, s, pos_u, pos_v,
-                       (const half_t*)qkv, (const half_t*)vt, (const half_t*)ptab, lens, Tp, D, H, Sk, rmax, scale,
-                       (half_t*)out, nqb, B);
-  else
-    hipLaunchKernelGGL((rel_attn_kernel<bf16_t, 192>), grid, dim3(256), lds, s, pos_u, pos_v,
-                       (const bf16_t*)qkv, (const bf16_t*)vt, (const bf16_t*)ptab, lens, Tp, D, H, Sk, rmax, scale,
-                       (bf16_t*)out, nqb, B);
+  // two key groups per block (TTS_ATTN_KSPLIT=1): batch 8 287 -> 248 us per forward, batch 32
+  // 757 -> 934 us (one block per CU).  Off by default: a batch-dependent choice would make a
+  // row's bits depend on the batch (the merge rounds differently from one online softmax)
+  const int kh = sw(SW_ATTN_KSPLIT) == 1 ? 2 : 1;
+  const size_t lds = rel_attn_lds<192>(kh);
+#define TTS_ATTN_LAUNCH(TT_, KH_)                                                                  \
+  hipLaunchKernelGGL((rel_attn_kernel<TT_, 192, KH_>), grid, dim3(256 * KH_), lds, s, pos_u, pos_v, \
+                     (const TT_*)qkv, (const TT_*)vt, (const TT_*)ptab, lens, Tp, D, H, Sk, rmax, scale, \
+                     (TT_*)out, nqb, B)
+  if (dt == DT_F16) {
+    if (kh == 2) TTS_ATTN_LAUNCH(half_t, 2); else TTS_ATTN_LAUNCH(half_t, 1);
+  } else {
+    if (kh == 2) TTS_ATTN_LAUNCH(bf16_t, 2); else TTS_ATTN_LAUNCH(bf16_t, 1);
+  }
+#undef TTS_ATTN_LAUNCH
   return hipGetLastError();
 }
 

@@ -19,6 +19,7 @@ enum Sw : int {
   SW_SPLIT_TILE,   // TTS_SPLIT_TILE=1/2: force the per-utterance split GEMM tile
   SW_PAIR_DIV,     // TTS_PAIR_DIV=1: full-height pair tiles; any other value: short tiles
   SW_ATTN_SPLIT,   // TTS_ATTN_SPLIT=0: the exact encoder's fused attention on f32 MFMA, not split
+  SW_ATTN_KSPLIT,  // TTS_ATTN_KSPLIT=1: 16-bit attention with two key groups per block (8 waves)
   SW_N
 };
 

@@ -249,6 +249,31 @@ def test_fused_rel_attention_matches_unfused_and_oracle(aw, dtype, switch):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_attention_key_groups_match(aw, dtype, switch):
+    """The 16-bit attention with the block's keys split over two groups of 4 waves
+    (TTS_ATTN_KSPLIT=1, merged through LDS) against the one-group kernel and the oracle: ragged
+    lengths where the second group is empty (1, 17 tokens x 5 frames <= 96 keys), partial and
+    full (utterances up to 500 frames)."""
+    eng = engine(dtype, aw)
+    rng = np.random.default_rng(13)
+    ids_list = [rng.integers(1, 78, size=n) for n in (100, 1, 17, 33, 64)]
+    durs = [np.full(len(x), 5) for x in ids_list]
+    one, l1, _ = run(eng, ids_list, t_cap=500, durations=durs)
+    switch("TTS_ATTN_KSPLIT", 1)
+    two, l2, _ = run(eng, ids_list, t_cap=500, durations=durs)
+    tol = {"bf16": 2.5e-2, "f16": 5e-3}[dtype]
+    for b, ids in enumerate(ids_list):
+        L = int(l1[b])
+        assert L == int(l2[b]) == len(ids) * 5
+        assert np.isfinite(two[b]).all()
+        assert rel_rms(two[b, :L], one[b, :L]) <= tol, (b, rel_rms(two[b, :L], one[b, :L]))
+        ref = acoustic_forward(ids, aw, durations=durs[b])
+        check(f"acoustic {dtype} two key groups b={b} ({len(ids)} tokens)", two[b, :L], ref["mel"],
+              kind="ac_" + dtype)
+        assert np.all(two[b, L:] == 0)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_short_row_tiles_bit_identical(aw, dtype, switch):
     """conv_xres picks 64-row tiles where 128-row tiles would leave much of each utterance's
     last tile empty (the encoder's short token rows).  The channel group, and so the K order

@@ -465,7 +465,10 @@ struct AcousticModel::Impl {
     // variance adaptor (HF:1198-1218)
     predict(pitch, ENC, tok_lens, B, Np, f_pitch, s);
     predict(energy, ENC, tok_lens, B, Np, f_energy, s);
-    predict(duration, ENC, tok_lens, B, Np, f_logd, s);
+    // HF inference always regulates with the predicted durations (HF:1211-1219); given durations
+    // are this engine's override (the oracle's `durations=`), under which the prediction is
+    // never read, so the duration predictor does not run
+    if (!dur_override) predict(duration, ENC, tok_lens, B, Np, f_logd, s);
     cur_rpad = 0;
     // logd is laid out [B][Np]; durations kernel reads [B][N] rows -> compact view via stride Np
     int* dur = durations ? durations : i_dur;
@@ -507,7 +510,7 @@ struct AcousticModel::Impl {
                                       int Tcap, int* dur, int* mel_lens) {
     // compact f_logd [B][Np] -> [B][N] in place is unsafe; copy into PB1 (float view) first
     float* logd = f_logd;
-    if (Np != N) {
+    if (Np != N && !ovr) {  // (with given durations the kernel does not read logd)
       HIP_CHECK(hipMemcpy2DAsync(PB1, (size_t)N * 4, f_logd, (size_t)Np * 4, (size_t)N * 4, B,
                                  hipMemcpyDeviceToDevice, s));
       logd = (float*)PB1;

@@ -179,7 +179,12 @@ class GonovaTTS:
             if need > t_cap:
                 mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
                                                           return_durations=True)
-        lens_h = mel_lens.cpu().numpy().astype(np.int64)
+            lens_h = mel_lens.cpu().numpy().astype(np.int64)
+        else:
+            # given durations fix the frame counts on the host: no device sync between the
+            # acoustic pass and the first chunk's vocoder launches (same-box C5: neutral, the
+            # host enqueues faster than the GPU drains either way)
+            lens_h = _mel_lens_host(lens, durations, t_cap)
         T = int(lens_h.max()) if B else 0
         hop = self.vocoder_cfg.hop
         for c0 in range(0, T, chunk_frames):
@@ -267,3 +272,18 @@ class GonovaTTS:
 # Alias with the reference's class name so `from gonova_tts_amd.model import ChatterboxTTS`
 # is a one-line swap at synthesizer.py:167.
 ChatterboxTTS = GonovaTTS
+
+
+def _mel_lens_host(lens: np.ndarray, durations: np.ndarray, t_cap: int) -> np.ndarray:
+    """Frame counts for given durations, as the engine's durations kernel computes them
+    (acoustic_kernels.hip: negative durations count 0; an utterance whose durations are all 0
+    gets one frame per token, HF:108-109; clamped to the frame cap)."""
+    d = np.asarray(durations, np.int64)
+    out = np.zeros(len(lens), np.int64)
+    for b, L in enumerate(np.asarray(lens, np.int64)):
+        L = int(min(L, d.shape[1]))
+        s = int(np.maximum(d[b, :L], 0).sum())
+        if s == 0 and L > 0:
+            s = L
+        out[b] = min(s, t_cap)
+    return out

@@ -47,3 +47,18 @@ def test_switches_set_and_reset_without_gpu():
         pass
     with pytest.raises(RuntimeError, match="unknown switch"):
         engine.set_switch("TTS_NO_SUCH_SWITCH", 1)
+
+
+def test_stream_mel_lens_host_matches_duration_rules():
+    """stream_tokens computes frame counts on the host when durations are given (no sync before
+    the first chunk); the rules are the durations kernel's: tokens past the length and negative
+    durations count 0, an utterance whose durations are all 0 gets one frame per token, and the
+    count is clamped to the frame cap."""
+    import numpy as np
+    from gonova_tts_amd.model import _mel_lens_host
+    lens = np.array([3, 2, 0, 4])
+    dur = np.array([[2, 3, 1, 9],      # 9 is past the length
+                    [0, 0, 5, 5],      # all zero within the length -> one frame per token
+                    [4, 4, 4, 4],      # empty utterance
+                    [-1, 6, 6, 6]])    # negative counts 0; 18 clamped to the cap
+    np.testing.assert_array_equal(_mel_lens_host(lens, dur, t_cap=16), [6, 2, 0, 16])

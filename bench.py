@@ -8,7 +8,9 @@ A "step" = one vocoder forward over the batch.
 
 The same line also carries `full_pipeline` (configs[2]: token ids U[1,77] [32,144],
 durations forced to 6 frames/token -> 864 frames; acoustic bf16 + vocoder bf16,
-tokens in HBM -> waveform in HBM), measured after the headline loop.
+tokens in HBM -> waveform in HBM), measured after the headline loop, and beside it the host
+end-to-end rate (`host_e2e_*`: token ids in host memory -> waveform in pinned host memory,
+the PCIe copies inside the timed region).
 `--workload full` makes that the headline instead.
 
 Multi-GPU: `bench.py --gpus N` runs one process per GPU.  Launched under
@@ -310,6 +312,18 @@ def bench_full(ctx, args, steps, warmup):
     # acoustic-only timing (same inputs) to split the step
     el_ac, _ = ctx.timed(lambda: eng.acoustic(tok, tl, T), steps, 1)
     ac_ms = el_ac * 1e3 / steps
+    # host end to end: token ids in host memory -> waveform in (pinned) host
+    # memory, the PCIe copies inside the timed region; reported beside the device-resident value
+    tok_h = tok.cpu()
+    wav_h = torch.empty((B, T * 256), dtype=torch.float32, pin_memory=True)
+
+    def host_step():
+        mel_, lens_ = eng.acoustic(tok_h.to(ctx.dev), tl, T)
+        eng.vocoder(mel_, lens_, out=wav)
+        wav_h.copy_(wav, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+
+    el_h, _ = ctx.timed(host_step, steps, 1)
     eng.close()
     # the same acoustic pass with encoder_precision="fast" (whole model bf16; durations may round
     # differently near .5), to show what the default exact-duration encoder costs
@@ -321,6 +335,8 @@ def bench_full(ctx, args, steps, warmup):
     return {"value": round(value, 1), "unit": "samples/s", "ms_per_step": round(el * 1e3 / steps, 3),
             "acoustic_ms_per_step": round(ac_ms, 3),
             "acoustic_ms_per_step_fast_encoder": round(el_f * 1e3 / steps, 3),
+            "host_e2e_ms_per_step": round(el_h * 1e3 / steps, 3),
+            "host_e2e_samples_per_s": round(samples / el_h, 1),
             "encoder_precision": "exact (fp32 encoder + variance predictors, GEMMs as 3 f16 MFMAs)",
             "per_gpu_samples_per_s": round(value / ctx.world, 1),
             "x_realtime_per_gpu": round(value / ctx.world / SR, 2), "dtype": "bf16",

@@ -18,6 +18,11 @@
 //   O^T += Vt . P^T    A = Vt rows (LDS),      B = P^T: the lane's own 8 probabilities
 // P^T's k index is permuted (keys 4g..4g+3, 16+4g..16+4g+3 for lane group g) and the Vt
 // fragment is read with the same permutation, so no cross-lane move is needed.
+//
+// Three forms share that schedule: rel_attn_kernel (16-bit stacks: the decoder, and the whole
+// model with encoder_precision "fast"), rel_attn_split_kernel (fp32 stacks of a 16-bit model:
+// the exact-duration encoder, each product as three f16 MFMAs) and rel_attn_f32_kernel (fp32
+// models, v_mfma_f32_16x16x4_f32).
 #include "acoustic_kernels.h"
 #include "common.h"
 #include "mrf_tile.h"

@@ -101,7 +101,8 @@ int tts_vocoder_forward_chunk(tts_engine* eng, const float* d_mel, const int32_t
 
 /* Acoustic model (replaces the text->spectrogram half of model.generate).
  *   d_tokens      [B][N] int32 token ids (padding ignored past d_tok_lens[b])
- *   d_dur_override optional [B][N] int32 frame counts (NULL = predicted durations)
+ *   d_dur_override optional [B][N] int32 frame counts (NULL = predicted durations; when given,
+ *                  the duration predictor is not run and d_durations returns these counts)
  *   d_mel         [B][Tcap][80] float32 output, d_mel_lens [B] int32 output
  *   d_durations   optional [B][N] int32 output of the durations actually used
  * Frames past Tcap are dropped (d_mel_lens is clamped to Tcap). */

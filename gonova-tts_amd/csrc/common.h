@@ -208,6 +208,9 @@ __device__ inline void store16(void* base, int byte_off, uint4 v) {
 
 // activation codes shared by host and device
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2, ACT_LRELU = 3, ACT_SILU = 4 };
+// compile-time activation tag (epilogues dispatch on the runtime kind once, outside their loops)
+template <int A>
+struct ActC { static constexpr int value = A; };
 
 __device__ inline float apply_act(float v, int act, float slope) {
   switch (act) {

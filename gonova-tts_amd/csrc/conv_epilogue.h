@@ -8,9 +8,9 @@ namespace tts {
 // Epilogue shared by conv_gemm_kernel and conv_split_kernel: lane (l31, hh) of a wave holds, for each 32x32 tile
 // (mt, nt), rows n = n_base + nt*32 + l31 and channels m_base + mt*32 + 8g + 4hh + [0, 4).
 //   y = ((alpha * (acc + bias)) -> act) + r1 + r2, times out_scale; transposed-conv row map.
-template <typename T, int MT, int NT>
-__device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x16 (&acc)[MT][NT], int b, int hd,
-                                              int n_base, int m_base, int ylen, int l31, int hh) {
+template <typename T, int MT, int NT, int ACT>
+__device__ __forceinline__ void conv_epilogue_act(const ConvParams& p, const f32x16 (&acc)[MT][NT], int b, int hd,
+                                                  int n_base, int m_base, int ylen, int l31, int hh) {
   T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.syb + (long long)hd * p.syh;
   const T* R1 = p.r1 ? reinterpret_cast<const T*>(p.r1) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const T* R2 = p.r2 ? reinterpret_cast<const T*>(p.r2) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
@@ -39,9 +39,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x16 
           v += bb;
         }
         if (p.alpha != 1.0f) v *= p.alpha;
-        if (p.act_out) {
+        if constexpr (ACT != ACT_NONE) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = apply_act(v[i], p.act_out, p.out_slope);
+          for (int i = 0; i < 4; ++i) v[i] = apply_act(v[i], ACT, p.out_slope);
         }
         if (R1) v += Vec4<T>::load(R1 + (long long)row * p.srr + col);
         if (R2) v += Vec4<T>::load(R2 + (long long)row * p.srr + col);
@@ -49,6 +49,19 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x16 
         Vec4<T>::store(Y + (long long)row * p.syr + col, v);
       }
     }
+  }
+}
+
+// the activation kind dispatched once per tile, outside the element loops
+template <typename T, int MT, int NT>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x16 (&acc)[MT][NT], int b, int hd,
+                                              int n_base, int m_base, int ylen, int l31, int hh) {
+  switch (p.act_out) {
+    case ACT_RELU: conv_epilogue_act<T, MT, NT, ACT_RELU>(p, acc, b, hd, n_base, m_base, ylen, l31, hh); break;
+    case ACT_TANH: conv_epilogue_act<T, MT, NT, ACT_TANH>(p, acc, b, hd, n_base, m_base, ylen, l31, hh); break;
+    case ACT_LRELU: conv_epilogue_act<T, MT, NT, ACT_LRELU>(p, acc, b, hd, n_base, m_base, ylen, l31, hh); break;
+    case ACT_SILU: conv_epilogue_act<T, MT, NT, ACT_SILU>(p, acc, b, hd, n_base, m_base, ylen, l31, hh); break;
+    default: conv_epilogue_act<T, MT, NT, ACT_NONE>(p, acc, b, hd, n_base, m_base, ylen, l31, hh); break;
   }
 }
 

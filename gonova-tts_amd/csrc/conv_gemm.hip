@@ -418,19 +418,32 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
     }
   }
   __syncthreads();  // X tile no longer read
+  // the activation is dispatched once for the whole tile: inside the element loop its runtime
+  // switch split the staging into a basic block per element and kind (same arithmetic either way)
+  auto stage_acc = [&](auto act_c) __attribute__((always_inline)) {
+    constexpr int ACT = decltype(act_c)::value;
 #pragma unroll
-  for (int j = 0; j < NT; ++j)
+    for (int j = 0; j < NT; ++j)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      f32x4 v = f32x4{acc[j][4 * g + 0], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]} + bl[g];
-      if (p.alpha != 1.0f) v *= p.alpha;
-      if (p.act_out) {
+      for (int g = 0; g < 4; ++g) {
+        // alpha always applied (x * 1.0f is exact): no per-group branch in the staging
+        const f32x4 v0 = f32x4{acc[j][4 * g + 0], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]} + bl[g];
+        f32x4 v = v0 * p.alpha;
+        if constexpr (ACT != ACT_NONE) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = apply_act(v[i], p.act_out, p.out_slope);
+          for (int i = 0; i < 4; ++i) v[i] = apply_act(v[i], ACT, p.out_slope);
+        }
+        *reinterpret_cast<uint2*>(smem + (wn * 32 * NT + j * 32 + l31) * OS16 + (wm * 32 + 8 * g + 4 * hh) * 2) =
+            pack4<T>(v);
       }
-      *reinterpret_cast<uint2*>(smem + (wn * 32 * NT + j * 32 + l31) * OS16 + (wm * 32 + 8 * g + 4 * hh) * 2) =
-          pack4<T>(v);
-    }
+  };
+  switch (p.act_out) {
+    case ACT_RELU: stage_acc(ActC<ACT_RELU>{}); break;
+    case ACT_TANH: stage_acc(ActC<ACT_TANH>{}); break;
+    case ACT_LRELU: stage_acc(ActC<ACT_LRELU>{}); break;
+    case ACT_SILU: stage_acc(ActC<ACT_SILU>{}); break;
+    default: stage_acc(ActC<ACT_NONE>{}); break;
+  }
   __syncthreads();
   const bool plain = !R1 && !R2 && p.out_scale == 1.0f;
 #pragma unroll

@@ -431,24 +431,34 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     }
     __syncthreads();
     const f32x4 bias = (p.bias && mok) ? *reinterpret_cast<const f32x4*>(p.bias + m4) : f32x4{};
+    // the activation kind is dispatched once, outside the row loop (conv_xres's epilogue)
+    auto row_pass = [&](auto act_c) __attribute__((always_inline)) {
+      constexpr int ACT = decltype(act_c)::value;
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int rl = (tid >> 5) + it * 8;
-      const int f = f0 + rl;
-      if (f >= F || !mok) continue;
-      const int b = f / p.x_rows, r = f - b * p.x_rows;
-      if (r >= (p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows)) continue;
-      f32x4 v = *reinterpret_cast<const f32x4*>(smem + rl * OSR + pc * 16) + bias;
-      if (p.alpha != 1.0f) v *= p.alpha;
-      if (p.act_out) {
+      for (int it = 0; it < NIT; ++it) {
+        const int rl = (tid >> 5) + it * 8;
+        const int f = f0 + rl;
+        if (f >= F || !mok) continue;
+        const int b = f / p.x_rows, r = f - b * p.x_rows;
+        if (r >= (p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows)) continue;
+        f32x4 v = (*reinterpret_cast<const f32x4*>(smem + rl * OSR + pc * 16) + bias) * p.alpha;  // x * 1.0f exact
+        if constexpr (ACT != ACT_NONE) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act_out, p.out_slope);
+          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], ACT, p.out_slope);
+        }
+        const long long ro = (long long)b * p.srb + (long long)r * p.srr + m4;
+        v += res[it];
+        if (p.r2) v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.r2) + ro);
+        if (p.out_scale != 1.0f) v *= p.out_scale;
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.y) + (long long)b * p.syb + (long long)r * p.syr + m4) = v;
       }
-      const long long ro = (long long)b * p.srb + (long long)r * p.srr + m4;
-      v += res[it];
-      if (p.r2) v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.r2) + ro);
-      if (p.out_scale != 1.0f) v *= p.out_scale;
-      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.y) + (long long)b * p.syb + (long long)r * p.syr + m4) = v;
+    };
+    switch (p.act_out) {
+      case ACT_RELU: row_pass(ActC<ACT_RELU>{}); break;
+      case ACT_TANH: row_pass(ActC<ACT_TANH>{}); break;
+      case ACT_LRELU: row_pass(ActC<ACT_LRELU>{}); break;
+      case ACT_SILU: row_pass(ActC<ACT_SILU>{}); break;
+      default: row_pass(ActC<ACT_NONE>{}); break;
     }
     return;
   }
@@ -470,7 +480,8 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
 
 // y[f][m] = epilogue(sum over slices of ws[s][f][m]) for every valid flat row (conv_epilogue's
 // arithmetic: ((alpha * (acc + bias)) -> act) + r1 + r2, times out_scale)
-__global__ __launch_bounds__(256) void split_reduce_kernel(ConvParams p, int S) {
+template <int ACT>
+__device__ inline void split_reduce(const ConvParams& p, int S) {
   const int F = p.B * p.x_rows;
   const int M4 = p.M / 4;
   const long long n = (long long)F * M4;
@@ -485,15 +496,25 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(ConvParams p, int S) 
     for (int s = 1; s < S; ++s) v += *reinterpret_cast<const f32x4*>(p.ws + ((long long)s * F + f) * p.M + m);
     if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + m);
     if (p.alpha != 1.0f) v *= p.alpha;
-    if (p.act_out) {
+    if constexpr (ACT != ACT_NONE) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act_out, p.out_slope);
+      for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], ACT, p.out_slope);
     }
     const long long ro = (long long)b * p.srb + (long long)r * p.srr + m;
     if (p.r1) v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.r1) + ro);
     if (p.r2) v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.r2) + ro);
     if (p.out_scale != 1.0f) v *= p.out_scale;
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.y) + (long long)b * p.syb + (long long)r * p.syr + m) = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void split_reduce_kernel(ConvParams p, int S) {
+  switch (p.act_out) {  // the activation kind dispatched once, outside the loop
+    case ACT_RELU: split_reduce<ACT_RELU>(p, S); break;
+    case ACT_TANH: split_reduce<ACT_TANH>(p, S); break;
+    case ACT_LRELU: split_reduce<ACT_LRELU>(p, S); break;
+    case ACT_SILU: split_reduce<ACT_SILU>(p, S); break;
+    default: split_reduce<ACT_NONE>(p, S); break;
   }
 }
 

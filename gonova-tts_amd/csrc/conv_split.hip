@@ -449,7 +449,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
         const long long ro = (long long)b * p.srb + (long long)r * p.srr + m4;
         v += res[it];
         if (p.r2) v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.r2) + ro);
-        if (p.out_scale != 1.0f) v *= p.out_scale;
+        v *= p.out_scale;  // exact for 1.0f: no branch
         *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.y) + (long long)b * p.syb + (long long)r * p.syr + m4) = v;
       }
     };

@@ -586,6 +586,9 @@ static bool xres_narrow(const ConvParams& p, int nt) {
 #ifndef TTS_XRES_SMALL_TILES
 #define TTS_XRES_SMALL_TILES 1
 #endif
+#ifndef TTS_XRES_NT2_MAXBLK
+#define TTS_XRES_NT2_MAXBLK 400        // 0 disables the small-grid 64-row rule below
+#endif
 // 64-row tiles (NT = 2) where 128-row tiles would leave much of the last tile of every
 // utterance empty (the encoder's 144 rows: 3 x 64 = 192 rows of work instead of 2 x 128)
 static int xres_nt(const ConvParams& p, int wm) {
@@ -594,7 +597,17 @@ static int xres_nt(const ConvParams& p, int wm) {
   if (force == 2 || force == 4) return force;
   if (!TTS_XRES_SMALL_TILES) return 4;
   const int r4 = (p.y_rows + 127) / 128 * 128, r2 = (p.y_rows + 63) / 64 * 64;
-  return 8 * r2 <= 7 * r4 ? 2 : 4;
+  if (8 * r2 <= 7 * r4) return 2;
+  // small grids (the batch-8 decoder): 64-row tiles where the 128-row grid fills under ~1.5
+  // blocks per CU but the 64-row one fills every CU, ahead of both the 128-row tiles and the
+  // narrow 64 x 64 tiles.  Measured per launch at batch 8 (same box): the FFN down-projection
+  // (M = 384, K = 4608) 63 us narrow / 57 us 128-row / 48.5 us 64-row; the pointwise conv
+  // (M = 768) 14 -> 12 us; the FFN up-projection (672 blocks) and Q/K/V (504) are faster at 128
+  // rows, hence the bound.  Same channel group, so the same bits.
+  const long long mb = (long long)((p.M + 127) / 128) * p.B * p.nh;
+  const long long b4 = (long long)(r4 / 128) * mb, b2 = (long long)(r2 / 64) * mb;
+  if (b4 < TTS_XRES_NT2_MAXBLK && b2 >= 256) return 2;
+  return 4;
 }
 
 template <typename T, int WM, int NT = 4, int OCC = TTS_XRES_OCC>

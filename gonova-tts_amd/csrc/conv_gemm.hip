@@ -233,6 +233,9 @@ constexpr int XRES_HR = 64;            // output rows per N-wave staged per half
 #define TTS_XRES_SU 4                  // more spills at 3 blocks/CU: acc + ring are live
 #endif
 constexpr int XRES_SU = TTS_XRES_SU;   // X staging loads in flight per thread
+#ifndef TTS_XRES_XFIRST
+#define TTS_XRES_XFIRST 0              // 1: X loads first, the weight ring primed after them
+#endif
 
 template <typename T>
 __device__ inline void ld8(const T* p, f32x4& a, f32x4& b) {
@@ -241,6 +244,18 @@ __device__ inline void ld8(const T* p, f32x4& a, f32x4& b) {
   a = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
   b = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
 }
+
+#ifndef TTS_XRES_STAMP
+#define TTS_XRES_STAMP 0               // diagnostic builds only: per-block phase timestamps
+#endif
+#if TTS_XRES_STAMP
+// Phase timestamps of the launches whose (M, Cin, taps) match g_xres_stamp_target, one record of
+// 8 words per block (tools/xres_stamps.py): s_memtime at entry / first group staged / MFMA loop
+// done / epilogue done, the summed staging cycles of every group, s_memrealtime at entry and end,
+// and the hardware ids.  Never built into the product library.
+__device__ int g_xres_stamp_target[3];
+__device__ unsigned long long g_xres_stamp[1 << 20];
+#endif
 
 template <typename T, int NT, int WM, int OCC = TTS_XRES_OCC>
 __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int CG) {
@@ -270,6 +285,10 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
   const int l31 = lane & 31;
   const int hh = lane >> 5;
   const int wm = wave % WM, wn = wave / WM;
+#if TTS_XRES_STAMP
+  const unsigned long long st0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long st1 = 0, ssum = 0;
+#endif
 
   const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.sxb + (long long)hd * p.sxh;
   // packed weights: [MB][taps][Cin/16][64][8]; a wave past M reads the last block (its
@@ -332,11 +351,16 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
   // quad ring, 3 deep: quad q's weights are issued while quads q-2 and q-1 compute
   for (int g0 = 0; g0 < p.Cin; g0 += CG) {
     Frag a0[4], a1[4], a2[4];
+#if TTS_XRES_STAMP
+    const unsigned long long sts = __builtin_amdgcn_s_memtime();
+#endif
+#if !TTS_XRES_XFIRST
     // first quads of the group in flight before the X loads (in-order vmcnt: they
     // complete first and are ready when the MFMA loop starts)
     TTS_LOADQ(a0, 0);
     TTS_LOADQ(a1, 1);
     TTS_LOADQ(a2, 2);
+#endif
     if (g0) __syncthreads();  // previous group's B reads are done
     const T* xg = X + g0 + cc * 8;
     for (int rb = r0; rb < R; rb += XRES_SU * rstep) {
@@ -356,7 +380,21 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
         if (rr < R) *reinterpret_cast<uint4*>(smem + rr * RS + cc * 16) = v;
       }
     }
+#if TTS_XRES_XFIRST
+    // the group's X rows were all in flight at once (one round trip); the ring's first quads
+    // follow, issued after the X registers are written out
+    TTS_LOADQ(a0, 0);
+    TTS_LOADQ(a1, 1);
+    TTS_LOADQ(a2, 2);
+#endif
     __syncthreads();
+#if TTS_XRES_STAMP
+    {
+      const unsigned long long ste = __builtin_amdgcn_s_memtime();
+      ssum += ste - sts;
+      if (g0 == 0) st1 = ste;
+    }
+#endif
     int q = 0;
     for (; q + 3 <= QT; q += 3) {  // straight-line body
       TTS_MMAQ(a0, q);
@@ -372,6 +410,9 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
 #undef TTS_LOADQ
 #undef TTS_MMAQ
 
+#if TTS_XRES_STAMP
+  const unsigned long long st2 = __builtin_amdgcn_s_memtime();
+#endif
   // ---- epilogue through LDS: fragments -> fp32 rows -> 8-channel row pieces ----
   T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.syb + (long long)hd * p.syh;
   const T* R1 = p.r1 ? reinterpret_cast<const T*>(p.r1) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
@@ -467,6 +508,21 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
     }
     store16<TTS_XRES_STORE>(Y, (int)(((long long)row * p.syr + col) * (long long)sizeof(T)), y);
   }
+#if TTS_XRES_STAMP
+  if (p.M == g_xres_stamp_target[0] && p.Cin == g_xres_stamp_target[1] && p.taps == g_xres_stamp_target[2]) {
+    __syncthreads();  // every wave's epilogue issued
+    if (tid == 0) {
+      const unsigned long long blk = blockIdx.x + (unsigned long long)gridDim.x * (blockIdx.y + (unsigned long long)gridDim.y * blockIdx.z);
+      if (blk < (1u << 17)) {
+        unsigned long long* r = g_xres_stamp + blk * 8;
+        r[0] = st0; r[1] = st1; r[2] = st2; r[3] = __builtin_amdgcn_s_memtime();
+        r[4] = ssum; r[5] = rt0; r[6] = __builtin_amdgcn_s_memrealtime();
+        r[7] = ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11)) << 32) |
+               (unsigned)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+      }
+    }
+  }
+#endif
 #else
   // staged half h holds rows wn*32*NT + 64h + [0, 64) of every N-wave, compacted to
   // staged row wn*64 + r; the row pass maps staged row sr back to its output row
@@ -690,6 +746,18 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
   if (wide) return launch_cfg<T, 1, 4, 4, 1, CKWW>(p, s);
   return launch_cfg<T, 1, 4, 4, 1, CKW>(p, s);
 }
+
+#if TTS_XRES_STAMP
+extern "C" int tts_debug_xres_target(int M, int Cin, int taps) {
+  const int t[3] = {M, Cin, taps};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_xres_stamp_target), t, sizeof(t)) == hipSuccess ? 0 : -1;
+}
+extern "C" int tts_debug_xres_stamps(unsigned long long* host, long long words) {
+  const long long n = words < (1LL << 20) ? words : (1LL << 20);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_xres_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int conv_gemm_check(const ConvParams& p, int dtype, const char** why) {
   const int epv = dtype == DT_F32 ? 4 : 8;

@@ -233,9 +233,10 @@ constexpr int XRES_HR = 64;            // output rows per N-wave staged per half
 #define TTS_XRES_SU 4                  // more spills at 3 blocks/CU: acc + ring are live
 #endif
 constexpr int XRES_SU = TTS_XRES_SU;   // X staging loads in flight per thread
-#ifndef TTS_XRES_XFIRST
-#define TTS_XRES_XFIRST 0              // 1: X loads first, the weight ring primed after them
+#ifndef TTS_XRES_UPFIRST
+#define TTS_XRES_UPFIRST 1             // transposed-conv (upsampler) launches: X-first staging (XF below)
 #endif
+constexpr int XRES_SU_XF = 9;          // XF staging: a group's X loads in flight at once (R <= 9 * rstep)
 
 template <typename T>
 __device__ inline void ld8(const T* p, f32x4& a, f32x4& b) {
@@ -257,7 +258,12 @@ __device__ int g_xres_stamp_target[3];
 __device__ unsigned long long g_xres_stamp[1 << 20];
 #endif
 
-template <typename T, int NT, int WM, int OCC = TTS_XRES_OCC>
+// XF: the group's X loads all in flight at once (one round trip instead of three), the weight
+// ring primed after them so the registers fit at three blocks per CU.  Same values staged, same
+// MFMA order: bit-identical.  Measured (same box, tools/ab_xres.sh): the stage 0-1 upsamplers
+// 155.5 -> 145.9 us and 316.4 -> 298.2 us; the acoustic GEMMs +2 % (their MFMA loops then wait on
+// the ring's first quads), so only the upsampler launches use it.
+template <typename T, int NT, int WM, int OCC = TTS_XRES_OCC, bool XF = false>
 __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int CG) {
   using MF = Mfma<T>;
   typedef typename MF::frag Frag;
@@ -354,24 +360,25 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
 #if TTS_XRES_STAMP
     const unsigned long long sts = __builtin_amdgcn_s_memtime();
 #endif
-#if !TTS_XRES_XFIRST
-    // first quads of the group in flight before the X loads (in-order vmcnt: they
-    // complete first and are ready when the MFMA loop starts)
-    TTS_LOADQ(a0, 0);
-    TTS_LOADQ(a1, 1);
-    TTS_LOADQ(a2, 2);
-#endif
+    if constexpr (!XF) {
+      // first quads of the group in flight before the X loads (in-order vmcnt: they
+      // complete first and are ready when the MFMA loop starts)
+      TTS_LOADQ(a0, 0);
+      TTS_LOADQ(a1, 1);
+      TTS_LOADQ(a2, 2);
+    }
     if (g0) __syncthreads();  // previous group's B reads are done
     const T* xg = X + g0 + cc * 8;
-    for (int rb = r0; rb < R; rb += XRES_SU * rstep) {
-      uint4 r[XRES_SU];
+    constexpr int SU = XF ? XRES_SU_XF : XRES_SU;
+    for (int rb = r0; rb < R; rb += SU * rstep) {
+      uint4 r[SU];
 #pragma unroll
-      for (int i = 0; i < XRES_SU; ++i) {
+      for (int i = 0; i < SU; ++i) {
         const int xr = min(max(x_start + min(rb + i * rstep, R - 1), 0), xlast);
         r[i] = *reinterpret_cast<const uint4*>(xg + xr * p.sxr);
       }
 #pragma unroll
-      for (int i = 0; i < XRES_SU; ++i) {
+      for (int i = 0; i < SU; ++i) {
         const int rr = rb + i * rstep;
         const int xr = x_start + rr;
         // consumed unconditionally: a load consumed only under the row mask stays "pending"
@@ -380,13 +387,13 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
         if (rr < R) *reinterpret_cast<uint4*>(smem + rr * RS + cc * 16) = v;
       }
     }
-#if TTS_XRES_XFIRST
-    // the group's X rows were all in flight at once (one round trip); the ring's first quads
-    // follow, issued after the X registers are written out
-    TTS_LOADQ(a0, 0);
-    TTS_LOADQ(a1, 1);
-    TTS_LOADQ(a2, 2);
-#endif
+    if constexpr (XF) {
+      // the group's X rows were all in flight at once (one round trip); the ring's first quads
+      // follow, issued after the X registers are written out
+      TTS_LOADQ(a0, 0);
+      TTS_LOADQ(a1, 1);
+      TTS_LOADQ(a2, 2);
+    }
     __syncthreads();
 #if TTS_XRES_STAMP
     {
@@ -666,13 +673,13 @@ static int xres_nt(const ConvParams& p, int wm) {
   return 4;
 }
 
-template <typename T, int WM, int NT = 4, int OCC = TTS_XRES_OCC>
+template <typename T, int WM, int NT = 4, int OCC = TTS_XRES_OCC, bool XF = false>
 static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s) {
   constexpr int BM = 32 * WM, BN = 32 * NT * (4 / WM);
   const size_t lds = std::max((size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16),
                               TTS_XRES_EPI16 ? (size_t)BN * (BM * 2 + 16) : (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
   dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
-  hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM, OCC>), grid, dim3(256), lds, s, p, cg);
+  hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM, OCC, XF>), grid, dim3(256), lds, s, p, cg);
   return hipGetLastError();
 }
 
@@ -699,6 +706,9 @@ static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err) {
                               : launch_xres_wm<T, 4, 4, 1>(p, cg, s);
   else if (xres_narrow(p, nt))
     *err = launch_xres_wm<T, 2, 1>(p, cg, s);
+  else if (TTS_XRES_UPFIRST && p.up_s)
+    *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, true>(p, cg, s)
+                   : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, true>(p, cg, s);
   else
     *err = nt == 2 ? launch_xres_wm<T, 4, 2>(p, cg, s) : launch_xres_wm<T, 4>(p, cg, s);
   return true;

@@ -23,7 +23,10 @@ rank with no data-path collective (weak scaling); the timed loop is bracketed by
 barriers and the max time over ranks is used.  value = samples of all ranks / max time.
 The same line carries `c4` (configs[3]: 256 mixed-length utterances owned by rank 0,
 RCCL broadcast -> per-rank length-bucketed synthesis -> RCCL P2P gather to rank 0 inside
-the timed region; strong scaling over N).
+the timed region; strong scaling over N; at N=1 no process group exists and no collective
+runs, which the line says), `streaming` (configs[4], C5: p50 first audio with predicted
+durations as a request runs it, beside the given-durations and fast-encoder variants) and
+`c1` (configs[0] through the WebSocket service with the fp32 engine).
 
 `roofline` is for the dominant kernel family (largest summed time per step: today the
 fused ResBlock-pair kernel of all four stages), timed live with hipEvents around every launch
@@ -31,11 +34,14 @@ on the stream it runs on; `roofline.kernels` lists every family the same way
 (conv_gemm_kernel, conv_xres_kernel, mrf_pair_kernel, mrf_chain_kernel, upsample_stream_kernel,
 conv_split_kernel).  `cpu_baseline` (rank 0, N=1 only) is the torch-CPU fp32
 restatement (oracle/torch_cpu.py) timed on the host cores on a bounded
-sample of C2 (4 utterances) and C3 (2 utterances).
+sample of C2 (4 utterances), C3 (2 utterances) and C1 (one 71-token sentence).
+`full_pipeline.acoustic_roofline` is the acoustic forward against the MFMA peak (80.19 GFLOP
+per utterance) with per-family splits.
 """
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -49,6 +55,12 @@ sys.path.insert(0, ROOT)
 SR = 22050
 METRIC = "audio samples/sec/GPU + real-time factor, batch-32 10s utterances @22.05kHz"
 MFMA_PEAK_TFLOPS = {"f16": 2500.0, "bf16": 2500.0, "f32": 157.3}  # dense, MI355X_MICROARCH.md
+# acoustic model: 92.82 MFLOP per mel frame at N = 144 tokens / T = 864 frames (SURVEY.md §8d,
+# BASELINE.md §2) = 80.19 GFLOP per 10 s utterance
+ACOUSTIC_FLOPS_PER_UTT = 92.82e6 * 864
+# C1 (BASELINE.json configs[0]): one sentence of N = 71 tokens x 6 frames = 426
+# frames = 109,056 samples (4.95 s); the text tokenizes to exactly 71 ids (gonova_tts_amd/text.py)
+C1_TEXT = "The quick brown fox jumps over the lazy dog and then ran to the woods."
 
 
 def parse():
@@ -67,9 +79,13 @@ def parse():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 sharded side measurement")
     ap.add_argument("--no-streaming", action="store_true", help="skip the C5 streaming latency side measurement")
     ap.add_argument("--no-full", action="store_true", help="skip the full-pipeline side measurement")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 service-latency side measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-c2-batch", type=int, default=4, help="C2 utterances in the CPU-baseline sample")
     ap.add_argument("--cpu-c3-batch", type=int, default=2, help="C3 utterances in the CPU-baseline sample")
+    ap.add_argument("--selftest-fail-rank", type=int, default=-1,
+                    help="selftest only: this rank exits with status 7 after joining the process group "
+                         "(tests/test_bench_cpu.py: the launcher must end the run, not hang)")
     return ap.parse_args()
 
 
@@ -77,7 +93,13 @@ def launch_ranks(args) -> int:
     """`bench.py --gpus N` without torch.distributed.run: start N rank processes of this
     script (one per GPU) and return the first non-zero exit status.  This process does not
     touch the GPU (torch.cuda.device_count() does not initialise HIP on this image), so the
-    children are fresh processes, never an exec of a GPU-initialised one."""
+    children are fresh processes, never an exec of a GPU-initialised one.
+
+    The children are polled together: as soon as one exits non-zero the others are
+    terminated (SIGTERM, then SIGKILL after a grace period) -- a rank that died after
+    init_process_group would otherwise leave its siblings blocked in a barrier or an RCCL
+    collective until the driver's own timeout, and an 8-GPU run would print nothing."""
+    import signal
     import socket
     import subprocess
     if args.workload != "selftest":
@@ -94,12 +116,36 @@ def launch_ranks(args) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def stop_all(grace=5.0):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        t_end = time.monotonic() + grace
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.0, t_end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
     rc = 0
-    for p in procs:
-        code = p.wait()
-        if code and not rc:
-            rc = code
-    return rc
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(i, c) for i, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                i, rc = bad[0]
+                print(f"bench.py: rank {i} exited with status {rc}; terminating the other ranks",
+                      file=sys.stderr, flush=True)
+                stop_all()
+                return rc
+            if all(c == 0 for c in codes):
+                return 0
+            time.sleep(0.2)
+    except BaseException:
+        stop_all()
+        raise
 
 
 def _cpu_model() -> str:
@@ -138,13 +184,25 @@ def cpu_baseline(b2: int, b3: int):
     m, _ = ac(ids, dur)
     w3 = voc(m)
     dt3 = time.perf_counter() - t
+    # C1: one N = 71 sentence, tokens -> waveform
+    from gonova_tts_amd.text import tokenize
+    ids1 = torch.from_numpy(np.asarray(tokenize(C1_TEXT), np.int64))[None]
+    assert ids1.shape[1] == 71
+    t = time.perf_counter()
+    m1, _ = ac(ids1, torch.full((1, 71), 6, dtype=torch.int64))
+    w1 = voc(m1)
+    dt1 = time.perf_counter() - t
     return {"value": round(wav.numel() / dt2, 1), "unit": "samples/s", "cores": threads, "kind": "port",
             "cpu_model": _cpu_model(),
             "sample": f"C2: {b2} utterances x 862 frames ({wav.numel() / SR:.1f} s audio) in {dt2:.1f} s; "
                       f"torch-CPU fp32 restatement (oracle/torch_cpu.py), {threads} threads",
             "c3": {"value": round(w3.numel() / dt3, 1), "unit": "samples/s",
                    "sample": f"C3: {b3} utterances x 144 tokens x 6 frames ({w3.numel() / SR:.1f} s audio) in "
-                             f"{dt3:.1f} s (acoustic + vocoder)"}}
+                             f"{dt3:.1f} s (acoustic + vocoder)"},
+            "c1": {"value": round(w1.numel() / dt1, 1), "unit": "samples/s", "latency_ms": round(dt1 * 1e3, 1),
+                   "rtf": round(dt1 / (w1.numel() / SR), 4),
+                   "sample": f"C1: 1 utterance x 71 tokens x 6 frames ({w1.numel() / SR:.2f} s audio) in {dt1:.2f} s "
+                             f"(acoustic + vocoder, fp32)"}}
 
 
 class Ctx:
@@ -157,13 +215,16 @@ class Ctx:
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.cpu = args.workload == "selftest"
         if self.world > 1:
+            # a bounded rendezvous / collective timeout: a rank that never arrives fails the run
+            # instead of hanging it (launch_ranks also terminates the siblings of a failed rank)
+            timeout = datetime.timedelta(seconds=float(os.environ.get("TTS_BENCH_PG_TIMEOUT", "300")))
             if self.cpu:
-                dist.init_process_group("gloo")
+                dist.init_process_group("gloo", timeout=timeout)
             else:
                 if self.local >= torch.cuda.device_count():
                     raise SystemExit(f"bench.py rank {self.rank}: LOCAL_RANK {self.local} but only "
                                      f"{torch.cuda.device_count()} HIP device(s) visible")
-                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local), timeout=timeout)
             self.world = dist.get_world_size()
             self.rank = dist.get_rank()
         if self.world != args.gpus:
@@ -261,6 +322,31 @@ def roofline(prof, elapsed, steps, dtype, traffic_for=None, prof_steps=None):
             "kernels": kernels}
 
 
+def acoustic_roofline(prof, ac_ms, B, prof_steps):
+    """The acoustic forward against the MFMA roofline: achieved = 80.19 GFLOP per utterance x B
+    / the timed acoustic step, and per kernel family (live hipEvent timing of
+    the last steps): its time per step, share of the step and, for the GEMM families and the
+    fused attention, its own FLOPs / its own time (conv FLOPs at the padded row extent:
+    the exact encoder's rows are padded to rup(N + 2, 32) = 160 per 144-token utterance)."""
+    if prof is None:
+        return None
+    achieved = ACOUSTIC_FLOPS_PER_UTT * B / (ac_ms * 1e-3) / 1e12
+    fam = {}
+    for name, (ms, fl, n) in prof.items():
+        if not n:
+            continue
+        e = {"ms_per_step": round(ms / prof_steps, 3), "launches_per_step": n // max(prof_steps, 1),
+             "share_of_step": round(ms / prof_steps / ac_ms, 4)}
+        if fl:
+            e["achieved_tflops"] = round(fl / (ms * 1e-3) / 1e12, 1)
+        fam[name] = e
+    kernel_ms = sum(v["ms_per_step"] for v in fam.values())
+    return {"bound": "mfma", "achieved": round(achieved, 1), "peak": 2500.0, "unit": "TFLOP/s",
+            "frac": round(achieved / 2500.0, 4), "flops_per_step": ACOUSTIC_FLOPS_PER_UTT * B,
+            "launches_per_step": sum(v["launches_per_step"] for v in fam.values()),
+            "kernel_ms_per_step": round(kernel_ms, 3), "families": fam}
+
+
 def bench_vocoder(ctx, args):
     torch = ctx.torch
     from gonova_tts_amd.config import vocoder_flops_per_sample
@@ -309,9 +395,11 @@ def bench_full(ctx, args, steps, warmup):
     samples = B * T * 256 * steps * ctx.world
     value = samples / el
     ac_ms = None
-    # acoustic-only timing (same inputs) to split the step
-    el_ac, _ = ctx.timed(lambda: eng.acoustic(tok, tl, T), steps, 1)
+    # acoustic-only timing (same inputs) to split the step; the live per-family timing of its
+    # last steps gives the acoustic model's own roofline
+    el_ac, prof_ac = ctx.timed(lambda: eng.acoustic(tok, tl, T), steps, 1, eng)
     ac_ms = el_ac * 1e3 / steps
+    ac_roof = acoustic_roofline(prof_ac, ac_ms, B, getattr(ctx, "prof_steps", None) or steps)
     # host end to end: token ids in host memory -> waveform in (pinned) host
     # memory, the PCIe copies inside the timed region; reported beside the device-resident value
     tok_h = tok.cpu()
@@ -334,6 +422,7 @@ def bench_full(ctx, args, steps, warmup):
     engf.close()
     return {"value": round(value, 1), "unit": "samples/s", "ms_per_step": round(el * 1e3 / steps, 3),
             "acoustic_ms_per_step": round(ac_ms, 3),
+            "acoustic_roofline": ac_roof,
             "acoustic_ms_per_step_fast_encoder": round(el_f * 1e3 / steps, 3),
             "host_e2e_ms_per_step": round(el_h * 1e3 / steps, 3),
             "host_e2e_samples_per_s": round(samples / el_h, 1),
@@ -374,26 +463,39 @@ def bench_c4(ctx, args, steps, warmup):
     m.engine.close()
     samples = int(lens.sum()) * 6 * 256 * steps
     value = samples / el
+    if ctx.world == 1:
+        comm = "single-rank path: no process group, no collective ran (dist.py ShardedSynthesis.single)"
+    else:
+        comm = f"RCCL broadcast of the tokens + P2P gather of the waveforms to rank 0 over {ctx.world} ranks, inside the timed region"
     return {"value": round(value, 1), "unit": "samples/s", "n_gpus": ctx.world, "scaling": "strong",
             "steps": steps, "warmup": warmup, "ms_per_step": round(el * 1e3 / steps, 3),
             "per_gpu_samples_per_s": round(value / ctx.world, 1),
             "x_realtime_per_gpu": round(value / ctx.world / SR, 2), "dtype": "bf16",
             "config": {"workload": f"C4 batch-{B} mixed-length utterances (N_i ~ U{{29..144}} tokens x 6 frames, "
                                    f"{int(lens.sum()) * 6 * 256 / SR:.0f} s audio), length buckets of "
-                                   f"{args.c4_bucket}, RCCL broadcast + P2P gather to rank 0 inside the timed region",
+                                   f"{args.c4_bucket}",
+                       "collectives": comm,
+                       "bucket_note": "SURVEY.md §8d specifies buckets of 32; 64 measured fastest of 32 / 64 / 128 "
+                                      "(BENCH.md) and is the default (--c4-bucket)" if args.c4_bucket != 32 else None,
                        "global_batch": B, "parallelism": f"utterance-sharded dp{ctx.world}"}}
 
 
-def bench_streaming(ctx, trials=50, B=8, N=144, chunk=32, encoder_precision="exact"):
-    """Config C5: batch-8 streaming; latency from host tokens to the first audio chunk on host."""
+def bench_streaming(ctx, trials=50, B=8, N=144, chunk=32, encoder_precision="exact", predicted=True):
+    """Config C5: batch-8 streaming; latency from host tokens to the first audio chunk on host.
+
+    predicted=True (the request path): durations come from the duration predictor (weights with
+    the duration linear at w = 0, b = ln 7, so every token gets exactly 6 frames, as C3), then
+    the host reads the frame counts (one sync) before the first vocoder chunk.  predicted=False:
+    durations given by the caller (stream_tokens(durations=...)): the predictor does not run and
+    the frame counts are known on the host without a sync."""
     torch = ctx.torch
     from gonova_tts_amd.model import GonovaTTS
     m = GonovaTTS.from_pretrained(ctx.dev.index, vocoder_dtype="bf16", acoustic_dtype="bf16",
-                                  encoder_precision=encoder_precision)
+                                  encoder_precision=encoder_precision, fixed_duration=6 if predicted else None)
     rng = np.random.default_rng(5)
     tok = rng.integers(1, 78, size=(B, N)).astype(np.int32)
     lens = np.full(B, N, np.int32)
-    dur = np.full((B, N), 6, np.int32)
+    dur = None if predicted else np.full((B, N), 6, np.int32)
     lat = []
     for i in range(trials + 5):
         torch.cuda.synchronize()
@@ -403,19 +505,68 @@ def bench_streaming(ctx, trials=50, B=8, N=144, chunk=32, encoder_precision="exa
         _ = wav.cpu()
         t = time.perf_counter() - t0
         gen.close()
+        assert int(valid[0]) == chunk * 256
         if i >= 5:
             lat.append(t * 1e3)
     m.engine.close()
     return {"p50_first_audio_ms": round(float(np.percentile(lat, 50)), 3),
             "p90_first_audio_ms": round(float(np.percentile(lat, 90)), 3), "trials": trials,
             "encoder_precision": encoder_precision,
+            "durations": "predicted (duration predictor + host read of the frame counts)" if predicted
+                         else "given by the caller (predictor skipped, no sync)",
             "config": f"C5 batch-{B} x {N} tokens x 6 frames, chunk {chunk} frames (~{chunk * 256 / SR * 1e3:.0f} ms) "
                       f"+ 16 frames context, bf16"}
+
+
+def bench_c1(ctx, trials=20):
+    """Config C1 (BASELINE.json configs[0]) on the GPU, as the reference serves it: the WebSocket
+    service (create_app, the reference's protocol) with the fp32 engine in a TestClient; one
+    client sends the 71-token sentence (seeded weights with 6 frames per token: 4.95 s of audio)
+    and the time to its first binary frame (= the whole sentence: the reference yields one frame
+    per sentence, synthesizer.py:321) and to synthesis_complete is taken over `trials` requests."""
+    from fastapi.testclient import TestClient
+    from gonova_tts_amd.model import GonovaTTS
+    from gonova_tts_amd.service.server import create_app
+
+    def factory():
+        return GonovaTTS.from_pretrained(ctx.dev.index, vocoder_dtype="f32", acoustic_dtype="f32", fixed_duration=6)
+
+    first, total, nbytes = [], [], None
+    with TestClient(create_app(factory)) as c:
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            for i in range(trials + 3):
+                t0 = time.perf_counter()
+                ws.send_text(json.dumps({"type": "synthesize", "text": C1_TEXT, "voice_id": "default"}))
+                t_first = None
+                while True:
+                    msg = ws.receive()
+                    if msg.get("bytes") is not None:
+                        if t_first is None:
+                            t_first = time.perf_counter() - t0
+                            nbytes = len(msg["bytes"])
+                    elif msg.get("text") is not None:
+                        assert json.loads(msg["text"])["type"] == "synthesis_complete"
+                        break
+                if i >= 3:
+                    first.append(t_first * 1e3)
+                    total.append((time.perf_counter() - t0) * 1e3)
+    samples = nbytes // 4
+    assert samples == 71 * 6 * 256, samples
+    p50 = float(np.percentile(first, 50))
+    return {"p50_first_frame_ms": round(p50, 3), "p90_first_frame_ms": round(float(np.percentile(first, 90)), 3),
+            "p50_request_ms": round(float(np.percentile(total, 50)), 3), "trials": trials,
+            "samples": samples, "audio_s": round(samples / SR, 3), "rtf": round(p50 * 1e-3 / (samples / SR), 5),
+            "dtype": "f32",
+            "config": "C1 single 71-token sentence (4.95 s) through the WebSocket service (create_app + TestClient, "
+                      "fp32 engine, dynamic batcher), latency from send to the first binary frame"}
 
 
 def selftest(ctx, args):
     """CPU-only check of the launcher and process group (tests/test_bench_cpu.py): every rank
     contributes its rank to a gloo all-reduce inside the same barrier-bracketed timing."""
+    if ctx.rank == args.selftest_fail_rank:
+        print(f"bench.py selftest: rank {ctx.rank} exiting on purpose", file=sys.stderr, flush=True)
+        os._exit(7)
     t = ctx.torch.tensor([float(ctx.rank)])
     el, _ = ctx.timed(lambda: ctx.dist.all_reduce(t) if ctx.world > 1 else None, 1, 0)
     return {"metric": METRIC, "value": None, "unit": "samples/s", "n_gpus": ctx.world, "steps": 1, "warmup": 0,
@@ -460,8 +611,11 @@ def main():
             out["c4"] = bench_c4(ctx, args, steps=max(2, args.steps // 3), warmup=1)
         if not args.no_streaming and ctx.rank == 0:
             out["streaming"] = bench_streaming(ctx)
-            fast = bench_streaming(ctx, encoder_precision="fast")
-            out["streaming"]["fast_encoder"] = {k: fast[k] for k in ("p50_first_audio_ms", "p90_first_audio_ms")}
+            for key, kw in (("given_durations", dict(predicted=False)), ("fast_encoder", dict(encoder_precision="fast"))):
+                r = bench_streaming(ctx, **kw)
+                out["streaming"][key] = {k: r[k] for k in ("p50_first_audio_ms", "p90_first_audio_ms")}
+        if not args.no_c1 and ctx.rank == 0 and ctx.world == 1:
+            out["c1"] = bench_c1(ctx)
     else:
         f = bench_full(ctx, args, args.steps, args.warmup)
         per_gpu = f["value"] / ctx.world

@@ -126,6 +126,14 @@ struct AcousticModel::Impl {
 
   ConvLayer conv(const GetData& get, const GetShape& shape, const std::string& w, const std::string& b, int pad,
                  const std::vector<float>* scale = nullptr, const std::vector<float>* bias_override = nullptr) {
+    try {
+      return conv_unnamed(get, shape, w, b, pad, scale, bias_override);
+    } catch (const TtsError& e) {
+      throw TtsError(e.code, w + ": " + e.what());
+    }
+  }
+  ConvLayer conv_unnamed(const GetData& get, const GetShape& shape, const std::string& w, const std::string& b, int pad,
+                         const std::vector<float>* scale, const std::vector<float>* bias_override) {
     const auto s = shape(w);
     std::vector<float> bias;
     if (bias_override) bias = *bias_override;
@@ -301,23 +309,25 @@ struct AcousticModel::Impl {
   }
 
   void reserve_fresh(int B, int N, int T) {
-    const size_t e = esz();
+    const size_t ee = dtype_size(dte), ed = dtype_size(dt);  // encoder-side / decoder-side element sizes
     const int Tm = std::max(N, T);
     const int Tp = std::max(rup(Tm, 32), enc_rows(N));
     const int dk = D / H;
     const size_t rows = (size_t)B * Tp;
-    X = alloc_ws(rows * D, e); Y = alloc_ws(rows * D, e); O = alloc_ws(rows * D, e); G = alloc_ws(rows * D, e);
-    Qu = alloc_ws(rows * D, e); Qv = alloc_ws(rows * D, e);
-    H1 = alloc_ws(rows * FFN, e); QKV = alloc_ws(rows * 3 * D, e); A = alloc_ws(rows * 2 * D, e);
-    const int Sk = rup(Tm, 16);
-    Vt = alloc_ws((size_t)B * H * dk * Sk, e);
     const size_t nrows = (size_t)B * enc_rows(N);
-    ENC = alloc_ws(nrows * D, e);
-    SPK = alloc_ws((size_t)B * D, e);
-    PB1 = alloc_ws(nrows * PRED, e); PB2 = alloc_ws(nrows * PRED, e);
+    // buffers both stacks use: the encoder's nrows in dte, the decoder's rows in dt (an fp32
+    // exact encoder of a 16-bit model needs 4-byte elements only for its own B*Np rows)
+    auto both = [&](size_t C) { return alloc_ws(std::max(nrows * C * ee, rows * C * ed), 1); };
+    X = both(D); Y = both(D); O = both(D); G = both(D);
+    Qu = both(D); Qv = both(D);
+    H1 = both(FFN); QKV = both(3 * D); A = both(2 * D);
+    Vt = alloc_ws(std::max((size_t)B * H * dk * rup(N, 16) * ee, (size_t)B * H * dk * rup(Tm, 16) * ed), 1);
+    ENC = alloc_ws(nrows * D, ee);
+    SPK = alloc_ws((size_t)B * D, ee);
+    PB1 = alloc_ws(nrows * PRED, std::max<size_t>(ee, 2)); PB2 = alloc_ws(nrows * PRED, ee);  // PB1 also holds f32 logd [B][N]
     const size_t trows = (size_t)B * rup(T, 32);
-    BEF = alloc_ws(trows * NMEL, e); MELT = alloc_ws(trows * NMEL, e);
-    PN1 = alloc_ws(trows * PRED, e); PN2 = alloc_ws(trows * PRED, e);
+    BEF = alloc_ws(trows * NMEL, ed); MELT = alloc_ws(trows * NMEL, ed);
+    PN1 = alloc_ws(trows * PRED, ed); PN2 = alloc_ws(trows * PRED, ed);
     f_pitch = (float*)alloc_ws(nrows, 4); f_energy = (float*)alloc_ws(nrows, 4); f_logd = (float*)alloc_ws(nrows, 4);
     i_dur = (int*)alloc_ws((size_t)B * N, 4);
     i_tokmap = (int*)alloc_ws((size_t)B * T, 4);
@@ -337,8 +347,16 @@ struct AcousticModel::Impl {
   }
 
   // ---------------------------------------------------------------- forward
+  // a non-GEMM launch (profiled as PK_AC_ELEM when the bench's live timing is on)
+  template <typename F>
+  void elem(hipStream_t s, F&& f) { prof_launch(PK_AC_ELEM, 0.0, s, f); }
+  template <typename F>
+  void prof_launch(int kind, double flops, hipStream_t s, F&& f) {
+    if (prof) prof->launch(kind, flops, s, f);
+    else HIP_CHECK(f());
+  }
   void ln_rows(int d, const void* in, void* out, int rows, int C, const LNParam& a, const LNParam* b, hipStream_t s) {
-    HIP_CHECK(launch_layernorm(d, in, out, rows, C, a.g, a.b, b ? b->g : nullptr, b ? b->b : nullptr, eps, s));
+    elem(s, [&] { return launch_layernorm(d, in, out, rows, C, a.g, a.b, b ? b->g : nullptr, b ? b->b : nullptr, eps, s); });
   }
 
   // one head-batched attention GEMM: Y[b,h][n][m] = sum_c X[b,h][n][c] * W[b,h][m][c]
@@ -371,14 +389,14 @@ struct AcousticModel::Impl {
       // relative-position MHSA: x = LN(x + mhsa(x))
       run(L.qkv, Xb, Tp, lens, QKV, Tp, B, dt, s, prof);
       const bool fused_attn = rel_attn_enabled() && rel_attn_supported(dt, D, H);
-      if (!fused_attn) HIP_CHECK(launch_pos_bias(dt, QKV, rows, D, L.pos_u, L.pos_v, Qu, Qv, s));
-      HIP_CHECK(launch_transpose_v(dt, QKV, lens, B, Tp, D, H, Sk, Vt, s));
+      if (!fused_attn) elem(s, [&] { return launch_pos_bias(dt, QKV, rows, D, L.pos_u, L.pos_v, Qu, Qv, s); });
+      elem(s, [&] { return launch_transpose_v(dt, QKV, lens, B, Tp, D, H, Sk, Vt, s); });
       if (fused_attn) {
         // fused flash-style relative-position attention (attention.hip); Qu / Qv formed in it
         // fp32 layers of a 16-bit model (the exact-duration encoder) in split precision, like their GEMMs
         const bool split = dt == DT_F32 && this->dt != DT_F32 && sw(SW_ATTN_SPLIT) != 0;
-        HIP_CHECK(launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale,
-                                  O, s));
+        prof_launch(PK_ATTN, 6.0 * D * (double)B * Tm * Tm, s, [&] { return launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale,
+                                  O, s); });
         run(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
         ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s);
         conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
@@ -391,7 +409,7 @@ struct AcousticModel::Impl {
       // BD[b,h][i][q] = Qv[b][i][h] . Ptab[rmax - Tm + q][h]   (q <-> rel = Tm-1-q)
       attn_gemm(dt, Qv, (long long)Tp * D, dk, D, lens, Tm, (const char*)L.ptab + (size_t)(rmax - Tm) * D * e, 0, dk, D,
                 Mbd, dk, BD, (long long)H * Tm * Sbd, (long long)Tm * Sbd, Sbd, B, s);
-      HIP_CHECK(launch_rel_softmax(dt, AC, BD, lens, B, H, Tm, Sac, Sbd, Sk, scale, P, s));
+      elem(s, [&] { return launch_rel_softmax(dt, AC, BD, lens, B, H, Tm, Sac, Sbd, Sk, scale, P, s); });
       // O[b][i][h*dk + d] = sum_j P[b,h][i][j] * Vt[b,h][d][j]
       attn_gemm(dt, P, (long long)H * Tm * Sk, (long long)Tm * Sk, Sk, lens, Tm, Vt, (long long)H * dk * Sk,
                 (long long)dk * Sk, Sk, dk, Sk, O, (long long)Tp * D, dk, D, B, s);
@@ -405,7 +423,7 @@ struct AcousticModel::Impl {
     const int dt = L.dt;
     // conv module: x = LN(x + pw2(silu(bn(dw(glu(pw1(x)))))))
     run(L.pw1, Xb, Tp, lens, A, Tp, B, dt, s, prof);
-    HIP_CHECK(launch_glu_dwconv(dt, A, lens, B, Tp, D, L.dw_w, L.dw_k, L.dw_b, G, s));
+    elem(s, [&] { return launch_glu_dwconv(dt, A, lens, B, Tp, D, L.dw_w, L.dw_k, L.dw_b, G, s); });
     run(L.pw2, G, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
     ln_rows(dt, Y, Xb, rows, D, L.ln_conv, nullptr, s);
     // FFN: x = final_LN(LN(x + 0.5 * ffn(x)))
@@ -427,7 +445,7 @@ struct AcousticModel::Impl {
       void* o = bufs[i & 1];
       run(Pr.convs[i], h, Np, lens, o, Np, B, dt, s, prof, 1.f, ACT_RELU);
       if (i + 1 < n) ln_rows(dt, o, o, B * Np, PRED, Pr.lns[i], nullptr, s);
-      else HIP_CHECK(launch_ln_linear1(dt, o, B * Np, PRED, Pr.lns[i].g, Pr.lns[i].b, eps, Pr.lin_w, Pr.lin_b, out, s));
+      else elem(s, [&] { return launch_ln_linear1(dt, o, B * Np, PRED, Pr.lns[i].g, Pr.lns[i].b, eps, Pr.lin_w, Pr.lin_b, out, s); });
       h = o;
     }
   }
@@ -446,11 +464,11 @@ struct AcousticModel::Impl {
     const float xscale = std::sqrt((float)D);
     const int Np = enc_rows(N), Tp = rup(Tcap, 32);
     // encoder
-    HIP_CHECK(launch_embed(dte, tokens, tok_lens, B, N, Np, embed, V, D, xscale, ENC, s));
+    elem(s, [&] { return launch_embed(dte, tokens, tok_lens, B, N, Np, embed, V, D, xscale, ENC, s); });
     cur_rpad = Np - N;  // encoder side: packed-row split GEMMs
     stack(enc, ENC, tok_lens, B, N, Np, s);
     if (spk && E) {  // speaker embedding (HF:1192-1196); without one HF skips the projection
-      HIP_CHECK(launch_spk_bias(dte, spk, B, E, proj_we, proj_b, D, SPK, s));
+      elem(s, [&] { return launch_spk_bias(dte, spk, B, E, proj_we, proj_b, D, SPK, s); });
       ConvParams p = conv_params_default();
       p.x = ENC; p.sxb = (long long)Np * D; p.sxr = D; p.x_len = tok_lens; p.x_rows = Np;
       p.w = proj_h.w; p.w_ld = D; p.bias = nullptr; p.wpk = proj_h.wpk;
@@ -472,14 +490,14 @@ struct AcousticModel::Impl {
     cur_rpad = 0;
     // logd is laid out [B][Np]; durations kernel reads [B][N] rows -> compact view via stride Np
     int* dur = durations ? durations : i_dur;
-    HIP_CHECK(launch_durations_strided(s, B, N, Np, tok_lens, dur_override, Tcap, dur, mel_lens));
-    HIP_CHECK(launch_var_embed_add(dte, ENC, B * Np, D, f_energy, ee_w, ee_b, f_pitch, pe_w, pe_b, s));
+    elem(s, [&] { return launch_durations_strided(s, B, N, Np, tok_lens, dur_override, Tcap, dur, mel_lens); });
+    elem(s, [&] { return launch_var_embed_add(dte, ENC, B * Np, D, f_energy, ee_w, ee_b, f_pitch, pe_w, pe_b, s); });
     // decoder rows are laid out with stride Tp; regulate writes [B][Tcap] rows
     void* Xd = X;
     if (Tp == Tcap) {
-      HIP_CHECK(launch_regulate(dte, dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, X, s));
+      elem(s, [&] { return launch_regulate(dte, dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, X, s); });
     } else {
-      HIP_CHECK(launch_regulate(dte, dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, Y, s));
+      elem(s, [&] { return launch_regulate(dte, dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, Y, s); });
       HIP_CHECK(hipMemcpy2DAsync(X, (size_t)Tp * D * dtype_size(dt), Y, (size_t)Tcap * D * dtype_size(dt),
                                  (size_t)Tcap * D * dtype_size(dt), B, hipMemcpyDeviceToDevice, s));
     }
@@ -498,11 +516,11 @@ struct AcousticModel::Impl {
     }
     // MELT rows have stride Tp; output [B][Tcap][80] float32
     if (Tp == Tcap) {
-      HIP_CHECK(launch_mel_out(dt, MELT, mel_lens, B, Tcap, NMEL, mel, s));
+      elem(s, [&] { return launch_mel_out(dt, MELT, mel_lens, B, Tcap, NMEL, mel, s); });
     } else {
       HIP_CHECK(hipMemcpy2DAsync(BEF, (size_t)Tcap * NMEL * dtype_size(dt), MELT, (size_t)Tp * NMEL * dtype_size(dt),
                                  (size_t)Tcap * NMEL * dtype_size(dt), B, hipMemcpyDeviceToDevice, s));
-      HIP_CHECK(launch_mel_out(dt, BEF, mel_lens, B, Tcap, NMEL, mel, s));
+      elem(s, [&] { return launch_mel_out(dt, BEF, mel_lens, B, Tcap, NMEL, mel, s); });
     }
   }
 

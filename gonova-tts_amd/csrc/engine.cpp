@@ -89,21 +89,37 @@ struct tts_engine {
   struct Resampler { int up, down, nq, n_pre_remove; float* hp; };
   std::vector<Resampler> resamplers;
 
-  // The workspace above is shared by every call on this engine.  A call on a stream other
-  // than the previous call's first waits for everything already enqueued on that stream
-  // (an event edge), so two callers on two streams never overwrite each other's scratch.
+  // The workspace above is shared by every call on this engine.  Every enqueuing call records
+  // order_ev on its own stream when it returns (CallOrder below); a call on a stream other than
+  // the previous call's first waits for that event, so two callers on two streams never
+  // overwrite each other's scratch.  The engine touches a caller's stream only inside that
+  // caller's own call: a C caller may destroy its stream as soon as the call has returned.
   hipStream_t last_stream = nullptr;
   bool has_last = false;
   hipEvent_t order_ev = nullptr;
   void order_after_previous(hipStream_t s) {
-    if (has_last && s != last_stream) {
-      if (!order_ev) HIP_CHECK(hipEventCreateWithFlags(&order_ev, hipEventDisableTiming));
-      HIP_CHECK(hipEventRecord(order_ev, last_stream));
-      HIP_CHECK(hipStreamWaitEvent(s, order_ev, 0));
-    }
-    last_stream = s;
-    has_last = true;
+    if (!order_ev) HIP_CHECK(hipEventCreateWithFlags(&order_ev, hipEventDisableTiming));
+    if (has_last && s != last_stream) HIP_CHECK(hipStreamWaitEvent(s, order_ev, 0));
   }
+  // records order_ev on s after the call's work (also when the call failed midway: whatever it
+  // enqueued is then ordered before the next caller's)
+  void order_record(hipStream_t s) {
+    if (order_ev && hipEventRecord(order_ev, s) == hipSuccess) {
+      last_stream = s;
+      has_last = true;
+    } else {
+      // nothing recorded: the next call on any other stream must not wait on a stale record
+      // older than this call's work, so fall back to a full device-side ordering point
+      hipStreamSynchronize(s);
+      has_last = false;
+    }
+  }
+  struct CallOrder {
+    tts_engine* e;
+    hipStream_t s;
+    CallOrder(tts_engine* e_, hipStream_t s_) : e(e_), s(s_) { e->order_after_previous(s); }
+    ~CallOrder() { e->order_record(s); }
+  };
 
   ~tts_engine() {
     hipSetDevice(device);
@@ -507,21 +523,35 @@ int tts_device_count(void) {
   return n;
 }
 
+int tts_abi_version(void) { return TTS_ABI_VERSION; }
+
 int tts_engine_create(int hip_device, const tts_config* cfg, tts_engine** out) {
+  return tts_engine_create_sized(hip_device, cfg, cfg ? sizeof(tts_config) : 0, out);
+}
+
+int tts_engine_create_sized(int hip_device, const tts_config* cfg, size_t cfg_size, tts_engine** out) {
   try {
     if (!out) throw TtsError(TTS_ERR_INVALID, "null out");
     *out = nullptr;
+    // the fields a caller's struct does not reach keep their zero defaults (ABI 1's five-int
+    // struct: cfg_size 20 -> encoder_precision EXACT); a larger struct is a newer header
+    if (cfg && cfg_size % sizeof(int) != 0) throw TtsError(TTS_ERR_INVALID, "cfg_size is not a whole number of fields");
+    if (cfg && cfg_size > sizeof(tts_config))
+      throw TtsError(TTS_ERR_INVALID, "tts_config of " + std::to_string(cfg_size) + " bytes is newer than this library (" +
+                                          std::to_string(sizeof(tts_config)) + ")");
+    tts_config c{};
+    if (cfg) std::memcpy(&c, cfg, cfg_size);
+    auto okdt = [](int d) { return d == DT_F32 || d == DT_F16 || d == DT_BF16; };
+    if (!okdt(c.vocoder_dtype) || !okdt(c.acoustic_dtype)) throw TtsError(TTS_ERR_INVALID, "bad dtype");
+    if (c.encoder_precision != TTS_ENCODER_EXACT && c.encoder_precision != TTS_ENCODER_FAST)
+      throw TtsError(TTS_ERR_INVALID, "bad encoder_precision");
     int n = 0;
     HIP_CHECK(hipGetDeviceCount(&n));
     if (hip_device < 0 || hip_device >= n)
       throw TtsError(TTS_ERR_INVALID, "hip device " + std::to_string(hip_device) + " out of range");
     std::unique_ptr<tts_engine> e(new tts_engine());
     e->device = hip_device;
-    if (cfg) e->cfg = *cfg;
-    auto okdt = [](int d) { return d == DT_F32 || d == DT_F16 || d == DT_BF16; };
-    if (!okdt(e->cfg.vocoder_dtype) || !okdt(e->cfg.acoustic_dtype)) throw TtsError(TTS_ERR_INVALID, "bad dtype");
-    if (e->cfg.encoder_precision != TTS_ENCODER_EXACT && e->cfg.encoder_precision != TTS_ENCODER_FAST)
-      throw TtsError(TTS_ERR_INVALID, "bad encoder_precision");
+    e->cfg = c;
     HIP_CHECK(hipSetDevice(hip_device));
     *out = e.release();
     return TTS_OK;
@@ -597,7 +627,7 @@ int tts_vocoder_forward(tts_engine* eng, const float* d_mel, const int32_t* d_me
   return guarded(eng, [&] {
     if (!eng->finalized) throw TtsError(TTS_ERR_STATE, "finalize first");
     if (!d_mel || !d_mel_lens || !d_wav || B <= 0 || T <= 0) throw TtsError(TTS_ERR_INVALID, "bad vocoder args");
-    eng->order_after_previous((hipStream_t)stream);
+    tts_engine::CallOrder order(eng, (hipStream_t)stream);
     eng->vocoder_forward(d_mel, d_mel_lens, B, T, d_wav, (long long)T * eng->voc.hop, (hipStream_t)stream);
   });
 }
@@ -610,7 +640,7 @@ int tts_vocoder_forward_chunk(tts_engine* eng, const float* d_mel, const int32_t
         ctx_left + T_chunk > T_win)
       throw TtsError(TTS_ERR_INVALID, "bad chunk args");
     hipStream_t s = (hipStream_t)stream;
-    eng->order_after_previous(s);
+    tts_engine::CallOrder order(eng, s);
     const int hop = eng->voc.hop;
     eng->reserve_chunk(B, T_win);
     eng->vocoder_forward(d_mel, d_win_lens, B, T_win, eng->vchunk_wav, (long long)T_win * hop, s);
@@ -629,7 +659,7 @@ int tts_acoustic_forward_spk(tts_engine* eng, const int32_t* d_tokens, const int
       throw TtsError(TTS_ERR_INVALID, "bad acoustic args");
     if (d_spk_emb && eng->ac.speaker_dim() && spk_dim != eng->ac.speaker_dim())
       throw TtsError(TTS_ERR_INVALID, "speaker embedding size does not match the model's projection");
-    eng->order_after_previous((hipStream_t)stream);
+    tts_engine::CallOrder order(eng, (hipStream_t)stream);
     eng->ac.forward(d_tokens, d_tok_lens, B, N, d_dur_override, d_mel, d_mel_lens, Tcap, d_durations, d_spk_emb,
                     (hipStream_t)stream);
   });
@@ -659,6 +689,14 @@ int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops
 
 int tts_set_switch(const char* name, int value) {
   if (tts::sw_set(name, value)) {
+    g_last_error = std::string("unknown switch: ") + (name ? name : "(null)");
+    return TTS_ERR_INVALID;
+  }
+  return TTS_OK;
+}
+
+int tts_get_switch(const char* name, int* value) {
+  if (!value || tts::sw_get(name, value)) {
     g_last_error = std::string("unknown switch: ") + (name ? name : "(null)");
     return TTS_ERR_INVALID;
   }
@@ -710,7 +748,7 @@ int tts_resample_poly(tts_engine* eng, const float* d_in, int64_t in_stride, con
       eng->resamplers.push_back({up, down, nq, npr, d});
       rs = &eng->resamplers.back();
     }
-    eng->order_after_previous((hipStream_t)stream);
+    tts_engine::CallOrder order(eng, (hipStream_t)stream);
     HIP_CHECK(launch_resample_poly(d_in, in_stride, d_in_lens, B, up, down, rs->nq, rs->n_pre_remove, rs->hp, d_out,
                                    out_stride, out_cap, d_out_lens, (hipStream_t)stream));
   });

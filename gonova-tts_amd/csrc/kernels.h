@@ -48,7 +48,9 @@ hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s);
 
 // kernel family a launch runs as (live profiling buckets; tts_engine_profile_read_kinds)
 enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_RETIRED = 2 /* mrf_fused, removed */, PK_MRF_PAIR = 3, PK_MRF_CHAIN = 4, PK_UPSAMPLE = 5,
-                      PK_CONV_SPLIT = 6, PK_N = 7 };
+                      PK_CONV_SPLIT = 6, PK_ATTN = 7 /* fused relative-position attention */,
+                      PK_AC_ELEM = 8 /* the acoustic model's non-GEMM launches: LN, GLU/depthwise, transposes, adaptor */,
+                      PK_N = 9 };
 int conv_gemm_kind(int dtype, const ConvParams& p);
 
 // fp32 conv as three f16 MFMAs (conv_split.hip): an fp32 layer whose ConvParams::wpk is a

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -173,6 +174,11 @@ inline ConvLayer make_conv(const std::vector<float>& w, int co, int ci, int k, c
     for (int c = 0; c < ci; ++c)
       for (int j = 0; j < k; ++j) p[((size_t)o * k + j) * ci + c] = w[((size_t)o * ci + c) * k + j] * s;
   }
+  if (dt == DT_F32 && split)  // the split halves are f16: hi = f16(w) must be finite (tts_hip.h, TTS_ENCODER_EXACT)
+    for (float v : p)
+      if (!(std::fabs(v) < 65504.f))
+        throw TtsError(TTS_ERR_INVALID, "weight magnitude " + std::to_string(v) +
+                                            " outside the f16 range of the exact-duration encoder (use encoder_precision fast or an fp32 model)");
   ConvLayer L;
   L.w = upload(p, dt);
   allocs.push_back(L.w);
@@ -220,6 +226,19 @@ struct Profiler {
     if (ms) *ms = tm;
     if (fl) *fl = tf;
     if (n) *n = tc;
+  }
+  // one launch (a callable returning hipError_t) bracketed by events when profiling is on
+  template <typename F>
+  void launch(int kind, double flops, hipStream_t s, F&& f) {
+    if (!on) {
+      HIP_CHECK(f());
+      return;
+    }
+    Rec r{get(), get(), flops, kind};
+    HIP_CHECK(hipEventRecord(r.a, s));
+    HIP_CHECK(f());
+    HIP_CHECK(hipEventRecord(r.b, s));
+    recs.push_back(r);
   }
   ~Profiler() {
     for (auto& r : recs) { hipEventDestroy(r.a); hipEventDestroy(r.b); }

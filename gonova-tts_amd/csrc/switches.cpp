@@ -40,4 +40,15 @@ int sw_set(const char* name, int value) {
   return -1;
 }
 
+int sw_get(const char* name, int* value) {
+  std::call_once(g_once, init);
+  if (!name || !value) return -1;
+  for (int i = 0; i < SW_N; ++i)
+    if (!strcmp(name, kNames[i])) {
+      *value = g_val[i].load(std::memory_order_relaxed);
+      return 0;
+    }
+  return -1;
+}
+
 }  // namespace tts

@@ -25,5 +25,6 @@ enum Sw : int {
 
 int sw(Sw s);                              // current value, -1 = not set
 int sw_set(const char* name, int value);   // 0, or -1 for an unknown name
+int sw_get(const char* name, int* value);  // 0 (value = current setting, -1 = not set), or -1 for an unknown name
 
 }  // namespace tts

@@ -60,7 +60,9 @@ class TtsConvDesc(ctypes.Structure):
 _VP, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 C_API = [
     ("tts_device_count", _I, []),
+    ("tts_abi_version", _I, []),
     ("tts_engine_create", _I, [_I, ctypes.POINTER(TtsConfig), ctypes.POINTER(_VP)]),
+    ("tts_engine_create_sized", _I, [_I, ctypes.POINTER(TtsConfig), ctypes.c_size_t, ctypes.POINTER(_VP)]),
     ("tts_engine_set_weight", _I, [_VP, ctypes.c_char_p, _VP, ctypes.POINTER(ctypes.c_int64), _I]),
     ("tts_engine_finalize", _I, [_VP]),
     ("tts_engine_reserve", _I, [_VP, _I, _I, _I]),
@@ -78,6 +80,7 @@ C_API = [
     ("tts_resample_poly", _I, [_VP, _VP, ctypes.c_int64, _VP, _I, _I, _I, _VP, ctypes.c_int64, _I, _VP, _VP]),
     ("tts_resample_filter", _I, [_I, _I, ctypes.POINTER(ctypes.c_double), _I, ctypes.POINTER(ctypes.c_int)]),
     ("tts_set_switch", _I, [ctypes.c_char_p, _I]),
+    ("tts_get_switch", _I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     ("tts_last_error", ctypes.c_char_p, []),
     ("tts_op_conv1d", _I, [_I, ctypes.POINTER(TtsConvDesc), _VP]),
 ]
@@ -124,17 +127,27 @@ def set_switch(name: str, value: int = -1):
     check(lib.tts_set_switch(name.encode(), int(value)), "tts_set_switch")
 
 
+def get_switch(name: str) -> int:
+    """Current value of a kernel-path switch (its environment value or the last set_switch;
+    -1 = not set, the built-in default)."""
+    lib = load_library()
+    v = ctypes.c_int()
+    check(lib.tts_get_switch(name.encode(), ctypes.byref(v)), "tts_get_switch")
+    return v.value
+
+
 @contextlib.contextmanager
 def switches(**values):
     """Context manager form of set_switch: `with switches(TTS_MRF_CHAIN=0): ...`; every named
-    switch goes back to its default on exit."""
+    switch goes back to the value it had before (e.g. one set in the environment) on exit."""
+    saved = {k: get_switch(k) for k in values}
     try:
         for k, v in values.items():
             set_switch(k, v)
         yield
     finally:
-        for k in values:
-            set_switch(k, -1)
+        for k, v in saved.items():
+            set_switch(k, v)
 
 
 def check(rc: int, what: str = ""):
@@ -182,8 +195,8 @@ class HipEngine:
         cfg = TtsConfig(DTYPES[vocoder_dtype], DTYPES[acoustic_dtype], max_batch, max_frames, max_tokens,
                         ENCODER_PRECISION[encoder_precision])
         h = ctypes.c_void_p()
-        check(self.lib.tts_engine_create(self.device_index, ctypes.byref(cfg), ctypes.byref(h)),
-              "tts_engine_create")
+        check(self.lib.tts_engine_create_sized(self.device_index, ctypes.byref(cfg), ctypes.sizeof(cfg),
+                                               ctypes.byref(h)), "tts_engine_create")
         self.handle = h
         self.hop = 256
         self._finalized = False
@@ -318,7 +331,7 @@ class HipEngine:
         return ms.value, fl.value, n.value
 
     PROFILE_KINDS = ("conv_gemm_kernel", "conv_xres_kernel", "retired", "mrf_pair_kernel", "mrf_chain_kernel",
-                     "upsample_stream_kernel", "conv_split_kernel")
+                     "upsample_stream_kernel", "conv_split_kernel", "rel_attn_kernel", "acoustic_elementwise")
 
     def profile_read_kinds(self):
         """-> {kernel name: (summed ms, algorithmic FLOPs, launch count)}; resets."""

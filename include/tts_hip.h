@@ -38,6 +38,7 @@
 #ifndef TTS_HIP_H
 #define TTS_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -54,6 +55,18 @@ enum { TTS_DTYPE_F32 = 0, TTS_DTYPE_F16 = 1, TTS_DTYPE_BF16 = 2 };
 
 typedef struct tts_engine tts_engine;
 
+/* ABI history (INTEGRATION.md "Changelog"):
+ *   1  tts_config of five ints (no encoder_precision)
+ *   2  tts_config gains encoder_precision (sixth int)
+ *   3  tts_engine_create_sized / tts_abi_version / tts_get_switch; stream ordering records
+ *      on the caller's stream at the end of each call (a caller may destroy its stream after
+ *      the call returns) */
+#define TTS_ABI_VERSION 3
+int tts_abi_version(void);
+
+/* Engine configuration.  Fields are only ever appended; a caller built against an older
+ * header passes its struct's size to tts_engine_create_sized and the fields past it keep
+ * their zero defaults. */
 typedef struct tts_config {
   int vocoder_dtype;   /* TTS_DTYPE_*: compute/storage dtype of vocoder activations */
   int acoustic_dtype;  /* TTS_DTYPE_*: compute/storage dtype of acoustic activations */
@@ -70,12 +83,21 @@ typedef struct tts_config {
  * acoustic_dtype.  FAST (1): the whole acoustic model runs in acoustic_dtype (durations can
  * round differently near .5).  With acoustic_dtype = F32 both are plain fp32. */
 enum { TTS_ENCODER_EXACT = 0, TTS_ENCODER_FAST = 1 };
+/* Range limit of EXACT: its split GEMMs and attention hold every fp32 operand as two f16 halves,
+ * so activations and encoder-side weights must stay below 65504 in magnitude (f16 max).
+ * tts_engine_finalize rejects encoder-side weights outside that range (TTS_ERR_INVALID naming
+ * the tensor; use FAST or an fp32 acoustic_dtype for such a checkpoint); activations are not
+ * checked on the device (LayerNorm bounds the residual stream to O(sqrt(D)) times its gain). */
 
 /* Number of HIP devices visible to this process. */
 int tts_device_count(void);
 
-/* Engine lifetime (replaces ChatterboxTTS.from_pretrained, synthesizer.py:185). */
+/* Engine lifetime (replaces ChatterboxTTS.from_pretrained, synthesizer.py:185).
+ * tts_engine_create reads a whole tts_config of THIS header; tts_engine_create_sized reads
+ * cfg_size bytes of it (sizeof(tts_config) of the caller's header; smaller = an older layout,
+ * the missing fields zero; larger than this library's struct = TTS_ERR_INVALID). */
 int tts_engine_create(int hip_device, const tts_config* cfg, tts_engine** out);
+int tts_engine_create_sized(int hip_device, const tts_config* cfg, size_t cfg_size, tts_engine** out);
 /* Host fp32 tensor in HF state_dict naming (e.g. "resblocks.3.convs1.2.weight"). */
 int tts_engine_set_weight(tts_engine* eng, const char* name, const float* host_data,
                           const int64_t* shape, int ndim);
@@ -128,7 +150,9 @@ int tts_engine_profile(tts_engine* eng, int enable);
 int tts_engine_profile_read(tts_engine* eng, double* gemm_ms, double* gemm_flops, int* n_launches);
 /* The same, split by kernel family into arrays of nkinds entries:
  * 0 = conv_gemm_kernel, 1 = conv_xres_kernel, 2 = (retired: round 1's whole-stage kernel), 3 = mrf_pair_kernel,
- * 4 = mrf_chain_kernel, 5 = upsample_stream_kernel, 6 = conv_split_kernel. */
+ * 4 = mrf_chain_kernel, 5 = upsample_stream_kernel, 6 = conv_split_kernel, 7 = the fused relative-position
+ * attention (FLOPs 6*D*B*Tm^2: scores, relative-position scores and P.V at the padded extent), 8 = the
+ * acoustic model's other launches (LayerNorm, GLU/depthwise, transposes, variance adaptor; no FLOPs). */
 int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, double* flops, int* n_launches);
 
 /* Process-wide switch selecting an alternative kernel path (A/B runs, the parity tests'
@@ -138,6 +162,8 @@ int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, doubl
  * starts from its environment variable, read once; value -1 restores the built-in default.
  * Applies to launches enqueued after the call (use from one thread while no forward runs). */
 int tts_set_switch(const char* name, int value);
+/* Current value of a switch (-1 = not set), so a caller can restore what it changed. */
+int tts_get_switch(const char* name, int* value);
 
 /* Rational-rate resampling of waveforms (22,050 -> 24,000 Hz for
  * clients that assume the reference's hard-coded 24 kHz, synthesizer.py:119 /

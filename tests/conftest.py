@@ -40,14 +40,16 @@ def pytest_sessionfinish(session, exitstatus):
 @pytest.fixture
 def switch():
     """set_switch(name, value) for one test (gonova_tts_amd.engine.set_switch: the process-wide
-    kernel-path switches of include/tts_hip.h); every switch it touched is reset afterwards."""
-    from gonova_tts_amd.engine import set_switch
-    touched = set()
+    kernel-path switches of include/tts_hip.h); every switch it touched goes back to the value
+    it had before the test (an environment setting included)."""
+    from gonova_tts_amd.engine import get_switch, set_switch
+    saved = {}
 
     def setter(name, value):
-        touched.add(name)
+        if name not in saved:
+            saved[name] = get_switch(name)
         set_switch(name, -1 if value is None else int(value))
 
     yield setter
-    for name in touched:
-        set_switch(name, -1)
+    for name, v in saved.items():
+        set_switch(name, v)

@@ -44,3 +44,17 @@ def test_more_gpus_than_visible_fails_loudly():
     r = _run(["--gpus", "64"])
     assert r.returncode == 2
     assert "HIP device(s) visible" in r.stderr
+
+
+def test_failed_rank_ends_the_run_within_seconds():
+    """A rank that dies after joining the process group: the launcher terminates its siblings
+    (blocked in the barrier) and returns the failed rank's status, well before any timeout."""
+    import time
+    t0 = time.monotonic()
+    r = _run(["--gpus", "3", "--workload", "selftest", "--selftest-fail-rank", "1"],
+             env_extra={"TTS_BENCH_PG_TIMEOUT": "120"}, timeout=90)
+    took = time.monotonic() - t0
+    assert r.returncode == 7, (r.returncode, r.stderr[-2000:])
+    assert "rank 1 exited with status 7" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert took < 60, took

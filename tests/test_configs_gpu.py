@@ -136,3 +136,70 @@ def test_c2_full_size_window_matches_oracle():
         check(f"C2.wav[b={b}] f16 frames {w0}-{w1}", wav[b, w0 * HOP:w1 * HOP],
               oracle_window(mel[b], w0, w1, vw), kind="voc_f16")
     eng.close()
+
+
+# ----------------------------------------------------------------------------- C4
+def test_c4_sharded_batch256_matches_solo_and_oracle():
+    """C4 itself (BASELINE.json configs[3]): 256 utterances of N_i ~ U{29..144} tokens x 6
+    frames, length buckets of 64, bf16, through dist.ShardedSynthesis exactly as bench.py runs
+    it -- once inside an RCCL process group (backend "nccl" = RCCL, one rank on this 1-GPU box:
+    the token broadcast and the size all-gather run as RCCL collectives; the P2P gather has no
+    peer here, tests/test_dist_cpu.py covers it with gloo ranks) and once with no group.
+    Checks: every utterance returns at 6 * 256 * N_i samples, both runs agree bit for bit,
+    8 utterances (shortest, longest and 6 between) equal the same utterance synthesized alone
+    bit for bit, and 2 match the oracle on 2 s windows."""
+    import datetime
+    import socket
+
+    import torch.distributed as dist
+
+    from gonova_tts_amd.dist import ShardedSynthesis
+
+    B, bucket = 256, 64
+    m = GonovaTTS.from_pretrained(DEV, vocoder_dtype="bf16", acoustic_dtype="bf16", max_batch=bucket,
+                                  max_frames=864, max_tokens=144)
+    rng = np.random.default_rng(7)  # bench.py's C4 draw
+    lens = rng.integers(29, 145, size=B).astype(np.int32)
+    tok = np.zeros((B, 144), np.int32)
+    for i, L in enumerate(lens):
+        tok[i, :L] = rng.integers(1, 78, size=L)
+
+    def durs(t, l):
+        return np.where(np.arange(t.shape[1])[None, :] < l[:, None], 6, 0).astype(np.int32)
+
+    def synth(t, l):
+        return m.synthesize_tokens(t, l, durations=durs(t, l), host_lens=False)
+
+    plain = ShardedSynthesis(synth, torch.device(DEV), bucket=bucket).run(tok, lens)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            timeout=datetime.timedelta(seconds=60), device_id=torch.device(DEV))
+    try:
+        sh = ShardedSynthesis(synth, torch.device(DEV), bucket=bucket)
+        assert not sh.single and sh.world == 1
+        out = sh.run(tok, lens)
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    for i in range(B):
+        assert out[i] is not None and out[i].shape == (int(lens[i]) * 6 * HOP,), i
+        assert np.isfinite(out[i]).all(), i
+        assert np.array_equal(out[i], plain[i]), i
+    order = np.argsort(lens, kind="stable")
+    picks = [int(order[j]) for j in np.linspace(0, B - 1, 8).round().astype(int)]
+    for u in picks:
+        L = int(lens[u])
+        solo, solo_lens = m.synthesize_tokens(tok[u:u + 1, :L], lens[u:u + 1], durations=durs(tok[u:u + 1, :L], lens[u:u + 1]))
+        solo = solo.cpu().numpy()[0, :int(solo_lens[0])]
+        assert np.array_equal(out[u], solo), (u, L, float(np.abs(out[u] - solo).max()))
+    aw, vw = make_acoustic_weights(0), make_vocoder_weights(0)
+    for u in (picks[0], picks[-1]):  # the shortest and the longest utterance
+        L = int(lens[u])
+        ref = acoustic_forward(tok[u, :L], aw, durations=np.full(L, 6, np.int32))
+        w1 = L * 6
+        w0 = w1 - 172  # the last 2 s, through the utterance's end
+        check(f"C4.wav[u={u}, N={L}] bf16 frames {w0}-{w1}", out[u][w0 * HOP:w1 * HOP],
+              oracle_window(ref["mel"], w0, w1, vw), kind="e2e_bf16")
+    m.engine.close()

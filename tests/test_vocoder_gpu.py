@@ -328,3 +328,39 @@ def test_two_streams_share_one_engine(vw):
     torch.cuda.synchronize()
     for a, b in outs:
         assert torch.equal(a, refA) and torch.equal(b, refB)
+
+
+def test_caller_stream_destroyed_between_calls(vw):
+    """A C caller may destroy its per-request stream as soon as a call returns (advisor finding:
+    the engine used to record its ordering event on the PREVIOUS call's stream at the start of
+    the next call).  Stream A runs a forward and is destroyed; the next call, on another
+    stream, must succeed and match, and so must a third on a fresh stream."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+
+    class RawStream:  # what engine._stream_ptr reads from a torch stream
+        def __init__(self):
+            self.ptr = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(self.ptr)) == 0
+            self.cuda_stream = self.ptr.value
+
+    eng = engine_for("f16", vw)
+    rng = np.random.default_rng(43)
+    mel = torch.from_numpy(rng.standard_normal((2, 64, 80)).astype(np.float32)).to(DEV)
+    ref = eng.vocoder(mel).clone()
+    torch.cuda.synchronize()
+    a = RawStream()
+    outA = eng.vocoder(mel, stream=a)
+    assert hip.hipStreamSynchronize(a.ptr) == 0
+    assert hip.hipStreamDestroy(a.ptr) == 0
+    outB = eng.vocoder(mel)  # torch's current stream: a different stream than A
+    torch.cuda.synchronize()
+    c = RawStream()
+    outC = eng.vocoder(mel, stream=c)
+    assert hip.hipStreamSynchronize(c.ptr) == 0
+    assert hip.hipStreamDestroy(c.ptr) == 0
+    assert torch.equal(outA, ref) and torch.equal(outB, ref) and torch.equal(outC, ref)

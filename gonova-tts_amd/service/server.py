@@ -32,6 +32,11 @@ from .queues import TTSQueueManager
 logger = logging.getLogger(__name__)
 
 
+# the sentences the reference warms its model up with, in order (synthesizer.py:197-207)
+WARMUP_TEXTS = ("Hello.", "Hello, this is a warmup test.",
+                "The quick brown fox jumps over the lazy dog, and this is a longer sentence to warm up the model properly.")
+
+
 class RateLimiter:
     """Sliding-window admission per client (reference server.py:358-382)."""
 
@@ -77,7 +82,7 @@ class TTSService:
     async def start(self):
         loop = asyncio.get_running_loop()
         self.model = await loop.run_in_executor(None, self.model_factory)
-        for text in ("Hello.", "Hello, this is a warmup test."):  # reference warmups (synthesizer.py:199-207)
+        for text in WARMUP_TEXTS:  # the reference's three warmups (synthesizer.py:197-207)
             await loop.run_in_executor(None, self.model.generate_batch, [text])
         self.queues = TTSQueueManager(sample_rate=getattr(self.model, "sr", 22050))
         await self.queues.start()
@@ -150,12 +155,14 @@ class TTSService:
         except WebSocketDisconnect:
             pass
         finally:
+            # bookkeeping first, before any await: when the handler itself is cancelled (the ASGI
+            # server tearing the connection down), every later await raises again and would skip it
             for t in tasks:
                 t.cancel()
-            await asyncio.gather(*tasks, return_exceptions=True)
             self.queues.unregister_connection(conn_id)
             self.sockets.pop(conn_id, None)
             self.active_connections -= 1
+            await asyncio.gather(*tasks, return_exceptions=True)
 
     async def handle_message(self, ws, conn_id: str, data: dict):
         """One client message (reference server.py:215-256)."""

@@ -173,3 +173,61 @@ def test_bad_messages_do_not_end_the_connection():
             ws.send_text(json.dumps({"type": "synthesize", "text": "Still here."}))
             frames, final = recv_until_complete(ws)
             assert len(frames) == 1 and final == {"type": "synthesis_complete", "chunk_id": 1}
+
+
+def test_ws_transcript_matches_reference_fixture():
+    """The reference service itself, recorded under TestClient with a fake chatterbox model
+    (tests/golden/make_ws_golden.py -> ws_transcript.json), against this build's
+    service driven with the same fake outputs (tests/golden/ws_fake.py): /health's 503 before
+    load (server.py:447-454), every binary frame of every request byte for byte (one frame of
+    raw float32 PCM per sentence, server.py:150-156, 279-280), the final
+    synthesis_complete message (server.py:159-164, 283-286), the sentences handed to the model
+    and the warmup texts (synthesizer.py:197-207, 257), and /metrics after the session
+    (queue_manager.py:282-291; the final marker counts as a chunk)."""
+    import hashlib
+    import os
+
+    from tests.golden.ws_fake import REQUESTS, fake_audio
+
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ws_transcript.json")))
+    seen = []
+
+    class TranscriptModel:
+        sr = 24000
+
+        def generate_batch(self, texts):
+            seen.extend(texts)
+            return [fake_audio(t) for t in texts]
+
+    app = create_app(lambda: TranscriptModel())
+    r = TestClient(app).get("/health")  # startup has not run: no model
+    assert {"status_code": r.status_code, "body": r.json()} == gold["health_before_load"]
+    with TestClient(app) as c:
+        warm = list(seen)
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            for req, g in zip(REQUESTS, gold["requests"]):
+                assert req == g["message"]
+                ws.send_text(json.dumps(req))
+                frames = []
+                while True:
+                    m = ws.receive()
+                    if m.get("bytes") is not None:
+                        frames.append({"bytes": len(m["bytes"]), "sha256": hashlib.sha256(m["bytes"]).hexdigest()})
+                    elif m.get("text") is not None:
+                        final = json.loads(m["text"])
+                        break
+                assert frames == g["frames"], req["text"]
+                assert final == g["final"]
+        # the server unregisters the closed connection asynchronously
+        for _ in range(100):
+            metrics = c.get("/metrics").json()
+            if metrics["active_connections"] == 0:
+                break
+            time.sleep(0.02)
+    ref_texts = [x["text"] for x in gold["generate_calls"]]
+    assert warm == ref_texts[:len(warm)]  # the reference's warmup sentences, in order
+    # then every sentence as the reference split them (the batcher orders a batch by length, so
+    # the engine sees them in another order; the frames above came back in the reference's)
+    assert sorted(seen[len(warm):]) == sorted(ref_texts[len(warm):])
+    for k, v in gold["metrics"].items():
+        assert metrics[k] == v, (k, metrics[k], v)

@@ -25,6 +25,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // 16-byte staging registers: a native vector, so a global -> register -> LDS copy is a plain
 // load / store pair (a uint4 struct copy becomes a memcpy that can land in scratch)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // ---------------------------------------------------------------------------
 // MFMA traits: one 32x32 output tile per wave-instruction.
@@ -170,12 +171,20 @@ __device__ inline uint4 lrelu_chunk(uint4 u, float slope) {
 // at launch): max(x, slope*x) -- packed f16, bf16 pairs, or f32 per element for f32.  Same
 // results as lrelu_chunk in that range, without its runtime slope branch (a uniform branch in
 // an epilogue splits the block the scheduler interleaves MFMAs across).
+// f16 max of two packed pairs without the IEEE-mode quieting the compiler puts in front of a
+// max of loaded values (v_pk_max_f16 x, x, x per operand: 12 instead of 8 instructions per
+// chunk); identical results for non-NaN inputs
+__device__ inline unsigned pk_max_f16(unsigned a, unsigned b) {
+  unsigned r;
+  asm("v_pk_max_f16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 template <typename T>
 __device__ inline uint4 lrelu_unit(uint4 u, float slope) {
   if constexpr (sizeof(T) == 2 && __is_same(T, _Float16)) {
-    half8 v = *reinterpret_cast<half8*>(&u);
-    v = __builtin_elementwise_max(v, v * (_Float16)slope);
-    return *reinterpret_cast<uint4*>(&v);
+    const half8 v = *reinterpret_cast<half8*>(&u);
+    const uint4 m = __builtin_bit_cast(uint4, v * (_Float16)slope);
+    return uint4{pk_max_f16(u.x, m.x), pk_max_f16(u.y, m.y), pk_max_f16(u.z, m.z), pk_max_f16(u.w, m.w)};
   } else if constexpr (__is_same(T, bf16_t)) {
     return uint4{lrelu_bf16x2(u.x, slope), lrelu_bf16x2(u.y, slope), lrelu_bf16x2(u.z, slope),
                  lrelu_bf16x2(u.w, slope)};

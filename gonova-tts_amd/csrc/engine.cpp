@@ -464,14 +464,17 @@ struct tts_engine {
               post_done = true;
             }
             const double fl = 2.0 * 2.0 * ch * (double)ch * pp.k * (double)B * Tout;
+            // C = 32 pairs without conv_post: the software-pipelined kernel (bit-identical)
+            const bool sp = !pp.post_wpk && sw(SW_PAIR_SP) != 0 && mrf_pair_sp_supported(dt, ch, pp.k);
+            auto launch = [&] { return sp ? mrf_pair_sp_launch(dt, ch, pp, s) : mrf_pair_launch(dt, ch, pp, s); };
             if (prof.on) {
               Profiler::Rec r{prof.get(), prof.get(), fl, PK_MRF_PAIR};
               HIP_CHECK(hipEventRecord(r.a, s));
-              HIP_CHECK(mrf_pair_launch(dt, ch, pp, s));
+              HIP_CHECK(launch());
               HIP_CHECK(hipEventRecord(r.b, s));
               prof.recs.push_back(r);
             } else {
-              HIP_CHECK(mrf_pair_launch(dt, ch, pp, s));
+              HIP_CHECK(launch());
             }
             h = pp.y;
           }

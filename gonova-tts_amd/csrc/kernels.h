@@ -103,6 +103,9 @@ bool upsample_stream_supported(int dtype, int Cin, int M, int taps);
 hipError_t upsample_stream_launch(int dtype, int Cin, int M, const UpsampleParams& p, hipStream_t s);
 // the pair launch can carry conv_post (C, k and post_k it was compiled for)
 bool mrf_pair_post_supported(int dtype, int C, int post_k);
+// software-pipelined pair for C = 32 (mrf_pair_sp.hip): same arithmetic, bit-identical; no conv_post
+bool mrf_pair_sp_supported(int dtype, int C, int k);
+hipError_t mrf_pair_sp_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s);
 hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s);
 
 // Fused resblock (mrf_chain.hip): the three pairs of one resblock (dilations 1, 3, 5) in one

@@ -190,6 +190,43 @@ __device__ inline uint4 epi_row(uint4 y, uint4 h, bool acc, uint4 s, float scale
   }
 }
 
+// row pass on 4 elements (one lane's MFMA output quad), rounded exactly as epi_row rounds them
+template <typename T>
+__device__ inline uint2 epi_row4(uint2 y, uint2 h, bool acc, uint2 s, float scale) {
+  if constexpr (__is_same(T, half_t)) {
+    half4 v = __builtin_bit_cast(half4, y) + __builtin_bit_cast(half4, h);
+    if (acc) v += __builtin_bit_cast(half4, s);
+    if (scale != 1.0f) v *= (half_t)scale;
+    return __builtin_bit_cast(uint2, v);
+  } else {
+    f32x2 v0 = bf16x2_unpack(y.x) + bf16x2_unpack(h.x);
+    f32x2 v1 = bf16x2_unpack(y.y) + bf16x2_unpack(h.y);
+    if (acc) {
+      v0 += bf16x2_unpack(s.x);
+      v1 += bf16x2_unpack(s.y);
+    }
+    return uint2{bf16x2_pack(v0 * scale), bf16x2_pack(v1 * scale)};
+  }
+}
+
+// the same, branch-free for the pipelined kernels (a uniform branch would split the basic block
+// their MFMAs and epilogues are interleaved in): s is 0 when the launch does not accumulate (a
+// zero-record descriptor) and scale 1 multiplies exactly, so the values equal epi_row4's (a
+// -0 sum may come out as +0)
+template <typename T>
+__device__ inline uint2 epi_row4_nb(uint2 y, uint2 h, uint2 s, float scale) {
+  if constexpr (__is_same(T, half_t)) {
+    half4 v = __builtin_bit_cast(half4, y) + __builtin_bit_cast(half4, h);
+    v += __builtin_bit_cast(half4, s);
+    v *= (half_t)scale;
+    return __builtin_bit_cast(uint2, v);
+  } else {
+    const f32x2 v0 = bf16x2_unpack(y.x) + bf16x2_unpack(h.x) + bf16x2_unpack(s.x);
+    const f32x2 v1 = bf16x2_unpack(y.y) + bf16x2_unpack(h.y) + bf16x2_unpack(s.y);
+    return uint2{bf16x2_pack(v0 * scale), bf16x2_pack(v1 * scale)};
+  }
+}
+
 template <typename T>
 __device__ inline void pair_st8(T* p, f32x4 a, f32x4 b) {
   *reinterpret_cast<uint4*>(p) = pack8<T>(a, b);

@@ -20,6 +20,7 @@ enum Sw : int {
   SW_PAIR_DIV,     // TTS_PAIR_DIV=1: full-height pair tiles; any other value: short tiles
   SW_ATTN_SPLIT,   // TTS_ATTN_SPLIT=0: the exact encoder's fused attention on f32 MFMA, not split
   SW_ATTN_KSPLIT,  // TTS_ATTN_KSPLIT=1: 16-bit attention with two key groups per block (8 waves)
+  SW_PAIR_SP,      // TTS_PAIR_SP=0: C = 32 pairs on mrf_pair_kernel instead of the pipelined mrf_pair_sp_kernel
   SW_N
 };
 

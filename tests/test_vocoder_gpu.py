@@ -195,6 +195,31 @@ def test_resblock_chain_bit_identical_to_pairs(vw, dtype, switch):
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_pipelined_c32_pairs_bit_identical(vw, dtype, switch):
+    """The software-pipelined C = 32 pair kernel (mrf_pair_sp.hip: weights in registers, tile-
+    outer order, epilogues interleaved with the next tile's MFMAs, conv2's epilogue straight to
+    HBM) reproduces mrf_pair_kernel bit for bit: every stage-3 resblock as pair launches (chains
+    and the fused conv_post off, so k = 3, 7 and 11 and every dilation run through it), ragged
+    and empty utterances, an utterance of one frame (256 rows: one 240-row tile and a 16-row
+    one) and one of 15 frames (3,840 rows = 16 whole tiles)."""
+    eng = engine_for(dtype, vw)
+    rng = np.random.default_rng(25)
+    lens = [71, 1, 0, 15, 33, 64]
+    mel = torch.from_numpy(rng.standard_normal((6, 71, 80)).astype(np.float32)).to(DEV)
+    ln = torch.tensor(lens, dtype=torch.int32)
+    switch("TTS_MRF_FUSED", 1)
+    switch("TTS_MRF_CHAIN", 0)
+    switch("TTS_POST_FUSE", 0)
+    switch("TTS_PAIR_SP", 1)
+    sp = eng.vocoder(mel, ln).cpu().numpy()
+    switch("TTS_PAIR_SP", 0)
+    ref = eng.vocoder(mel, ln).cpu().numpy()
+    for b, L in enumerate(lens):
+        assert np.array_equal(sp[b], ref[b]), (b, float(np.abs(sp[b] - ref[b]).max()))
+        assert np.all(sp[b, L * 256:] == 0)
+
+
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
 def test_fused_conv_post_bit_identical(vw, dtype, switch):
     """conv_post inside the last pair launch (its halo rows computed in the block, the final
     MRF sum never written) reproduces the separate conv_post launch bit for bit: ragged and

@@ -76,9 +76,31 @@ struct AcousticModel::Impl {
   long long split_ws_bytes = 0;
   void run(const ConvLayer& L, const void* x, int x_rows, const int* lens, void* y, int y_rows, int B, int d,
            hipStream_t s, Profiler* pr, float in_slope = 1.f, int act = ACT_NONE, float alpha = 1.f,
-           const void* r1 = nullptr) {
+           const void* r1 = nullptr, const ConvParams* ln = nullptr) {
     run_layer(L, x, x_rows, lens, y, y_rows, B, d, s, pr, in_slope, act, alpha, r1, nullptr, 1.f, 0, 0, cur_rpad,
-              split_ws, split_ws_bytes);
+              split_ws, split_ws_bytes, ln);
+  }
+  // a residual GEMM followed by the block's post-LN: out = LN2?(LN1(y)).  The exact encoder's
+  // split-K projections apply the LayerNorm in their reduce (conv_split.hip); other paths run it
+  // as its own launch inside the same call.
+  void run_ln(const ConvLayer& L, const void* x, int x_rows, const int* lens, void* y, int y_rows, int B, int d,
+              hipStream_t s, float alpha, const void* r1, void* out, const LNParam& a, const LNParam* b2) {
+    // the ConvParams this GEMM launches with (run_layer's), to ask whether its path fuses the LN
+    ConvParams q = conv_params_default();
+    q.x = x; q.sxb = (long long)x_rows * L.Cin; q.sxr = L.Cin; q.x_len = lens; q.x_rows = x_rows;
+    q.w = L.w; q.w_ld = L.taps * L.Cin; q.bias = L.bias; q.wpk = L.wpk;
+    q.y = y; q.syb = (long long)y_rows * L.M; q.syr = L.M; q.r1 = r1; q.srb = q.syb; q.srr = L.M;
+    q.y_len = lens; q.y_rows = y_rows; q.M = L.M; q.Cin = L.Cin; q.taps = L.taps; q.dil = L.dil; q.pad = L.pad;
+    q.alpha = alpha; q.B = B; q.rows_pad = cur_rpad; q.ws = split_ws; q.ws_bytes = split_ws_bytes;
+    if (d == DT_F32 && conv_split_fuses_ln(q)) {
+      ConvParams ln = conv_params_default();
+      ln.ln_out = out; ln.ln_g1 = a.g; ln.ln_b1 = a.b; ln.ln_g2 = b2 ? b2->g : nullptr; ln.ln_b2 = b2 ? b2->b : nullptr;
+      ln.ln_eps = eps;
+      run(L, x, x_rows, lens, y, y_rows, B, d, s, prof, 1.f, ACT_NONE, alpha, r1, &ln);
+      return;
+    }
+    run(L, x, x_rows, lens, y, y_rows, B, d, s, prof, 1.f, ACT_NONE, alpha, r1);
+    ln_rows(d, y, out, B * y_rows, D, a, b2, s);
   }
   Profiler* prof = nullptr;
   int D = 384, H = 2, V = 78, NMEL = 80, FFN = 1536, PRED = 256;
@@ -384,8 +406,7 @@ struct AcousticModel::Impl {
       const int dt = L.dt;
       // macaron FFN: x = LN(x + 0.5 * ffn(x))
       run(L.ffm1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
-      run(L.ffm2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
-      ln_rows(dt, Y, Xb, rows, D, L.ln_mac, nullptr, s);
+      run_ln(L.ffm2, H1, Tp, lens, Y, Tp, B, dt, s, 0.5f, Xb, Xb, L.ln_mac, nullptr);
       // relative-position MHSA: x = LN(x + mhsa(x))
       run(L.qkv, Xb, Tp, lens, QKV, Tp, B, dt, s, prof);
       const bool fused_attn = rel_attn_enabled() && rel_attn_supported(dt, D, H);
@@ -428,8 +449,7 @@ struct AcousticModel::Impl {
     ln_rows(dt, Y, Xb, rows, D, L.ln_conv, nullptr, s);
     // FFN: x = final_LN(LN(x + 0.5 * ffn(x)))
     run(L.ff1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
-    run(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 0.5f, Xb);
-    ln_rows(dt, Y, Xb, rows, D, L.ln_ff, &L.ln_final, s);
+    run_ln(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, 0.5f, Xb, Xb, L.ln_ff, &L.ln_final);
   }
 
   // The three predictors run in sequence on one stream: pitch and energy on two side streams

@@ -27,6 +27,7 @@
 // after the fact (no per-element branches around loads).
 #include "common.h"
 #include "conv_epilogue.h"
+#include "acoustic_kernels.h"
 #include "kernels.h"
 #include "switches.h"
 
@@ -792,10 +793,10 @@ int conv_gemm_kind(int dtype, const ConvParams& p) {
   return (dtype != DT_F32 && xres_mode() && xres_group(p, 32 * 4 * (4 / xres_wm(p)))) ? PK_CONV_XRES : PK_CONV_GEMM;
 }
 
-hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s) {
+static hipError_t conv_gemm_launch_noln(int dtype, const ConvParams& p, hipStream_t s, bool* ln_done) {
   switch (dtype) {
     case DT_F32:
-      if (conv_split_eligible(p)) return conv_split_launch(p, s);
+      if (conv_split_eligible(p)) return conv_split_launch(p, s, ln_done);
       return launch_t<float>(p, s);
     case DT_F16: {
       hipError_t e;
@@ -809,6 +810,15 @@ hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s) {
     }
   }
   return hipErrorInvalidValue;
+}
+
+hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s) {
+  bool ln_done = false;
+  const hipError_t e = conv_gemm_launch_noln(dtype, p, s, &ln_done);
+  if (e != hipSuccess || !p.ln_out || ln_done) return e;
+  // LayerNorm as its own launch over the whole [B][y_rows] output (contiguous rows of M)
+  if (p.syr != p.M || p.syb != (long long)p.y_rows * p.syr || p.nh != 1) return hipErrorInvalidValue;
+  return launch_layernorm(dtype, p.y, p.ln_out, p.B * p.y_rows, p.M, p.ln_g1, p.ln_b1, p.ln_g2, p.ln_b2, p.ln_eps, s);
 }
 
 }  // namespace tts

@@ -518,6 +518,76 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(ConvParams p, int S) 
   }
 }
 
+// The same reduce with the post-LN of a residual block fused (ConvParams::ln_out): one wave per
+// row of M <= 512 channels, lane l owning channels l + 64 i.  Each element is summed over the
+// slices in slice order with the epilogue applied as split_reduce does, then the row is
+// normalised exactly as layernorm_kernel<float, 8> does it (two-pass fp32, the same lane layout
+// and wave reduction, the optional second LayerNorm on the first's output), so ln_out equals
+// split_reduce + launch_layernorm bit for bit on every valid row; y is not written and rows past
+// an utterance are left alone (the separate LayerNorm also normalised their stale contents,
+// which no consumer reads: every kernel masks rows >= len on load).
+__global__ __launch_bounds__(256) void split_reduce_ln_kernel(ConvParams p, int S) {
+  constexpr int PER = 8;
+  const int F = p.B * p.x_rows;
+  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (f >= F) return;
+  const int b = f / p.x_rows;
+  const int r = f - b * p.x_rows;
+  const int ylen = p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows;
+  if (r >= ylen) return;
+  const int C = p.M;
+  const long long ro = (long long)b * p.srb + (long long)r * p.srr;
+  float v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    float x = 0.f;
+    if (c < C) {
+      x = p.ws[(long long)f * C + c];
+      for (int sl = 1; sl < S; ++sl) x += p.ws[((long long)sl * F + f) * C + c];
+      if (p.bias) x += p.bias[c];
+      if (p.alpha != 1.0f) x *= p.alpha;
+      if (p.r1) x += reinterpret_cast<const float*>(p.r1)[ro + c];
+      if (p.r2) x += reinterpret_cast<const float*>(p.r2)[ro + c];
+      if (p.out_scale != 1.0f) x *= p.out_scale;
+    }
+    v[i] = x;
+  }
+  const float invC = 1.f / (float)C;
+  for (int pass = 0; pass < (p.ln_g2 ? 2 : 1); ++pass) {
+    const float* g = pass ? p.ln_g2 : p.ln_g1;
+    const float* bb = pass ? p.ln_b2 : p.ln_b1;
+    float sm = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) sm += v[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+    const float mu = sm * invC;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      const float dd = c < C ? v[i] - mu : 0.f;
+      q += dd * dd;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float rstd = rsqrtf(q * invC + p.ln_eps);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      if (c < C) v[i] = (v[i] - mu) * rstd * g[c] + bb[c];
+    }
+  }
+  float* o = reinterpret_cast<float*>(p.ln_out) + (long long)b * p.syb + (long long)r * p.syr;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    if (c < C) o[c] = v[i];
+  }
+}
+
 constexpr int SPLIT_LDS_MAX = 76 * 1024;  // two blocks per CU
 
 // channel group: largest power of two dividing Cin with both planes of UW utterances' rows within
@@ -593,7 +663,14 @@ long long conv_split_ws_bytes(int taps, int Cin, int M, int rows) {
   return cg ? (long long)split_slices(q, cg) * rows * M * 4 : 0;
 }
 
-hipError_t conv_split_launch(const ConvParams& p, hipStream_t s) {
+bool conv_split_fuses_ln(const ConvParams& p) {
+  if (!conv_split_eligible(p) || !packed_ok(p) || p.M > 512 || p.act_out != ACT_NONE) return false;
+  const int cg = packed_group(p);
+  return cg && split_slices(p, cg) > 1;
+}
+
+hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done) {
+  if (ln_done) *ln_done = false;
   if (packed_ok(p)) {
     const int cg = packed_group(p);
     if (cg) {
@@ -604,7 +681,10 @@ hipError_t conv_split_launch(const ConvParams& p, hipStream_t s) {
       const size_t lds = std::max((size_t)2 * (32 * SPK_NT + (p.taps - 1) * p.dil) * (cg * 2 + 16),
                                   (size_t)32 * SPK_NT * (128 * 4 + 16));  // X planes / epilogue tile
       hipLaunchKernelGGL(conv_splitp_kernel, dim3(nwg), dim3(256), lds, s, p, cg, S, gps);
-      if (S > 1) {
+      if (S > 1 && p.ln_out && p.M <= 512 && p.act_out == ACT_NONE) {
+        hipLaunchKernelGGL(split_reduce_ln_kernel, dim3((F + 3) / 4), dim3(256), 0, s, p, S);
+        if (ln_done) *ln_done = true;
+      } else if (S > 1) {
         const long long n = (long long)F * (p.M / 4);
         const unsigned g = (unsigned)std::min<long long>((n + 255) / 256, 4096);
         hipLaunchKernelGGL(split_reduce_kernel, dim3(g), dim3(256), 0, s, p, S);

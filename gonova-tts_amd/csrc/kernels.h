@@ -34,6 +34,13 @@ struct ConvParams {
   int rows_pad;
   float* ws;
   long long ws_bytes;
+  // optional LayerNorm of the result (post-LN residual blocks, HF:551-645): ln_out[row] =
+  // LN2?(LN1(y[row])) with y's strides.  The split-K fp32 path applies it in its reduce
+  // (split_reduce_ln_kernel: y is never written); every other path writes y and then runs
+  // launch_layernorm(y -> ln_out) over the B * y_rows rows.
+  void* ln_out;
+  const float *ln_g1, *ln_b1, *ln_g2, *ln_b2;
+  float ln_eps;
 };
 
 inline ConvParams conv_params_default() {
@@ -56,7 +63,10 @@ int conv_gemm_kind(int dtype, const ConvParams& p);
 // fp32 conv as three f16 MFMAs (conv_split.hip): an fp32 layer whose ConvParams::wpk is a
 // split-packed copy (frag_pack_split) runs here when eligible (Cin % 64 == 0, no head batching)
 bool conv_split_eligible(const ConvParams& p);
-hipError_t conv_split_launch(const ConvParams& p, hipStream_t s);
+// whether conv_split_launch applies p.ln_out's LayerNorm in its split-K reduce (dtype f32)
+bool conv_split_fuses_ln(const ConvParams& p);
+// *ln_done: whether the launch applied p.ln_out's LayerNorm itself (the split-K reduce)
+hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done = nullptr);
 // split-K workspace bytes a packed-row launch of this shape over `rows` flat rows can use (0: none)
 long long conv_split_ws_bytes(int taps, int Cin, int M, int rows);
 

@@ -265,7 +265,8 @@ inline void launch_conv_checked(const ConvParams& p, int dt, hipStream_t s, Prof
 inline void run_layer(const ConvLayer& L, const void* x, int x_rows, const int* lens, void* y, int y_rows, int B,
                       int dt, hipStream_t s, Profiler* prof, float in_slope = 1.f, int act = ACT_NONE,
                       float alpha = 1.f, const void* r1 = nullptr, const void* r2 = nullptr, float out_scale = 1.f,
-                      int x_ld = 0, int y_ld = 0, int rows_pad = 0, float* ws = nullptr, long long ws_bytes = 0) {
+                      int x_ld = 0, int y_ld = 0, int rows_pad = 0, float* ws = nullptr, long long ws_bytes = 0,
+                      const ConvParams* ln = nullptr) {
   ConvParams p = conv_params_default();
   const int xl = x_ld ? x_ld : L.Cin, yl = y_ld ? y_ld : L.M;
   p.x = x; p.sxb = (long long)x_rows * xl; p.sxr = xl; p.x_len = lens; p.x_rows = x_rows;
@@ -277,6 +278,10 @@ inline void run_layer(const ConvLayer& L, const void* x, int x_rows, const int* 
   p.in_slope = in_slope; p.act_out = act; p.alpha = alpha; p.out_scale = out_scale;
   p.B = B;
   p.rows_pad = rows_pad; p.ws = ws; p.ws_bytes = ws_bytes;
+  if (ln) {  // the LayerNorm fields of *ln (ln_out, gains, biases, eps)
+    p.ln_out = ln->ln_out; p.ln_g1 = ln->ln_g1; p.ln_b1 = ln->ln_b1; p.ln_g2 = ln->ln_g2; p.ln_b2 = ln->ln_b2;
+    p.ln_eps = ln->ln_eps;
+  }
   launch_conv_checked(p, dt, s, prof, 2.0 * L.M * (double)L.Cin * L.taps * (double)B * y_rows);
 }
 

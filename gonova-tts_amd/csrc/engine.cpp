@@ -55,6 +55,9 @@ struct VocoderWeights {
   int hop = 256;
 };
 
+#ifndef TTS_PAIR_SP_DEFAULT
+#define TTS_PAIR_SP_DEFAULT 0  // 1: C = 32 pairs on the software-pipelined kernel (measured slower)
+#endif
 // TTS_MRF_FUSED=0 selects the unfused per-conv path (A/B and parity tests)
 static bool mrf_fused_enabled() { return sw(SW_MRF_FUSED) != 0; }
 // resblock chain kernel for the HBM-bound resblocks (default on; TTS_MRF_CHAIN=0: pairs only)
@@ -465,7 +468,8 @@ struct tts_engine {
             }
             const double fl = 2.0 * 2.0 * ch * (double)ch * pp.k * (double)B * Tout;
             // C = 32 pairs without conv_post: the software-pipelined kernel (bit-identical)
-            const bool sp = !pp.post_wpk && sw(SW_PAIR_SP) != 0 && mrf_pair_sp_supported(dt, ch, pp.k);
+            const int spsw = sw(SW_PAIR_SP);
+            const bool sp = !pp.post_wpk && (spsw < 0 ? TTS_PAIR_SP_DEFAULT : spsw) != 0 && mrf_pair_sp_supported(dt, ch, pp.k);
             auto launch = [&] { return sp ? mrf_pair_sp_launch(dt, ch, pp, s) : mrf_pair_launch(dt, ch, pp, s); };
             if (prof.on) {
               Profiler::Rec r{prof.get(), prof.get(), fl, PK_MRF_PAIR};

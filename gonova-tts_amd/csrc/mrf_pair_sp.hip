@@ -42,6 +42,9 @@ namespace tts {
 #ifndef TTS_SP_BN11
 #define TTS_SP_BN11 240
 #endif
+#ifndef TTS_SP_SCHED
+#define TTS_SP_SCHED 1  // 0: leave the MFMA / epilogue interleave to the compiler's scheduler
+#endif
 #ifndef TTS_SP_OCC
 #define TTS_SP_OCC 3
 #endif
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(256, TTS_SP_OCC) void mrf_pair_sp_kernel(MrfPairPar
         if (gn < NU * S) ring[g % PF] = *reinterpret_cast<const Frag*>(ad[gn % S] + (gn / S) * 64 * RS);
       }
       if (u > 0) epi(acc[(u - 1) & 1], u - 1);
-      if (u > 0) {  // interleave: MFMA, V x VALU, ... ; a DS read after every MT MFMAs
+      if (TTS_SP_SCHED && u > 0) {  // interleave: MFMA, V x VALU, ... ; a DS read after every MT MFMAs
 #pragma unroll
         for (int s = 0; s < S; ++s) {
 #pragma unroll
@@ -235,12 +238,17 @@ __global__ __launch_bounds__(256, TTS_SP_OCC) void mrf_pair_sp_kernel(MrfPairPar
     int ro[MT];  // byte offset of this lane's 4 channels in its row of tile u = 0
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) ro[mt] = ((n0 + 16 * wn + l15) * C + ch0 + 16 * mt) * (int)sizeof(T);
-    uint2 hv[2][MT], sv[2][MT];
+    // residual rows of tile u in slot u % 3: tile u + 1's loads are issued while tile u - 1's
+    // epilogue still reads its slot
+    uint2 hv[3][MT], sv[3][MT];
     auto load_res = [&](int u) __attribute__((always_inline)) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        hv[u & 1][mt] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, ro[mt], u * 64 * RS, 0));
-        sv[u & 1][mt] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(sr, ro[mt], u * 64 * RS, 0));
+        // the tile offset goes into the VGPR offset: the descriptor's range check does not
+        // include soffset
+        const int off = ro[mt] + u * 64 * RS;
+        hv[u % 3][mt] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
+        sv[u % 3][mt] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(sr, off, 0, 0));
       }
     };
     const float scale = p.scale;
@@ -248,8 +256,8 @@ __global__ __launch_bounds__(256, TTS_SP_OCC) void mrf_pair_sp_kernel(MrfPairPar
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const uint2 y = epi_conv2<T>(acc[mt], bias2[mt]);
-        const uint2 o = epi_row4_nb<T>(y, hv[u & 1][mt], sv[u & 1][mt], scale);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), yr, ro[mt], u * 64 * RS, TTS_ROW_STORE);
+        const uint2 o = epi_row4_nb<T>(y, hv[u % 3][mt], sv[u % 3][mt], scale);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), yr, ro[mt] + u * 64 * RS, 0, TTS_ROW_STORE);
       }
     };
     constexpr int NU = (NT2 + WN - 1) / WN;

@@ -10,14 +10,14 @@ for L in "$@"; do case $L in /*) LIBS="$LIBS $L";; *) LIBS="$LIBS $R/$L";; esac;
 for rep in 1 2; do
   for L in $LIBS; do
     n=$(basename $L .so)
-    TTS_LIB=$L timeout -k 10 200 python3 $R/bench.py --no-full --no-c4 --no-streaming --no-cpu-baseline > $O/$n.$rep.json 2> $O/$n.$rep.err || { tail -5 $O/$n.$rep.err; exit 1; }
+    TTS_LIB=$L timeout -k 10 200 python3 $R/bench.py --no-full --no-c4 --no-streaming --no-cpu-baseline --no-c1 > $O/$n.$rep.json 2> $O/$n.$rep.err || { tail -5 $O/$n.$rep.err; exit 1; }
     python3 -c "import json; d=json.load(open('$O/$n.$rep.json')); k=d['roofline']['kernels']; print('$n', $rep, d['ms_per_step'], {a: b['ms_per_step'] for a, b in k.items()})"
   done
 done
 cd /tmp && export TMPDIR=/tmp
 for L in $LIBS; do
   n=$(basename $L .so)
-  TTS_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof_$n -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-full --no-c4 --no-streaming --no-cpu-baseline > $O/prof_$n.log 2>&1 || exit 1
+  TTS_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof_$n -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-full --no-c4 --no-streaming --no-cpu-baseline --no-c1 > $O/prof_$n.log 2>&1 || exit 1
   python3 $R/tools/step_breakdown.py $O/prof_$n/run_kernel_trace.csv > $O/bd_$n.txt || exit 1
 done
 echo ab done

@@ -189,6 +189,11 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) ring[i][mt] = *reinterpret_cast<const Frag*>(wp + ((long long)mt * S + i) * 1024);
   };
+  // the running conv's bias: the accumulators start at it (TTS_BIAS_ACC); each is loaded
+  // before the weight preload of its conv (in-order vmcnt)
+  f32x4 bias[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b1[0] + ch0 + 16 * mt);
   preload(p.w1[0]);
 
   // ---- stage h (Hs) and g = lrelu(h) (GT), zero outside the utterance ----
@@ -238,16 +243,17 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
 #pragma unroll
       for (int u = 0; u < NU1; ++u)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = f32x4{};
+        for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = acc_init(bias[mt]);
       int tile[NU1];
 #pragma unroll
       for (int u = 0; u < NU1; ++u) tile[u] = 16 * min(wn + WN * u, NT1 - 1) * RS;
       const int rb = LO1 - A * DQ + l15;
       pair_conv<T, C, S, NU1, D>(acc1, ring, w1, GT + rb * RS, DQ * RS, DQ, tile, rb, lq);
       __builtin_amdgcn_sched_barrier(0);
-      f32x4 bias[MT];  // bias before the weight preload: in-order vmcnt
+      const f32x4 b1v[MT] = {bias[0], bias[1]};  // conv1's bias for its epilogue (no-op with TTS_BIAS_ACC)
+      // conv2's bias before the weight preload: in-order vmcnt
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b1[Q] + ch0 + 16 * mt);
+      for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2[Q] + ch0 + 16 * mt);
       preload(p.w2[Q]);  // conv2's first steps in flight during the epilogue
       __builtin_amdgcn_sched_barrier(0);
       __syncthreads();  // T overwrites G
@@ -259,7 +265,7 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
           const bool valid = gr >= 0 && gr < len;
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
-            uint2 pk = epi_conv1<T>(acc1[u][mt], bias[mt], slope);
+            uint2 pk = epi_conv1<T>(acc1[u][mt], b1v[mt], slope);
             if (!valid) pk = uint2{0u, 0u};
             *reinterpret_cast<uint2*>(GT + lds4(tr, mt)) = pk;
           }
@@ -272,17 +278,18 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
 #pragma unroll
       for (int u = 0; u < NU2; ++u)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = f32x4{};
+        for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = acc_init(bias[mt]);
       int tile[NU2];
 #pragma unroll
       for (int u = 0; u < NU2; ++u) tile[u] = 16 * min(wn + WN * u, NT2 - 1) * RS;
       const int rb = LO2 - A + l15;
       pair_conv<T, C, S, NU2, D>(acc2, ring, w2, GT + rb * RS, RS, 1, tile, rb, lq);
       __builtin_amdgcn_sched_barrier(0);
-      f32x4 bias[MT];  // bias before the weight / MRF-sum prefetch: in-order vmcnt
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2[Q] + ch0 + 16 * mt);
+      const f32x4 b2v[MT] = {bias[0], bias[1]};  // conv2's bias for its epilogue (no-op with TTS_BIAS_ACC)
       if constexpr (Q < 2) {
+        // the next pair's conv1 bias before its weight preload: in-order vmcnt
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b1[Q + 1] + ch0 + 16 * mt);
         preload(p.w1[Q + 1]);
       } else {  // MRF-sum rows in flight during the last epilogue (no records: not accumulating)
         const auto yrsrc = __builtin_amdgcn_make_buffer_rsrc(Y, 0, p.accum ? len * C * (int)sizeof(T) : 0, 0x00020000);
@@ -302,7 +309,7 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             const int o = lds4(tr, mt);
-            const uint2 y = epi_conv2<T>(acc2[u][mt], bias[mt]);
+            const uint2 y = epi_conv2<T>(acc2[u][mt], b2v[mt]);
             if constexpr (Q < 2) {
               const int gr = r0g + tr;
               const bool valid = gr >= 0 && gr < len;

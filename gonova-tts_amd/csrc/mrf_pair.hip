@@ -130,6 +130,10 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   // weights: [C/16][k][KS][64][8] -> step s of m-tile mb at (mb*S + s) KiB
   const char* w1 = reinterpret_cast<const char*>(p.w1) + (long long)(MT * wm) * S * 1024 + lane * 16;
   const char* w2 = reinterpret_cast<const char*>(p.w2) + (long long)(MT * wm) * S * 1024 + lane * 16;
+  // conv1's bias first (the accumulators start at it; in-order vmcnt), then its first weight steps
+  f32x4 bias1[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) bias1[mt] = *reinterpret_cast<const f32x4*>(p.b1 + ch0 + 16 * mt);
   Frag ring[D][MT];
 #pragma unroll
   for (int i = 0; i < D; ++i)
@@ -183,7 +187,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
 #pragma unroll
   for (int u = 0; u < NU1; ++u)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = f32x4{};
+    for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = acc_init(bias1[mt]);
   {
     int tile[NU1];
 #pragma unroll
@@ -191,11 +195,11 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
     pair_conv<T, C, S, NU1, D, MT, (C >= TTS_PAIR_MTO_MIN)>(acc1, ring, w1, Gs + l15 * RS, d * RS, d, tile, l15, lq);
   }
   __builtin_amdgcn_sched_barrier(0);
-  // bias first, then conv2's first weight steps (in flight during the conv1 epilogue): vmcnt
+  // conv2's bias first, then its first weight steps (in flight during the conv1 epilogue): vmcnt
   // retires in order, so waiting for the bias does not wait for the weights
-  f32x4 bias1[MT];
+  f32x4 bias2[MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) bias1[mt] = *reinterpret_cast<const f32x4*>(p.b1 + ch0 + 16 * mt);
+  for (int mt = 0; mt < MT; ++mt) bias2[mt] = *reinterpret_cast<const f32x4*>(p.b2 + ch0 + 16 * mt);
 #pragma unroll
   for (int i = 0; i < D; ++i)
     if (i < S)
@@ -230,7 +234,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
 #pragma unroll
   for (int u = 0; u < NU2; ++u)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = f32x4{};
+    for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = acc_init(bias2[mt]);
   {
     int tile[NU2];
 #pragma unroll
@@ -255,9 +259,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
     }
   };
   // with conv_post fused the residual rows wait until the accumulators are staged (registers)
-  f32x4 bias[MT];  // before the row loads (in-order vmcnt: the staging waits for the bias only)
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b2 + ch0 + 16 * mt);
+  const f32x4 (&bias)[MT] = bias2;
   load_rows(!POST, true);
   __builtin_amdgcn_sched_barrier(0);
   __syncthreads();  // T no longer read

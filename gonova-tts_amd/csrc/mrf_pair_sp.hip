@@ -156,7 +156,8 @@ __global__ __launch_bounds__(256, TTS_SP_OCC) void mrf_pair_sp_kernel(MrfPairPar
   // matrix instructions execute.  pre(u) issues tile u's global loads (conv2: residual rows)
   // one tile ahead of its epilogue.
   constexpr int PF = S < 4 ? S : S >= 11 ? 3 : 4;  // k = 11: 88 weight VGPRs leave room for 3
-  auto conv_pipe = [&](auto NUC, auto VC, auto&& epi, auto&& pre, auto&& before_last) __attribute__((always_inline)) {
+  auto conv_pipe = [&](auto NUC, auto VC, const f32x4 (&binit)[MT], auto&& epi, auto&& pre, auto&& before_last)
+                       __attribute__((always_inline)) {
     constexpr int NU = decltype(NUC)::value, V = decltype(VC)::value;
     Frag ring[PF];
 #pragma unroll
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(256, TTS_SP_OCC) void mrf_pair_sp_kernel(MrfPairPar
       if (u + 1 < NU) pre(u + 1);
       f32x4 (&a)[MT] = acc[u & 1];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) a[mt] = f32x4{};
+      for (int mt = 0; mt < MT; ++mt) a[mt] = acc_init(binit[mt]);
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const int g = u * S + s;
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(256, TTS_SP_OCC) void mrf_pair_sp_kernel(MrfPairPar
       }
     };
     // conv2's weights in flight during the last epilogue and the barrier
-    conv_pipe(std::integral_constant<int, NT1 / WN>{}, std::integral_constant<int, VPM>{}, epi1, [](int) {},
+    conv_pipe(std::integral_constant<int, NT1 / WN>{}, std::integral_constant<int, VPM>{}, bias1, epi1, [](int) {},
               [&] { load_w(p.w2); });
   }
   f32x4 bias2[MT];
@@ -261,7 +262,7 @@ __global__ __launch_bounds__(256, TTS_SP_OCC) void mrf_pair_sp_kernel(MrfPairPar
       }
     };
     constexpr int NU = (NT2 + WN - 1) / WN;
-    conv_pipe(std::integral_constant<int, NU>{}, std::integral_constant<int, VPM>{}, epi2, load_res, [] {});
+    conv_pipe(std::integral_constant<int, NU>{}, std::integral_constant<int, VPM>{}, bias2, epi2, load_res, [] {});
   }
 }
 

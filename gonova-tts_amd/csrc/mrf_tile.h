@@ -129,6 +129,23 @@ __device__ inline void pair_ld8(const T* p, f32x4& a, f32x4& b) {
   a = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
   b = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
 }
+// Bias in the accumulator (TTS_BIAS_ACC, default): every conv's accumulators start at its bias
+// (the first MFMA reads the bias registers as its C operand), so the epilogues add nothing --
+// 2 packed f16 adds (f16) or 4 f32 adds (bf16) fewer per accumulator quad, and for f16 one
+// rounding of acc + bias instead of f16(acc) + f16(bias).  Pair, chain and pipelined kernels all
+// use it, so they stay bit-identical to each other.
+#ifndef TTS_BIAS_ACC
+#define TTS_BIAS_ACC 1
+#endif
+__device__ inline f32x4 acc_init(f32x4 bias) {
+#if TTS_BIAS_ACC
+  return bias;
+#else
+  (void)bias;
+  return f32x4{};
+#endif
+}
+
 // Epilogue arithmetic.  f16: packed half math after one cvt_pk per pair of accumulators
 // (v_pk_add/mul/max_f16: a fraction of the f32 instruction count; a sum of two f16 values
 // is correctly rounded either way, the bias/slope products differ by <= 1 ulp).  bf16:
@@ -136,11 +153,22 @@ __device__ inline void pair_ld8(const T* p, f32x4& a, f32x4& b) {
 template <typename T>
 __device__ inline uint2 epi_conv1(f32x4 acc, f32x4 bias, float slope) {  // lrelu(acc + b) -> 4 x T
   if constexpr (__is_same(T, half_t)) {
+#if TTS_BIAS_ACC
+    (void)bias;
+    half4 h = __builtin_convertvector(acc, half4);
+#else
     half4 h = __builtin_convertvector(acc, half4) + __builtin_convertvector(bias, half4);
-    h = __builtin_elementwise_max(h, h * (half_t)slope);
-    return *reinterpret_cast<const uint2*>(&h);
+#endif
+    const half4 m = h * (half_t)slope;
+    const uint2 hu = __builtin_bit_cast(uint2, h), mu = __builtin_bit_cast(uint2, m);
+    return uint2{pk_max_f16(hu.x, mu.x), pk_max_f16(hu.y, mu.y)};
   } else {
+#if TTS_BIAS_ACC
+    (void)bias;
+    f32x4 v = acc;
+#else
     f32x4 v = acc + bias;
+#endif
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaxf(v[e], v[e] * slope);  // 0 <= slope <= 1
     return pack4<T>(v);
@@ -148,12 +176,17 @@ __device__ inline uint2 epi_conv1(f32x4 acc, f32x4 bias, float slope) {  // lrel
 }
 template <typename T>
 __device__ inline uint2 epi_conv2(f32x4 acc, f32x4 bias) {  // acc + b -> 4 x T
+#if TTS_BIAS_ACC
+  (void)bias;
+  return pack4<T>(acc);
+#else
   if constexpr (__is_same(T, half_t)) {
     half4 h = __builtin_convertvector(acc, half4) + __builtin_convertvector(bias, half4);
     return *reinterpret_cast<const uint2*>(&h);
   } else {
     return pack4<T>(acc + bias);
   }
+#endif
 }
 // row pass: (y + h (+ s)) * scale on 8 elements
 template <typename T>

@@ -175,10 +175,7 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
   const float slope = p.slope;
   const int ch0 = 32 * wm + 4 * lq;    // + 16*mt: this lane's 4 output channels
   const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
-  auto lds4 = [&](int r, int mt) {     // byte offset of this lane's 4 channels (ch0 + 16 mt) in row r
-    const int cb = (ch0 + 16 * mt) * 2;
-    return r * RS + (((cb >> 4) ^ swz(r)) << 4) + (cb & 15);
-  };
+  constexpr int TU = 16 * WN * RS;     // bytes from a wave's tile u to its tile u + 1
 
   Frag ring[D][MT];
   auto preload = [&](const void* w) __attribute__((always_inline)) {
@@ -244,11 +241,9 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
       for (int u = 0; u < NU1; ++u)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = acc_init(bias[mt]);
-      int tile[NU1];
-#pragma unroll
-      for (int u = 0; u < NU1; ++u) tile[u] = 16 * min(wn + WN * u, NT1 - 1) * RS;
       const int rb = LO1 - A * DQ + l15;
-      pair_conv<T, C, S, NU1, D>(acc1, ring, w1, GT + rb * RS, DQ * RS, DQ, tile, rb, lq);
+      pair_conv<T, C, S, NU1, D, MT, false, TU>(acc1, ring, w1, GT + (rb + 16 * wn) * RS, DQ * RS, DQ, rb, lq,
+                                                16 * (min(wn + WN * (NU1 - 1), NT1 - 1) - wn) * RS);
       __builtin_amdgcn_sched_barrier(0);
       const f32x4 b1v[MT] = {bias[0], bias[1]};  // conv1's bias for its epilogue (no-op with TTS_BIAS_ACC)
       // conv2's bias before the weight preload: in-order vmcnt
@@ -257,19 +252,23 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
       preload(p.w2[Q]);  // conv2's first steps in flight during the epilogue
       __builtin_amdgcn_sched_barrier(0);
       __syncthreads();  // T overwrites G
+      {
+        int eo[MT];  // the lane's bytes in the wave's tile 0 (tile u: + u * TU)
 #pragma unroll
-      for (int u = 0; u < NU1; ++u)
-        if (NT1 % WN == 0 || wn + WN * u < NT1) {
-          const int tr = LO1 + 16 * (wn + WN * u) + l15;
-          const int gr = r0g + tr;
-          const bool valid = gr >= 0 && gr < len;
+        for (int mt = 0; mt < MT; ++mt) eo[mt] = pair_lds4<C>(LO1 + 16 * wn + l15, ch0 + 16 * mt);
+        const int gr0 = r0g + LO1 + 16 * wn + l15;
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            uint2 pk = epi_conv1<T>(acc1[u][mt], b1v[mt], slope);
-            if (!valid) pk = uint2{0u, 0u};
-            *reinterpret_cast<uint2*>(GT + lds4(tr, mt)) = pk;
+        for (int u = 0; u < NU1; ++u)
+          if (NT1 % WN == 0 || wn + WN * u < NT1) {
+            const bool valid = (unsigned)(gr0 + 16 * WN * u) < (unsigned)len;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+              uint2 pk = epi_conv1<T>(acc1[u][mt], b1v[mt], slope);
+              if (!valid) pk = uint2{0u, 0u};
+              *reinterpret_cast<uint2*>(GT + eo[mt] + u * TU) = pk;
+            }
           }
-        }
+      }
       __syncthreads();
     }
     // conv2: output rows [LO2, LO2 + 16 NT2) read T rows (row - A) + tap
@@ -279,11 +278,9 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
       for (int u = 0; u < NU2; ++u)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = acc_init(bias[mt]);
-      int tile[NU2];
-#pragma unroll
-      for (int u = 0; u < NU2; ++u) tile[u] = 16 * min(wn + WN * u, NT2 - 1) * RS;
       const int rb = LO2 - A + l15;
-      pair_conv<T, C, S, NU2, D>(acc2, ring, w2, GT + rb * RS, RS, 1, tile, rb, lq);
+      pair_conv<T, C, S, NU2, D, MT, false, TU>(acc2, ring, w2, GT + (rb + 16 * wn) * RS, RS, 1, rb, lq,
+                                                16 * (min(wn + WN * (NU2 - 1), NT2 - 1) - wn) * RS);
       __builtin_amdgcn_sched_barrier(0);
       const f32x4 b2v[MT] = {bias[0], bias[1]};  // conv2's bias for its epilogue (no-op with TTS_BIAS_ACC)
       if constexpr (Q < 2) {
@@ -302,25 +299,29 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
       }
       __builtin_amdgcn_sched_barrier(0);
       __syncthreads();  // T no longer read
+      {
+        int eo[MT];  // the lane's bytes in the wave's tile 0 (tile u: + u * TU)
 #pragma unroll
-      for (int u = 0; u < NU2; ++u)
-        if (NT2 % WN == 0 || wn + WN * u < NT2) {
-          const int tr = LO2 + 16 * (wn + WN * u) + l15;
+        for (int mt = 0; mt < MT; ++mt) eo[mt] = pair_lds4<C>(LO2 + 16 * wn + l15, ch0 + 16 * mt);
+        const int gr0 = r0g + LO2 + 16 * wn + l15;
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const int o = lds4(tr, mt);
-            const uint2 y = epi_conv2<T>(acc2[u][mt], b2v[mt]);
-            if constexpr (Q < 2) {
-              const int gr = r0g + tr;
-              const bool valid = gr >= 0 && gr < len;
-              const uint2 h = epi_add4<T>(y, *reinterpret_cast<const uint2*>(Hs + o));
-              *reinterpret_cast<uint2*>(Hs + o) = h;
-              *reinterpret_cast<uint2*>(GT + o) = valid ? lrelu4<T>(h, slope) : uint2{0u, 0u};
-            } else {
-              *reinterpret_cast<uint2*>(GT + o) = y;  // row pass: epi_row(y, h, S)
+        for (int u = 0; u < NU2; ++u)
+          if (NT2 % WN == 0 || wn + WN * u < NT2) {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+              const int o = eo[mt] + u * TU;
+              const uint2 y = epi_conv2<T>(acc2[u][mt], b2v[mt]);
+              if constexpr (Q < 2) {
+                const bool valid = (unsigned)(gr0 + 16 * WN * u) < (unsigned)len;
+                const uint2 h = epi_add4<T>(y, *reinterpret_cast<const uint2*>(Hs + o));
+                *reinterpret_cast<uint2*>(Hs + o) = h;
+                *reinterpret_cast<uint2*>(GT + o) = valid ? lrelu4<T>(h, slope) : uint2{0u, 0u};
+              } else {
+                *reinterpret_cast<uint2*>(GT + o) = y;  // row pass: epi_row(y, h, S)
+              }
             }
           }
-        }
+      }
       __syncthreads();
     }
   };

@@ -69,6 +69,7 @@ static size_t pair_lds_bytes(int k, int d, bool post) {
   const int a1 = (k - 1) / 2 * d, a2 = (k - 1) / 2;
   const int bo = G::BN + (post ? 2 * PAIR_PO : 0);
   const int nt1 = (bo + 2 * a2 + 15) / 16;
+
   const size_t g = (size_t)(16 * nt1 + 2 * a1) * G::RS;
   const size_t t = (size_t)16 * nt1 * G::RS;
   return std::max(std::max(g, t), (size_t)bo * (C * 2 + 16));
@@ -188,12 +189,10 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   for (int u = 0; u < NU1; ++u)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = acc_init(bias1[mt]);
-  {
-    int tile[NU1];
-#pragma unroll
-    for (int u = 0; u < NU1; ++u) tile[u] = 16 * min(wn + WN * u, NT1 - 1) * RS;
-    pair_conv<T, C, S, NU1, D, MT, (C >= TTS_PAIR_MTO_MIN)>(acc1, ring, w1, Gs + l15 * RS, d * RS, d, tile, l15, lq);
-  }
+  // (a wave whose share is one short repeats the block's last tile: its offset from tile 0)
+  auto last_off = [&](int nt, int nu) { return 16 * (min(wn + WN * (nu - 1), nt - 1) - wn) * RS; };
+  pair_conv<T, C, S, NU1, D, MT, (C >= TTS_PAIR_MTO_MIN), 16 * WN * RS>(acc1, ring, w1, Gs + (16 * wn + l15) * RS, d * RS,
+                                                                        d, l15, lq, last_off(NT1, NU1));
   __builtin_amdgcn_sched_barrier(0);
   // conv2's bias first, then its first weight steps (in flight during the conv1 epilogue): vmcnt
   // retires in order, so waiting for the bias does not wait for the weights
@@ -209,18 +208,19 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   __syncthreads();  // T overwrites G: every wave is done reading it
   {
     const f32x4 (&bias)[MT] = bias1;
+    int eo[MT];  // this lane's T bytes in the wave's tile 0 (tile u: + u * 16 WN rows)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) eo[mt] = pair_lds4<C>(16 * wn + l15, ch0 + 16 * mt);
+    const int gr0 = n0 - PO - A2 + 16 * wn + l15;  // utterance row of the lane's row in tile 0
 #pragma unroll
     for (int u = 0; u < NU1; ++u)
       if (NT1 % WN == 0 || wn + WN * u < NT1) {
-        const int tr = 16 * (wn + WN * u) + l15;
-        const int gr = n0 - PO - A2 + tr;
-        const bool valid = gr >= 0 && gr < len;
+        const bool valid = (unsigned)(gr0 + 16 * WN * u) < (unsigned)len;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           uint2 pk = epi_conv1<T>(acc1[u][mt], bias[mt], slope);
           if (!valid) pk = uint2{0u, 0u};
-          const int cb = (ch0 + 16 * mt) * 2;  // byte offset in the row
-          *reinterpret_cast<uint2*>(Ts + tr * RS + (((cb >> 4) ^ swz(tr)) << 4) + (cb & 15)) = pk;
+          *reinterpret_cast<uint2*>(Ts + eo[mt] + u * 16 * WN * RS) = pk;
         }
       }
   }
@@ -235,12 +235,8 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   for (int u = 0; u < NU2; ++u)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = acc_init(bias2[mt]);
-  {
-    int tile[NU2];
-#pragma unroll
-    for (int u = 0; u < NU2; ++u) tile[u] = 16 * min(wn + WN * u, NT2 - 1) * RS;
-    pair_conv<T, C, S, NU2, D, MT, (C >= TTS_PAIR_MTO_MIN)>(acc2, ring, w2, Ts + l15 * RS, RS, 1, tile, l15, lq);
-  }
+  pair_conv<T, C, S, NU2, D, MT, (C >= TTS_PAIR_MTO_MIN), 16 * WN * RS>(acc2, ring, w2, Ts + (16 * wn + l15) * RS, RS, 1,
+                                                                        l15, lq, last_off(NT2, NU2));
   __builtin_amdgcn_sched_barrier(0);  // keep the epilogue's loads out of the MFMA tail
   // residual h (input rows) and, for accumulating launches, the MRF-sum rows in flight while
   // the tile is staged.  The sum is read through a buffer descriptor with no records when the
@@ -263,14 +259,16 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   load_rows(!POST, true);
   __builtin_amdgcn_sched_barrier(0);
   __syncthreads();  // T no longer read
+  {
+    char* ob = smem + (16 * wn + l15) * YS16 + ch0 * 2;  // the lane's output bytes in the wave's tile 0
 #pragma unroll
-  for (int u = 0; u < NU2; ++u)
-    if (NT2 % WN == 0 || wn + WN * u < NT2) {
-      const int o = 16 * (wn + WN * u) + l15;
+    for (int u = 0; u < NU2; ++u)
+      if (NT2 % WN == 0 || wn + WN * u < NT2) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        *reinterpret_cast<uint2*>(smem + o * YS16 + (ch0 + 16 * mt) * 2) = epi_conv2<T>(acc2[u][mt], bias[mt]);
-    }
+        for (int mt = 0; mt < MT; ++mt)
+          *reinterpret_cast<uint2*>(ob + u * 16 * WN * YS16 + 32 * mt) = epi_conv2<T>(acc2[u][mt], bias[mt]);
+      }
+  }
   __syncthreads();
   if constexpr (POST) {
     // final MRF-sum rows (rounded to T as the unfused path stores them) -> lrelu -> LDS tile

@@ -271,15 +271,19 @@ __device__ inline void pair_st8(T* p, f32x4 a, f32x4 b) {
 // (every step reloads its slot D steps ahead), then a peeled last group whose reloads stop
 // at S, then the S % D tail.  Straight-line bodies let the waitcnt pass keep the ring's
 // 2*(D-1) younger loads in flight (a conditional reload made it drain vmcnt to 0 every step).
-// lb: this lane's LDS base (its row rb of the first tile, tap 0); tstep: LDS bytes per tap;
-// trow: rows per tap (swizzle); tile[u]: byte offset of tile u (a multiple of 16 rows).
+// lb: this lane's LDS base for its wave's first tile (row rb of it, tap 0); the wave's tile u
+// sits TU bytes after tile u - 1 (TU = 16 rows x WN waves x row bytes: the waves' tiles are
+// dealt round robin), a compile-time immediate of the LDS reads -- no per-tile address
+// arithmetic -- except for the last tile, at last_off bytes: a wave whose share is one short
+// repeats the block's last tile there (straight-line, result not stored).
+// tstep: LDS bytes per tap; trow: rows per tap (swizzle); rb: the lane's row mod 8 in tile 0.
 // MTO: MFMA order within a step -- M tile outer (each A fragment feeds NU MFMAs back to
 // back) or row tile outer.  Same-box A/B: M-outer 1-3 % faster for the C = 64 / 128 / 256
 // pairs, slower for C = 32 and the chains.
-template <typename T, int C, int S, int NU, int D, int MT = 2, bool MTO = false>
+template <typename T, int C, int S, int NU, int D, int MT = 2, bool MTO = false, int TU = 0>
 __device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][MT], typename Mfma<T>::frag (&ring)[D][MT],
                                           const char* __restrict__ wp, const char* lb, int tstep, int trow,
-                                          const int (&tile)[NU], int rb, int lq) {
+                                          int rb, int lq, int last_off) {
   using G = PairGeom<C>;
   using MF = Mfma16<T>;
   typedef typename Mfma<T>::frag Frag;
@@ -291,7 +295,7 @@ __device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][MT], typename Mfma<T>
     const char* bp = lb + tap * tstep + (((lq + 4 * ks) ^ (((r * G::SW_MUL) >> G::SW_S) & G::SW_M)) << 4);
     Frag bf[NU];
 #pragma unroll
-    for (int u = 0; u < NU; ++u) bf[u] = *reinterpret_cast<const Frag*>(bp + tile[u]);
+    for (int u = 0; u < NU; ++u) bf[u] = *reinterpret_cast<const Frag*>(bp + (u + 1 < NU ? u * TU : last_off));
     if constexpr (MTO) {  // one A fragment held across the NU tiles
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -323,6 +327,15 @@ __device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][MT], typename Mfma<T>
   }
 #pragma unroll
   for (int i = 0; i < REM; ++i) step(NG * D + i, i, false);
+}
+
+// byte offset of this lane's 4 channels (c0 .. c0+3) in LDS row r of a PairGeom<C> tile; the
+// swizzle depends on r mod 8 only, so row r + 16 t is the same offset + 16 t rows
+template <int C>
+__device__ inline int pair_lds4(int r, int c0) {
+  using G = PairGeom<C>;
+  const int cb = c0 * 2;
+  return r * G::RS + ((((cb >> 4) ^ (((r * G::SW_MUL) >> G::SW_S) & G::SW_M))) << 4) + (cb & 15);
 }
 
 }  // namespace tts

@@ -100,7 +100,7 @@ struct AcousticModel::Impl {
       return;
     }
     run(L, x, x_rows, lens, y, y_rows, B, d, s, prof, 1.f, ACT_NONE, alpha, r1);
-    ln_rows(d, y, out, B * y_rows, D, a, b2, s);
+    ln_rows(d, y, out, B * y_rows, D, a, b2, s, lens, y_rows);
   }
   Profiler* prof = nullptr;
   int D = 384, H = 2, V = 78, NMEL = 80, FFN = 1536, PRED = 256;
@@ -377,8 +377,12 @@ struct AcousticModel::Impl {
     if (prof) prof->launch(kind, flops, s, f);
     else HIP_CHECK(f());
   }
-  void ln_rows(int d, const void* in, void* out, int rows, int C, const LNParam& a, const LNParam* b, hipStream_t s) {
-    elem(s, [&] { return launch_layernorm(d, in, out, rows, C, a.g, a.b, b ? b->g : nullptr, b ? b->b : nullptr, eps, s); });
+  // LayerNorm over [B][stride] rows, skipping each utterance's padding rows (r >= lens[b])
+  void ln_rows(int d, const void* in, void* out, int rows, int C, const LNParam& a, const LNParam* b, hipStream_t s,
+               const int* lens, int stride) {
+    elem(s, [&] {
+      return launch_layernorm(d, in, out, rows, C, a.g, a.b, b ? b->g : nullptr, b ? b->b : nullptr, eps, s, lens, stride);
+    });
   }
 
   // one head-batched attention GEMM: Y[b,h][n][m] = sum_c X[b,h][n][c] * W[b,h][m][c]
@@ -419,7 +423,7 @@ struct AcousticModel::Impl {
         prof_launch(PK_ATTN, 6.0 * D * (double)B * Tm * Tm, s, [&] { return launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale,
                                   O, s); });
         run(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
-        ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s);
+        ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s, lens, Tp);
         conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
         continue;
       }
@@ -435,7 +439,7 @@ struct AcousticModel::Impl {
       attn_gemm(dt, P, (long long)H * Tm * Sk, (long long)Tm * Sk, Sk, lens, Tm, Vt, (long long)H * dk * Sk,
                 (long long)dk * Sk, Sk, dk, Sk, O, (long long)Tp * D, dk, D, B, s);
       run(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
-      ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s);
+      ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s, lens, Tp);
       conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
     }
   }
@@ -446,7 +450,7 @@ struct AcousticModel::Impl {
     run(L.pw1, Xb, Tp, lens, A, Tp, B, dt, s, prof);
     elem(s, [&] { return launch_glu_dwconv(dt, A, lens, B, Tp, D, L.dw_w, L.dw_k, L.dw_b, G, s); });
     run(L.pw2, G, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
-    ln_rows(dt, Y, Xb, rows, D, L.ln_conv, nullptr, s);
+    ln_rows(dt, Y, Xb, rows, D, L.ln_conv, nullptr, s, lens, Tp);
     // FFN: x = final_LN(LN(x + 0.5 * ffn(x)))
     run(L.ff1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
     run_ln(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, 0.5f, Xb, Xb, L.ln_ff, &L.ln_final);
@@ -464,7 +468,7 @@ struct AcousticModel::Impl {
     for (int i = 0; i < n; ++i) {
       void* o = bufs[i & 1];
       run(Pr.convs[i], h, Np, lens, o, Np, B, dt, s, prof, 1.f, ACT_RELU);
-      if (i + 1 < n) ln_rows(dt, o, o, B * Np, PRED, Pr.lns[i], nullptr, s);
+      if (i + 1 < n) ln_rows(dt, o, o, B * Np, PRED, Pr.lns[i], nullptr, s, lens, Np);
       else elem(s, [&] { return launch_ln_linear1(dt, o, B * Np, PRED, Pr.lns[i].g, Pr.lns[i].b, eps, Pr.lin_w, Pr.lin_b, out, s); });
       h = o;
     }

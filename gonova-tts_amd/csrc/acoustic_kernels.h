@@ -7,7 +7,7 @@ namespace tts {
 hipError_t launch_embed(int dt, const int* ids, const int* lens, int B, int N, int Tm, const void* E, int V, int D,
                         float scale, void* out, hipStream_t s);
 hipError_t launch_layernorm(int dt, const void* in, void* out, int rows, int C, const float* g1, const float* b1,
-                            const float* g2, const float* b2, float eps, hipStream_t s);
+                            const float* g2, const float* b2, float eps, hipStream_t s, const int* lens = nullptr, int stride = 0);
 hipError_t launch_pos_bias(int dt, const void* qkv, int rows, int D, const float* u, const float* v, void* qu,
                            void* qv, hipStream_t s);
 hipError_t launch_transpose_v(int dt, const void* qkv, const int* lens, int B, int Tm, int D, int H, int Sk, void* vt,

@@ -39,14 +39,23 @@ __device__ inline float wave_sum(float v) {
   return v;
 }
 
+// lens (optional): rows are [B][stride]; row r of utterance b is skipped when r >= lens[b] (the
+// padding past each utterance: no consumer reads it, every kernel masks rows >= len on load)
+__device__ inline bool ln_row_valid(int row, const int* lens, int stride) {
+  if (!lens) return true;
+  const int b = row / stride;
+  return row - b * stride < lens[b];
+}
+
 template <typename T, int PER>
 __global__ __launch_bounds__(256) void layernorm_kernel(const T* __restrict__ in, T* __restrict__ out, int rows,
                                                        int C, const float* __restrict__ g1,
                                                        const float* __restrict__ b1, const float* __restrict__ g2,
-                                                       const float* __restrict__ b2, float eps) {
+                                                       const float* __restrict__ b2, float eps, const int* lens,
+                                                       int stride) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
+  if (row >= rows || !ln_row_valid(row, lens, stride)) return;
   const T* x = in + (long long)row * C;
   float v[PER];
 #pragma unroll
@@ -513,10 +522,11 @@ template <typename T>
 __global__ __launch_bounds__(256) void layernorm8_kernel(const T* __restrict__ in, T* __restrict__ out, int rows,
                                                         int C, const float* __restrict__ g1,
                                                         const float* __restrict__ b1, const float* __restrict__ g2,
-                                                        const float* __restrict__ b2, float eps) {
+                                                        const float* __restrict__ b2, float eps, const int* lens,
+                                                        int stride) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
+  if (row >= rows || !ln_row_valid(row, lens, stride)) return;
   const int c0 = 8 * lane;
   const bool on = c0 < C;
   float v[8];
@@ -564,24 +574,24 @@ __global__ __launch_bounds__(256) void layernorm8_kernel(const T* __restrict__ i
 }
 
 hipError_t launch_layernorm(int dt, const void* in, void* out, int rows, int C, const float* g1, const float* b1,
-                            const float* g2, const float* b2, float eps, hipStream_t s) {
-  if (C > 512) return hipErrorInvalidValue;
+                            const float* g2, const float* b2, float eps, hipStream_t s, const int* lens, int stride) {
+  if (C > 512 || (lens && stride <= 0)) return hipErrorInvalidValue;
   dim3 grid((rows + 3) / 4);
   if (dt != DT_F32 && C % 8 == 0) {
     if (dt == DT_F16)
       hipLaunchKernelGGL(layernorm8_kernel<half_t>, grid, dim3(256), 0, s, (const half_t*)in, (half_t*)out, rows, C,
-                         g1, b1, g2, b2, eps);
+                         g1, b1, g2, b2, eps, lens, stride);
     else
       hipLaunchKernelGGL(layernorm8_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, rows, C,
-                         g1, b1, g2, b2, eps);
+                         g1, b1, g2, b2, eps, lens, stride);
     return hipGetLastError();
   }
   if (C <= 256) {
     TTS_DISPATCH(dt, hipLaunchKernelGGL((layernorm_kernel<TT, 4>), grid, dim3(256), 0, s, (const TT*)in, (TT*)out,
-                                        rows, C, g1, b1, g2, b2, eps));
+                                        rows, C, g1, b1, g2, b2, eps, lens, stride));
   }
   TTS_DISPATCH(dt, hipLaunchKernelGGL((layernorm_kernel<TT, 8>), grid, dim3(256), 0, s, (const TT*)in, (TT*)out, rows,
-                                      C, g1, b1, g2, b2, eps));
+                                      C, g1, b1, g2, b2, eps, lens, stride));
 }
 
 hipError_t launch_pos_bias(int dt, const void* qkv, int rows, int D, const float* u, const float* v, void* qu,

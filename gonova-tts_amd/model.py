@@ -136,11 +136,14 @@ class GonovaTTS:
         spk = speaker_embedding
         mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True,
                                                   speaker_embedding=spk)
+        lens_known = None
         if durations is None:
-            need = int(dur.sum(dim=1).max().item())
+            # one host read for both the frames the durations need and the frame counts
+            need, lens_known = _need_and_lens(dur, mel_lens)
             if need > t_cap:  # exact second pass with the predicted durations and a fitting cap
                 mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
                                                           return_durations=True, speaker_embedding=spk)
+                need, lens_known = _need_and_lens(dur, mel_lens)
         wav = self.engine.vocoder(mel, mel_lens, stream=stream)
         if self.sr != self.native_sr:
             g = gcd(self.sr, self.native_sr)
@@ -148,6 +151,8 @@ class GonovaTTS:
                                                  self.native_sr // g, stream=stream)
             out_lens = out_lens.to(torch.int64)
             return wav, (out_lens.cpu().numpy() if host_lens else out_lens)
+        if host_lens and lens_known is not None:  # already on the host: no second sync
+            return wav, lens_known * self.vocoder_cfg.hop
         wav_lens = mel_lens.to(torch.int64) * self.vocoder_cfg.hop
         return wav, (wav_lens.cpu().numpy() if host_lens else wav_lens)
 
@@ -175,11 +180,11 @@ class GonovaTTS:
             max(1, int(np.asarray(durations).sum(axis=1).max()))
         mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True)
         if durations is None:
-            need = int(dur.sum(dim=1).max().item())
+            need, lens_h = _need_and_lens(dur, mel_lens)  # one host read before the first chunk
             if need > t_cap:
                 mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
                                                           return_durations=True)
-            lens_h = mel_lens.cpu().numpy().astype(np.int64)
+                need, lens_h = _need_and_lens(dur, mel_lens)
         else:
             # given durations fix the frame counts on the host: no device sync between the
             # acoustic pass and the first chunk's vocoder launches (same-box C5: neutral, the
@@ -272,6 +277,16 @@ class GonovaTTS:
 # Alias with the reference's class name so `from gonova_tts_amd.model import ChatterboxTTS`
 # is a one-line swap at synthesizer.py:167.
 ChatterboxTTS = GonovaTTS
+
+
+def _need_and_lens(dur, mel_lens):
+    """One device -> host read: (frames the used durations add up to at most, the frame counts
+    np.int64 [B]) -- the durations kernel's all-zero rule gives an utterance len frames, so the
+    need is the larger of the two per utterance."""
+    import torch
+    h = torch.stack([dur.sum(dim=1).to(torch.int64), mel_lens.to(torch.int64)]).cpu().numpy()
+    need = int(np.maximum(h[0], h[1]).max()) if h.shape[1] else 0
+    return need, h[1].astype(np.int64)
 
 
 def _mel_lens_host(lens: np.ndarray, durations: np.ndarray, t_cap: int) -> np.ndarray:

@@ -160,7 +160,8 @@ class GonovaTTS:
     STREAM_CONTEXT = 16  # mel frames of context per side; HiFi-GAN V1's receptive field is < 13
 
     def stream_tokens(self, tokens: np.ndarray, lens: np.ndarray, chunk_frames: int = 32,
-                      context: Optional[int] = None, durations: Optional[np.ndarray] = None, stream=None):
+                      context: Optional[int] = None, durations: Optional[np.ndarray] = None, stream=None,
+                      speaker_embedding: Optional[np.ndarray] = None):
         """Sub-sentence streaming: one acoustic pass, then the vocoder
         runs on windows [c0 - ctx, c0 + chunk + ctx) and keeps the middle `chunk` frames.
         With ctx >= the receptive field every kept sample is computed from the same inputs
@@ -178,12 +179,14 @@ class GonovaTTS:
         dd = None if durations is None else torch.from_numpy(np.ascontiguousarray(durations, np.int32)).to(dev)
         t_cap = max(64, int(self.FRAMES_PER_TOKEN_CAP * N)) if durations is None else \
             max(1, int(np.asarray(durations).sum(axis=1).max()))
-        mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True)
+        spk = speaker_embedding
+        mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True,
+                                                  speaker_embedding=spk)
         if durations is None:
             need, lens_h = _need_and_lens(dur, mel_lens)  # one host read before the first chunk
             if need > t_cap:
                 mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
-                                                          return_durations=True)
+                                                          return_durations=True, speaker_embedding=spk)
                 need, lens_h = _need_and_lens(dur, mel_lens)
         else:
             # given durations fix the frame counts on the host: no device sync between the
@@ -202,24 +205,59 @@ class GonovaTTS:
             valid = np.clip(lens_h - c0, 0, tc) * hop
             yield c0, wav, valid
 
+    def _voice_groups(self, n: int, speaker_embeddings):
+        """Sentence index groups that share one engine pass: on a multi-speaker model the
+        sentences with and without a voice run as two batches (HF skips the projection when no
+        embedding is given, HF:1192)."""
+        if not self.acoustic_cfg.speaker_embed_dim or speaker_embeddings is None or \
+                all(e is None for e in speaker_embeddings):
+            return [(list(range(n)), None)]
+        with_v = [i for i, e in enumerate(speaker_embeddings) if e is not None]
+        without = [i for i, e in enumerate(speaker_embeddings) if e is None]
+        groups = [(with_v, np.stack([np.asarray(speaker_embeddings[i], np.float32).reshape(-1) for i in with_v]))]
+        if without:
+            groups.append((without, None))
+        return groups
+
+    def stream_batch(self, texts: List[str], chunk_frames: int = 32,
+                     speaker_embeddings: Optional[List[Optional[np.ndarray]]] = None):
+        """Sub-sentence streaming of many sentences in one batched pass (the service's opt-in
+        `stream_frames` mode): yields, per vocoder chunk, a list of (sentence index, float32
+        samples of that chunk, sentence finished).  A sentence's pieces concatenate to the
+        stream_tokens output, which equals the full pass (stream_tokens).  With an output rate
+        other than the vocoder's the pieces would need the resampler's filter context across
+        chunk edges, so each sentence comes as one piece then."""
+        if not texts:
+            return
+        if self.sr != self.native_sr:
+            yield [(i, a, True) for i, a in enumerate(self.generate_batch(texts, speaker_embeddings))]
+            return
+        with self._lock:
+            for idx, spk in self._voice_groups(len(texts), speaker_embeddings):
+                tokens, lens = tokenize_batch([texts[i] for i in idx])
+                done = [False] * len(idx)
+                for c0, wav, valid in self.stream_tokens(tokens, lens, chunk_frames, speaker_embedding=spk):
+                    host = wav.cpu().numpy()
+                    full = host.shape[1]
+                    out = []
+                    for r, i in enumerate(idx):
+                        if done[r]:
+                            continue
+                        v = int(valid[r])
+                        done[r] = v < full  # a short (or empty) piece is the sentence's last
+                        out.append((i, host[r, :v].astype(np.float32, copy=False), done[r]))
+                    yield out
+                last = [(i, np.zeros(0, np.float32), True) for r, i in enumerate(idx) if not done[r]]
+                if last:  # sentences whose length is a whole number of chunks
+                    yield last
+
     def generate_batch(self, texts: List[str], speaker_embeddings: Optional[List[Optional[np.ndarray]]] = None,
                        **_ignored) -> List[np.ndarray]:
         """Synthesize many sentences in one batched pass -> list of float32 waveforms.
-        speaker_embeddings: optional per-sentence voice vectors (None entries: no voice); on a
-        multi-speaker model the sentences with and without a voice run as two batches (HF
-        skips the projection when no embedding is given, HF:1192)."""
+        speaker_embeddings: optional per-sentence voice vectors (None entries: no voice)."""
         if not texts:
             return []
-        if not self.acoustic_cfg.speaker_embed_dim or speaker_embeddings is None or \
-                all(e is None for e in speaker_embeddings):
-            groups = [(list(range(len(texts))), None)]
-        else:
-            with_v = [i for i, e in enumerate(speaker_embeddings) if e is not None]
-            without = [i for i, e in enumerate(speaker_embeddings) if e is None]
-            groups = [(with_v, np.stack([np.asarray(speaker_embeddings[i], np.float32).reshape(-1)
-                                         for i in with_v]))]
-            if without:
-                groups.append((without, None))
+        groups = self._voice_groups(len(texts), speaker_embeddings)
         out: List[Optional[np.ndarray]] = [None] * len(texts)
         with self._lock:
             for idx, spk in groups:

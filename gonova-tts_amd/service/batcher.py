@@ -9,6 +9,9 @@ batches of up to `max_sentences` (one acoustic + one vocoder pass per batch, rag
 lengths handled on device).  Audio goes back per request in sentence order, one binary
 frame per sentence, then the final marker -- the reference's framing
 (`server.py:150-164`) -- as soon as all earlier sentences of that request are done.
+Requests that ask for sub-sentence frames (`stream_frames` > 0) run through
+`synth_stream` (`GonovaTTS.stream_batch`) in batches of their own: each vocoder chunk's
+pieces go out as soon as they reach the host, still in sentence order per request.
 
 Failure: the reference logs and swallows synthesis errors, so the client never gets a
 final marker (`server.py:173-179`).  That stays the default; `notify_errors=True` sends
@@ -31,7 +34,7 @@ logger = logging.getLogger(__name__)
 class DynamicBatcher:
     def __init__(self, queues, synth_batch: Callable[[List[str]], List[np.ndarray]], max_sentences: int = 32,
                  max_requests: int = 64, max_wait: float = 0.004, notify_errors: bool = False,
-                 send_error: Optional[Callable] = None):
+                 send_error: Optional[Callable] = None, synth_stream: Optional[Callable] = None):
         self.queues = queues
         self.synth_batch = synth_batch
         self.max_sentences = max_sentences
@@ -39,6 +42,7 @@ class DynamicBatcher:
         self.max_wait = max_wait
         self.notify_errors = notify_errors
         self.send_error = send_error
+        self.synth_stream = synth_stream  # model.stream_batch: sub-sentence frames (opt-in per request)
         self.running = False
         self.stats = {"rounds": 0, "engine_batches": 0, "sentences": 0, "requests": 0, "errors": 0,
                       "audio_seconds": 0.0, "busy_seconds": 0.0, "max_batch_seen": 0}
@@ -69,37 +73,71 @@ class DynamicBatcher:
         self.stats["requests"] += len(reqs)
         sentences = [split_into_sentences(r.text) for r in reqs]
         work = [(i, j, s) for i, ss in enumerate(sentences) for j, s in enumerate(ss)]
-        results: List[List[Optional[np.ndarray]]] = [[None] * len(ss) for ss in sentences]
+        # per sentence: audio pieces not yet sent, and whether its last piece has arrived
+        pending: List[List[List[np.ndarray]]] = [[[] for _ in ss] for ss in sentences]
+        done = [[False] * len(ss) for ss in sentences]
         failed = [False] * len(reqs)
-        cursor = [0] * len(reqs)
+        cursor = [0] * len(reqs)  # the sentence whose pieces go out next
+        sent = [0] * len(reqs)    # frames sent: the chunk_id of the next frame / the final marker
         finished = [False] * len(reqs)
 
         async def flush():
             for i, r in enumerate(reqs):
                 if finished[i]:
                     continue
-                while cursor[i] < len(results[i]) and results[i][cursor[i]] is not None:
-                    a = results[i][cursor[i]]
-                    await self.queues.enqueue_audio_chunk(r.connection_id, a.astype(np.float32).tobytes(), cursor[i])
+                while cursor[i] < len(pending[i]):
+                    j = cursor[i]
+                    for a in pending[i][j]:
+                        await self.queues.enqueue_audio_chunk(r.connection_id, a.astype(np.float32).tobytes(), sent[i])
+                        sent[i] += 1
+                    pending[i][j].clear()
+                    if not done[i][j]:
+                        break
                     cursor[i] += 1
-                if cursor[i] == len(results[i]) or failed[i]:
+                if cursor[i] == len(pending[i]) or failed[i]:
                     if failed[i] and not self.notify_errors:
                         finished[i] = True  # reference behaviour: no marker after a failure
                         continue
-                    await self.queues.enqueue_audio_chunk(r.connection_id, b"", cursor[i], is_final=True)
+                    await self.queues.enqueue_audio_chunk(r.connection_id, b"", sent[i], is_final=True)
                     finished[i] = True
 
-        order = sorted(range(len(work)), key=lambda k: len(work[k][2]))
-        for b0 in range(0, len(order), self.max_sentences):
-            chunk = order[b0:b0 + self.max_sentences]
+        # engine batches: sentences grouped by framing (per sentence, or sub-sentence frames of
+        # one size; the streamed groups first, they are the latency-sensitive ones), each group
+        # sorted by length and cut into batches of max_sentences
+        def framing(i):
+            f = getattr(reqs[i], "stream_frames", 0) or 0
+            return f if self.synth_stream is not None else 0
+        groups = {}
+        for k, (i, _, _) in enumerate(work):
+            groups.setdefault(framing(i), []).append(k)
+        batches = []
+        for f in sorted(groups, key=lambda f: (f == 0, f)):
+            ks = sorted(groups[f], key=lambda k: len(work[k][2]))
+            batches += [(f, ks[b0:b0 + self.max_sentences]) for b0 in range(0, len(ks), self.max_sentences)]
+
+        for frames, chunk in batches:
             texts = [work[k][2] for k in chunk]
             voices = [getattr(reqs[work[k][0]], "voice", None) for k in chunk]
+            # per-sentence voice (registered embedding) only when one is set
+            kw = {"speaker_embeddings": voices} if any(v is not None for v in voices) else {}
             try:
-                if any(v is not None for v in voices):  # per-sentence voice (registered embedding)
-                    audios = await loop.run_in_executor(
-                        None, lambda: self.synth_batch(texts, speaker_embeddings=voices))
+                if frames == 0:
+                    audios = await loop.run_in_executor(None, lambda: self.synth_batch(texts, **kw))
+                    for k, a in zip(chunk, audios):
+                        i, j, _ = work[k]
+                        pending[i][j].append(a)
+                        done[i][j] = True
+                        self.stats["audio_seconds"] += len(a) / 22050.0
                 else:
-                    audios = await loop.run_in_executor(None, self.synth_batch, texts)
+                    async def deliver(pieces):
+                        for t, a, fin in pieces:
+                            i, j, _ = work[chunk[t]]
+                            if len(a):
+                                pending[i][j].append(a)
+                                self.stats["audio_seconds"] += len(a) / 22050.0
+                            done[i][j] = done[i][j] or fin
+                        await flush()
+                    await self._stream(loop, texts, frames, kw, deliver)
             except Exception as e:
                 self.stats["errors"] += 1
                 logger.error("synthesis_failed: %s", e)
@@ -114,12 +152,35 @@ class DynamicBatcher:
             self.stats["engine_batches"] += 1
             self.stats["sentences"] += len(chunk)
             self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(chunk))
-            for k, a in zip(chunk, audios):
-                i, j, _ = work[k]
-                results[i][j] = a
-                self.stats["audio_seconds"] += len(a) / 22050.0
             await flush()
         await flush()
+
+    async def _stream(self, loop, texts, frames, kw, deliver):
+        """Run `synth_stream` (a generator of per-chunk pieces) on an executor thread and hand
+        each chunk to `deliver` on the event loop as soon as it is on the host, so the first
+        frames go out while the vocoder still works on the rest of the batch."""
+        q: asyncio.Queue = asyncio.Queue()
+        end = object()
+
+        def produce():
+            try:
+                for item in self.synth_stream(texts, frames, **kw):
+                    loop.call_soon_threadsafe(q.put_nowait, item)
+            except BaseException as e:  # noqa: BLE001 -- re-raised on the loop
+                loop.call_soon_threadsafe(q.put_nowait, e)
+                return
+            loop.call_soon_threadsafe(q.put_nowait, end)
+
+        fut = loop.run_in_executor(None, produce)
+        while True:
+            item = await q.get()
+            if item is end:
+                break
+            if isinstance(item, BaseException):
+                await fut
+                raise item
+            await deliver(item)
+        await fut
 
     def stop(self):
         self.running = False

@@ -32,6 +32,7 @@ class SynthesisRequest:
     exaggeration: float = 0.5
     streaming: bool = True
     voice: Optional[Any] = None  # the voice_id's registered speaker embedding (None: default voice)
+    stream_frames: int = 0       # > 0: sub-sentence frames of that many mel frames (opt-in; 0 = per sentence)
 
 
 @dataclass
@@ -94,8 +95,9 @@ class TTSQueueManager:
     # ------------------------------------------------------------------ requests
     async def enqueue_request(self, connection_id: str, text: str, voice_id: str = "default", chunk_size: int = 50,
                               exaggeration: float = 0.5, streaming: bool = True, timeout: float = 2.0,
-                              voice: Optional[Any] = None) -> bool:
-        req = SynthesisRequest(connection_id, text, voice_id, time.time(), chunk_size, exaggeration, streaming, voice)
+                              voice: Optional[Any] = None, stream_frames: int = 0) -> bool:
+        req = SynthesisRequest(connection_id, text, voice_id, time.time(), chunk_size, exaggeration, streaming, voice,
+                               stream_frames)
         try:
             await asyncio.wait_for(self.input_queue.put(req), timeout=timeout)
         except asyncio.TimeoutError:

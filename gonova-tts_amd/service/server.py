@@ -9,6 +9,12 @@
   `register_voice` / `list_voices` answer in the reference's message shapes
   (`server.py:226-256`) -- this engine has no voice cloning, so registration reports
   an error and the list is empty;
+* opt-in sub-sentence streaming: a `"stream_frames": N` field (or the
+  service's `stream_frames` default) splits each sentence's audio into frames of N mel frames
+  (N x 256 samples, the last one shorter) as the vocoder produces them, in sentence order, with
+  the same final marker (its chunk_id = frames sent).  The reference accepts `streaming` /
+  `chunk_size` and ignores them (`core/synthesizer.py:226,245,320-321`); so does this service,
+  and without `stream_frames` the framing stays one frame per sentence;
 * `GET /health` 503 until the model is loaded (`server.py:450-454`), plus the sample rate
   the PCM is in (the reference never tells clients its 24 kHz);
 * `GET /metrics`: the queue metrics dict (`server.py:478-481`).
@@ -59,7 +65,7 @@ class RateLimiter:
 class TTSService:
     def __init__(self, model_factory: Callable, max_connections: int = 50, chunk_size: int = 50,
                  max_sentences: int = 32, max_wait: float = 0.004, notify_errors: bool = False,
-                 device: str = "cuda", device_index: int = 0):
+                 device: str = "cuda", device_index: int = 0, stream_frames: int = 0):
         self.model_factory = model_factory
         self.max_connections = max_connections
         self.chunk_size = chunk_size
@@ -77,6 +83,7 @@ class TTSService:
         self.max_sentences = max_sentences
         self.max_wait = max_wait
         self.notify_errors = notify_errors
+        self.stream_frames = _frames(stream_frames)
         self._task = None
 
     async def start(self):
@@ -88,7 +95,8 @@ class TTSService:
         await self.queues.start()
         self.batcher = DynamicBatcher(self.queues, self.model.generate_batch, max_sentences=self.max_sentences,
                                       max_wait=self.max_wait, notify_errors=self.notify_errors,
-                                      send_error=self._send_error)
+                                      send_error=self._send_error,
+                                      synth_stream=getattr(self.model, "stream_batch", None))
         self._task = asyncio.create_task(self.batcher.run())
         self.is_loaded = True
 
@@ -172,12 +180,13 @@ class TTSService:
             text = data.get("text", "")
             if not isinstance(text, str):
                 raise ValueError("text must be a string")
+            frames = _frames(data.get("stream_frames", self.stream_frames))
             # unknown voices fall back to the default voice (reference server.py:127-138)
             await self.queues.enqueue_request(
                 connection_id=conn_id, text=text, voice_id=vid,
                 chunk_size=data.get("chunk_size", self.chunk_size),
                 exaggeration=data.get("exaggeration", 0.5), streaming=data.get("streaming", True),
-                voice=self.voices.get(vid) if isinstance(vid, str) else None)
+                voice=self.voices.get(vid) if isinstance(vid, str) else None, stream_frames=frames)
         elif kind == "register_voice":
             await ws.send_json(self.register_voice(data))
         elif kind == "list_voices":
@@ -225,6 +234,13 @@ class TTSService:
         except Exception:
             pass
         return info
+
+
+def _frames(v) -> int:
+    """A `stream_frames` value: a whole number of mel frames, 0 (per-sentence frames) to 4096."""
+    if isinstance(v, bool) or not isinstance(v, int) or not 0 <= v <= 4096:
+        raise ValueError(f"stream_frames must be an integer in [0, 4096], got {v!r}")
+    return v
 
 
 def create_app(model_factory: Optional[Callable] = None, **service_kwargs):

@@ -231,3 +231,58 @@ def test_ws_transcript_matches_reference_fixture():
     assert sorted(seen[len(warm):]) == sorted(ref_texts[len(warm):])
     for k, v in gold["metrics"].items():
         assert metrics[k] == v, (k, metrics[k], v)
+
+
+class FakeStreamModel(FakeModel):
+    """Fake with stream_batch: a sentence of n characters is 100 n samples of value n, cut into
+    pieces of chunk_frames * 10 samples (the last shorter), yielded chunk by chunk for the batch."""
+
+    def __init__(self):
+        super().__init__()
+        self.stream_calls = []
+
+    def stream_batch(self, texts, chunk_frames, speaker_embeddings=None):
+        with self.lock:
+            self.stream_calls.append((list(texts), chunk_frames))
+        step = chunk_frames * 10
+        full = [np.full(100 * len(t), len(t), np.float32) for t in texts]
+        n = max(len(a) for a in full)
+        for c0 in range(0, n, step):
+            yield [(i, a[c0:c0 + step], c0 + step >= len(a)) for i, a in enumerate(full) if c0 < len(a)]
+
+
+def test_stream_frames_split_sentences_in_order():
+    """Opt-in sub-sentence frames: a request with stream_frames gets each
+    sentence in pieces, in sentence order, that concatenate to the per-sentence audio; the final
+    marker's chunk_id counts the frames; a request without it in the same session keeps the
+    reference's one frame per sentence; a bad stream_frames value is skipped like any bad message."""
+    model = FakeStreamModel()
+    app = create_app(lambda: model)
+    text = "Hello world. This is a test! Is it working? yes it is."
+    with TestClient(app) as c:
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            ws.send_text(json.dumps({"type": "synthesize", "text": text, "stream_frames": 40}))
+            frames, final = recv_until_complete(ws)
+            assert [len(f) for f in frames] == [400] * 3 + [400] * 3 + [300] + [400] * 6 + [100]
+            assert final == {"type": "synthesis_complete", "chunk_id": len(frames)}
+            want = np.concatenate([np.full(100 * n, n, np.float32) for n in (12, 15, 25)])
+            np.testing.assert_array_equal(np.concatenate(frames), want)
+            ws.send_text(json.dumps({"type": "synthesize", "text": "One. Two!", "stream_frames": -3}))
+            ws.send_text(json.dumps({"type": "synthesize", "text": text}))
+            frames, final = recv_until_complete(ws)
+            assert [len(f) for f in frames] == [1200, 1500, 2500] and final["chunk_id"] == 3
+    assert model.stream_calls == [(["Hello world.", "This is a test!", "Is it working? yes it is."], 40)]
+
+
+def test_stream_frames_service_default():
+    model = FakeStreamModel()
+    app = create_app(lambda: model, stream_frames=100)
+    with TestClient(app) as c:
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            ws.send_text(json.dumps({"type": "synthesize", "text": "Short one. And a much longer second sentence here."}))
+            frames, final = recv_until_complete(ws)
+            # sentence 1: 1000 samples = one piece; sentence 2: 3900 samples = 3 pieces
+            assert [len(f) for f in frames] == [1000, 1000, 1000, 1000, 900] and final["chunk_id"] == 5
+            ws.send_text(json.dumps({"type": "synthesize", "text": "Per sentence again.", "stream_frames": 0}))
+            frames, final = recv_until_complete(ws)
+            assert [len(f) for f in frames] == [1900] and final["chunk_id"] == 1

@@ -122,63 +122,77 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
   const float sl2 = scale * 1.4426950408889634f;  // scores in log2 units
   float* gw = Gs + (kh * 4 + w) * 48 * 16;
 
-  // Staging.  K[j0 .. j0+32) (zero past len) and Vt[:, j0 .. j0+32) per step; the R window
-  // (block slot sb <-> m = i0 - j0 - 31 + sb, 96 rows) lives in a 96-row ring indexed by
-  // m mod 96: a step shifts the window by 32, so only the 32 rows entering it are loaded,
-  // into the slots of the 32 that left.  Loads for step s+1 are issued before step s's
-  // MFMAs (registers, pinned there by a scheduling barrier) and written to LDS after the
-  // barrier that ends step s -- on every step, the last one included, so the loads are
-  // consumed unconditionally (consumed only under a branch, they were sunk into it and
-  // their latency was exposed once per step)
+  // Staging.  K[j0 .. j0+32) and Vt[:, j0 .. j0+32) per step; the R window (block slot sb <->
+  // m = i0 - j0 - 31 + sb, 96 rows) lives in a 96-row ring indexed by m mod 96: a step shifts the
+  // window by 32, so only the 32 rows entering it are loaded, into the slots of the 32 that left.
+  // Loads for step s+1 are issued before step s's MFMAs (registers, pinned there by a scheduling
+  // barrier) and written to LDS after the barrier that ends step s -- on every step, the last one
+  // included, so the loads are consumed unconditionally (consumed only under a branch, they were
+  // sunk into it and their latency was exposed once per step).
+  // The per-step loads go through buffer descriptors whose base moves with j0 (scalar arithmetic)
+  // and whose range ends at the utterance's last key (K rows >= len read 0: no clamp, no mask),
+  // at the end of the (utterance, head) Vt block, and at the position table's last row; each
+  // thread's byte offsets, LDS destinations and ring slots are fixed or stepped by one unsigned
+  // min, so the staging costs no index arithmetic per step (it was ~40 % of the loop's VALU).
   constexpr int KP = AT_BK * (DK / 8) / 256;   // 16-byte pieces per thread: K, Vt, new R rows
   static_assert(AT_BK * (DK / 8) % 256 == 0 && DK * (AT_BK / 8) % 256 == 0, "staging split");
+  constexpr unsigned RING = AT_RW * KR;        // R ring bytes
   auto rslot = [](int m) { const int r = m % AT_RW; return r < 0 ? r + AT_RW : r; };
   auto rrow = [&](int m) { return min(max(rmax - 1 - m, 0), 2 * rmax - 1); };
+  // next ring slot, 32 rows back (mod 96), of a byte address slot * KR + col (col < KR)
+  auto ring_back = [](unsigned a) { return min(a - AT_BK * KR, a + (AT_RW - AT_BK) * KR); };
+  const int rowB = 3 * D * (int)sizeof(T);     // QKV row bytes
+  int kofs[KP], vofs[KP], rofs[KP];
+  unsigned kdst[KP], vdst[KP], rdst[KP];
+#pragma unroll
+  for (int i = 0; i < KP; ++i) {
+    const int p = tid + 256 * i;
+    const int r = p / (DK / 8), c = p - r * (DK / 8);
+    kofs[i] = r * rowB + c * 16;
+    kdst[i] = r * KR + c * 16;
+    // position-table row row0 + r <-> m = i0 - j0 - r; the first prefetch is for j0 = kbeg + 32
+    rofs[i] = r * D * (int)sizeof(T) + c * 16;
+    rdst[i] = rslot(i0 - kbeg - AT_BK - r) * KR + c * 16;
+    const int d = p / (AT_BK / 8), cv = p - d * (AT_BK / 8);
+    vofs[i] = d * Sk * (int)sizeof(T) + cv * 16;
+    vdst[i] = d * VR + cv * 16;
+  }
   u32x4 pkv[KP], pvt[KP], prr[KP];
   auto load_kv = [&](int j0) __attribute__((always_inline)) {
+    // Vt is zero past len (transpose_v); columns past Sk read the next row's (finite) values or,
+    // past the block, 0 -- those keys are masked out of the softmax
+    const auto kr = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(qkv + ((long long)b * Tp + j0) * 3 * rowD + D + h * DK),
+                                                      0, max(len - j0, 0) * rowB, 0x00020000);
+    const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(vt + ((long long)b * H + h) * DK * Sk + j0), 0,
+                                                      max(DK * Sk - j0, 0) * (int)sizeof(T), 0x00020000);
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
-      const int p = tid + 256 * i;
-      const int r = p / (DK / 8), c = p - r * (DK / 8);
-      const int j = j0 + r;
-      // addresses clamped into the buffers and the loads consumed unconditionally (a load under
-      // a branch or consumed only under a mask makes the waitcnt pass drain vmcnt); keys past
-      // len are masked out of the softmax, so their K / Vt only have to be finite
-      pkv[i] = *reinterpret_cast<const u32x4*>(qkv + ((long long)b * Tp + min(j, Tp - 1)) * 3 * rowD + D + h * DK + c * 8);
-      const int d = p / (AT_BK / 8), cv = p - d * (AT_BK / 8);
-      const int jv = j0 + cv * 8;  // Vt is zero past len (transpose_v) and padded to Sk
-      pvt[i] = *reinterpret_cast<const u32x4*>(vt + (((long long)b * H + h) * DK + d) * Sk + min(jv, Sk - 8));
+      pkv[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(kr, kofs[i], 0, 0));
+      pvt[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vr, vofs[i], 0, 0));
     }
   };
   auto load_r = [&](int j0) __attribute__((always_inline)) {
+    // R rows entering the window: table rows rmax - 1 - i0 + j0 + [0, 32) (m = i0 - j0 - [0, 32));
+    // rows past the table's last (m < -(rmax - 1), only masked keys use them) read 0
+    const int row0 = rmax - 1 - i0 + j0;  // >= 0: i0 < len <= Tm <= rmax
+    const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(ptab + (long long)row0 * rowD + h * DK), 0,
+                                                      max(rmax + i0 - j0, 0) * D * (int)sizeof(T), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < KP; ++i)
+      prr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, rofs[i], 0, 0));
+  };
+  auto write_kv = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
-      const int p = tid + 256 * i;
-      const int r = p / (DK / 8), c = p - r * (DK / 8);
-      // R rows entering the window: m = i0 - j0 - 31 + [0, 32)
-      const int m = i0 - j0 - (AT_BK - 1) + r;
-      prr[i] = *reinterpret_cast<const u32x4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 8);
+      *reinterpret_cast<u32x4*>(Ks + kdst[i]) = pkv[i];
+      *reinterpret_cast<u32x4*>(Vs + vdst[i]) = pvt[i];
     }
   };
-  // the zero masks are applied here, after the step's MFMAs (applied at the loads, they pulled
-  // the loads' waits into the step)
-  auto write_kv = [&](int j0) __attribute__((always_inline)) {
+  auto write_r = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
-      const int p = tid + 256 * i;
-      const int r = p / (DK / 8), c = p - r * (DK / 8);
-      *reinterpret_cast<u32x4*>(Ks + r * KR + c * 16) = j0 + r < len ? pkv[i] : u32x4{};
-      const int d = p / (AT_BK / 8), cv = p - d * (AT_BK / 8);
-      *reinterpret_cast<u32x4*>(Vs + d * VR + cv * 16) = j0 + cv * 8 < Sk ? pvt[i] : u32x4{};
-    }
-  };
-  auto write_r = [&](int j0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < KP; ++i) {
-      const int p = tid + 256 * i;
-      const int r = p / (DK / 8), c = p - r * (DK / 8);
-      const int m = i0 - j0 - (AT_BK - 1) + r;
-      *reinterpret_cast<u32x4*>(Rs + rslot(m) * KR + c * 16) = prr[i];
+      *reinterpret_cast<u32x4*>(Rs + rdst[i]) = prr[i];
+      rdst[i] = ring_back(rdst[i]);
     }
   };
   // first step: the whole 96-row R window
@@ -189,17 +203,24 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
         *reinterpret_cast<const uint4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 8);
   }
   load_kv(kbeg);
-  write_kv(kbeg);
+  write_kv();
   __syncthreads();
+  // this lane's R fragment rows: slot of m = i0w - j0 - 31 + q (+ 16 t per tile), plus its column
+  unsigned ra = rslot(i0w - kbeg - (AT_BK - 1) + q) * KR + 16 * g;
 
   for (int j0 = kbeg; j0 < kbeg + khalf; j0 += AT_BK) {
     load_kv(j0 + AT_BK);  // in flight during this step's MFMAs (the last step's are written, unused)
     load_r(j0 + AT_BK);
     __builtin_amdgcn_sched_barrier(0);
-    const int mbw = i0w - j0 - (AT_BK - 1);  // m of this wave's G slot 0
     // S^T tiles (keys 16 kt + 4g + e, query q) and G^T tiles (slots 16 t + 4g + e)
     f32x4 sacc[2] = {f32x4{}, f32x4{}};
     f32x4 gacc[3] = {f32x4{}, f32x4{}, f32x4{}};
+    unsigned rt[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const unsigned y = ra + 16 * t * KR;
+      rt[t] = t ? min(y, y - RING) : y;
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
@@ -209,10 +230,11 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
       }
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        const Frag a = *reinterpret_cast<const Frag*>(Rs + rslot(mbw + 16 * t + q) * KR + (ks * 32 + 8 * g) * 2);
+        const Frag a = *reinterpret_cast<const Frag*>(Rs + rt[t] + ks * 64);
         gacc[t] = MF::mma(a, bv[ks], gacc[t]);
       }
     }
+    ra = ring_back(ra);
     // G^T -> wave scratch [slot][q]; gather G[q][q - key + 31] for the lane's 8 keys
 #pragma unroll
     for (int t = 0; t < 3; ++t)
@@ -221,19 +243,25 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's scratch writes landed
     __builtin_amdgcn_wave_barrier();
     float sv[8];
-    float mloc = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int kk = 16 * kt + 4 * g + e;
         const float bd = gw[(q - kk + AT_BK - 1) * 16 + q];
-        float sc = (sacc[kt][e] + bd) * sl2;
-        if (j0 + kk >= kend) sc = -INFINITY;
-        sv[4 * kt + e] = sc;
-        mloc = fmaxf(mloc, sc);
+        sv[4 * kt + e] = (sacc[kt][e] + bd) * sl2;
       }
     __builtin_amdgcn_wave_barrier();
+    if (j0 + AT_BK > kend) {  // wave-uniform: only a group's last step has keys past its end
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (j0 + 16 * kt + 4 * g + e >= kend) sv[4 * kt + e] = -INFINITY;
+    }
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mloc = fmaxf(mloc, sv[e]);
     mloc = at_xor32_max(at_xor16_max(mloc));
     const float m_new = fmaxf(m_run, mloc);
     // a step with every key masked (the second key group of a short utterance) keeps m = -inf:
@@ -266,8 +294,8 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
       oacc[t] = MF::mma(*reinterpret_cast<const Frag*>(&av), bp, oacc[t] * alpha);
     }
     __syncthreads();  // every wave is done with this step's K / Vt and the leaving R rows
-    write_kv(j0 + AT_BK);
-    write_r(j0 + AT_BK);
+    write_kv();
+    write_r();
     __syncthreads();
   }
   if constexpr (KH > 1) {

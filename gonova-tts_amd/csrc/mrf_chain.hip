@@ -174,6 +174,15 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
   const int r0g = n0 - H0;             // utterance row of LDS row 0
   const float slope = p.slope;
   const int ch0 = 32 * wm + 4 * lq;    // + 16*mt: this lane's 4 output channels
+  // per-lane swizzle tables of the 8 row phases (every conv's rows and taps are compile-time
+  // offsets from l15): B-fragment chunks and epilogue bytes without per-step swizzle arithmetic
+  int sw8[8], ep8[8];
+  pair_sw8<C>(sw8, l15, lq);
+  pair_ep8<C>(ep8, l15, lq);
+  const int lrow = (16 * wn + l15) * RS;  // the lane's row in its wave's tile 0, LDS row 0 based
+  // Interior blocks (every LDS row inside the utterance) store the epilogues unmasked; only the
+  // first and last blocks of an utterance zero the rows outside it (the unfused convs' padding)
+  const bool edge = r0g < 0 || r0g + NRA > len;
   const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
   constexpr int TU = 16 * WN * RS;     // bytes from a wave's tile u to its tile u + 1
 
@@ -241,9 +250,9 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
       for (int u = 0; u < NU1; ++u)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc1[u][mt] = acc_init(bias[mt]);
-      const int rb = LO1 - A * DQ + l15;
-      pair_conv<T, C, S, NU1, D, MT, false, TU>(acc1, ring, w1, GT + (rb + 16 * wn) * RS, DQ * RS, DQ, rb, lq,
-                                                16 * (min(wn + WN * (NU1 - 1), NT1 - 1) - wn) * RS);
+      constexpr int RB1 = LO1 - A * DQ;
+      pair_conv<T, C, S, NU1, D, MT, false, TU, RB1, DQ>(acc1, ring, w1, GT + RB1 * RS + lrow, DQ * RS, DQ, RB1 + l15, lq,
+                                                         16 * (min(wn + WN * (NU1 - 1), NT1 - 1) - wn) * RS, sw8);
       __builtin_amdgcn_sched_barrier(0);
       const f32x4 b1v[MT] = {bias[0], bias[1]};  // conv1's bias for its epilogue (no-op with TTS_BIAS_ACC)
       // conv2's bias before the weight preload: in-order vmcnt
@@ -252,15 +261,15 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
       preload(p.w2[Q]);  // conv2's first steps in flight during the epilogue
       __builtin_amdgcn_sched_barrier(0);
       __syncthreads();  // T overwrites G
-      {
+      auto epi1 = [&](auto EDGE) __attribute__((always_inline)) {
         int eo[MT];  // the lane's bytes in the wave's tile 0 (tile u: + u * TU)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) eo[mt] = pair_lds4<C>(LO1 + 16 * wn + l15, ch0 + 16 * mt);
+        for (int mt = 0; mt < MT; ++mt) eo[mt] = LO1 * RS + lrow + (ep8[LO1 & 7] ^ ((2 * wm + mt) << 5));
         const int gr0 = r0g + LO1 + 16 * wn + l15;
 #pragma unroll
         for (int u = 0; u < NU1; ++u)
           if (NT1 % WN == 0 || wn + WN * u < NT1) {
-            const bool valid = (unsigned)(gr0 + 16 * WN * u) < (unsigned)len;
+            const bool valid = !decltype(EDGE)::value || (unsigned)(gr0 + 16 * WN * u) < (unsigned)len;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
               uint2 pk = epi_conv1<T>(acc1[u][mt], b1v[mt], slope);
@@ -268,7 +277,8 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
               *reinterpret_cast<uint2*>(GT + eo[mt] + u * TU) = pk;
             }
           }
-      }
+      };
+      if (edge) epi1(std::true_type{}); else epi1(std::false_type{});
       __syncthreads();
     }
     // conv2: output rows [LO2, LO2 + 16 NT2) read T rows (row - A) + tap
@@ -278,9 +288,9 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
       for (int u = 0; u < NU2; ++u)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc2[u][mt] = acc_init(bias[mt]);
-      const int rb = LO2 - A + l15;
-      pair_conv<T, C, S, NU2, D, MT, false, TU>(acc2, ring, w2, GT + (rb + 16 * wn) * RS, RS, 1, rb, lq,
-                                                16 * (min(wn + WN * (NU2 - 1), NT2 - 1) - wn) * RS);
+      constexpr int RB2 = LO2 - A;
+      pair_conv<T, C, S, NU2, D, MT, false, TU, RB2, 1>(acc2, ring, w2, GT + RB2 * RS + lrow, RS, 1, RB2 + l15, lq,
+                                                        16 * (min(wn + WN * (NU2 - 1), NT2 - 1) - wn) * RS, sw8);
       __builtin_amdgcn_sched_barrier(0);
       const f32x4 b2v[MT] = {bias[0], bias[1]};  // conv2's bias for its epilogue (no-op with TTS_BIAS_ACC)
       if constexpr (Q < 2) {
@@ -299,10 +309,10 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
       }
       __builtin_amdgcn_sched_barrier(0);
       __syncthreads();  // T no longer read
-      {
+      auto epi2 = [&](auto EDGE) __attribute__((always_inline)) {
         int eo[MT];  // the lane's bytes in the wave's tile 0 (tile u: + u * TU)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) eo[mt] = pair_lds4<C>(LO2 + 16 * wn + l15, ch0 + 16 * mt);
+        for (int mt = 0; mt < MT; ++mt) eo[mt] = LO2 * RS + lrow + (ep8[LO2 & 7] ^ ((2 * wm + mt) << 5));
         const int gr0 = r0g + LO2 + 16 * wn + l15;
 #pragma unroll
         for (int u = 0; u < NU2; ++u)
@@ -312,7 +322,7 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
               const int o = eo[mt] + u * TU;
               const uint2 y = epi_conv2<T>(acc2[u][mt], b2v[mt]);
               if constexpr (Q < 2) {
-                const bool valid = (unsigned)(gr0 + 16 * WN * u) < (unsigned)len;
+                const bool valid = !decltype(EDGE)::value || (unsigned)(gr0 + 16 * WN * u) < (unsigned)len;
                 const uint2 h = epi_add4<T>(y, *reinterpret_cast<const uint2*>(Hs + o));
                 *reinterpret_cast<uint2*>(Hs + o) = h;
                 *reinterpret_cast<uint2*>(GT + o) = valid ? lrelu4<T>(h, slope) : uint2{0u, 0u};
@@ -321,7 +331,8 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
               }
             }
           }
-      }
+      };
+      if (edge) epi2(std::true_type{}); else epi2(std::false_type{});
       __syncthreads();
     }
   };

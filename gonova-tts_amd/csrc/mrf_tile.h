@@ -280,19 +280,30 @@ __device__ inline void pair_st8(T* p, f32x4 a, f32x4 b) {
 // MTO: MFMA order within a step -- M tile outer (each A fragment feeds NU MFMAs back to
 // back) or row tile outer.  Same-box A/B: M-outer 1-3 % faster for the C = 64 / 128 / 256
 // pairs, slower for C = 32 and the chains.
-template <typename T, int C, int S, int NU, int D, int MT = 2, bool MTO = false, int TU = 0>
+// RB0 / TROW (the chain kernel, whose row offsets and dilations are compile-time): rb = l15 + RB0
+// and trow = TROW, so a step's row phase (r mod 8, which fixes the swizzle) is a compile-time
+// index into sw8 (pair_sw8) and its chunk offset one register -- no swizzle arithmetic per step.
+// Used where every step is unrolled (fewer than two full groups of D steps).
+template <typename T, int C, int S, int NU, int D, int MT = 2, bool MTO = false, int TU = 0, int RB0 = -1, int TROW = 0>
 __device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][MT], typename Mfma<T>::frag (&ring)[D][MT],
                                           const char* __restrict__ wp, const char* lb, int tstep, int trow,
-                                          int rb, int lq, int last_off) {
+                                          int rb, int lq, int last_off, const int* sw8 = nullptr) {
   using G = PairGeom<C>;
   using MF = Mfma16<T>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int KS = C / 32;
   constexpr int NG = S / D, REM = S % D;
+  constexpr bool TABLE = RB0 >= 0 && NG < 2;
   auto step = [&](const int s, const int slot, const bool reload) __attribute__((always_inline)) {
     const int tap = KS == 1 ? s : s / KS, ks = KS == 1 ? 0 : s % KS;
-    const int r = rb + tap * trow;
-    const char* bp = lb + tap * tstep + (((lq + 4 * ks) ^ (((r * G::SW_MUL) >> G::SW_S) & G::SW_M)) << 4);
+    const char* bp;
+    if constexpr (TABLE) {
+      // (lq + 4 ks) ^ sw = (lq ^ sw) ^ 4 ks: lq < 4, so the k-step only flips chunk bits >= 2
+      bp = lb + tap * TROW * G::RS + (sw8[(RB0 + tap * TROW) & 7] ^ (ks << 6));
+    } else {
+      const int r = rb + tap * trow;
+      bp = lb + tap * tstep + (((lq + 4 * ks) ^ (((r * G::SW_MUL) >> G::SW_S) & G::SW_M)) << 4);
+    }
     Frag bf[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) bf[u] = *reinterpret_cast<const Frag*>(bp + (u + 1 < NU ? u * TU : last_off));
@@ -327,6 +338,23 @@ __device__ __forceinline__ void pair_conv(f32x4 (&acc)[NU][MT], typename Mfma<T>
   }
 #pragma unroll
   for (int i = 0; i < REM; ++i) step(NG * D + i, i, false);
+}
+
+// sw8[j]: the B-fragment chunk byte offset (k-step 0) of a lane whose tile row is l15 + j (mod 8)
+template <int C>
+__device__ inline void pair_sw8(int (&sw8)[8], int l15, int lq) {
+  using G = PairGeom<C>;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sw8[j] = (lq ^ ((((l15 + j) * G::SW_MUL) >> G::SW_S) & G::SW_M)) << 4;
+}
+// ep8[j]: pair_lds4's chunk bytes for row l15 + j (mod 8) and channels 4 lq .. 4 lq + 3; channel
+// c0 = 4 lq + 16 m (m = 2 wm + mt) adds m to the chunk's bits >= 1, i.e. ep8[j] ^ (m << 5)
+template <int C>
+__device__ inline void pair_ep8(int (&ep8)[8], int l15, int lq) {
+  using G = PairGeom<C>;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    ep8[j] = (((lq >> 1) ^ ((((l15 + j) * G::SW_MUL) >> G::SW_S) & G::SW_M)) << 4) + 8 * (lq & 1);
 }
 
 // byte offset of this lane's 4 channels (c0 .. c0+3) in LDS row r of a PairGeom<C> tile; the

@@ -28,6 +28,11 @@ def main():
         m, ml = e.acoustic(tok, tl, 864)
         out[f"mel_b{B}"] = m.cpu().numpy()
         out[f"wav_b{B}"] = e.vocoder(m, ml).cpu().numpy()
+        if B == 8:  # ragged lengths: the attention kernels' partial key steps and padding rows
+            tl = torch.randint(29, 145, (B,), generator=g, dtype=torch.int32).cuda()
+            m, ml = e.acoustic(tok, tl, 864)
+            valid = torch.arange(m.shape[1], device=m.device)[None, :] < ml[:, None].long()
+            out["mel_ragged_b8"] = torch.where(valid[..., None], m, torch.zeros_like(m)).cpu().numpy()
         e.close()
     for k, v in out.items():
         print(k, v.shape, hashlib.sha256(v.tobytes()).hexdigest()[:16])

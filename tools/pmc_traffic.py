@@ -25,8 +25,25 @@ import os
 import sys
 from collections import defaultdict
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from tools.layer_breakdown import vocoder_layers  # noqa: E402
+
+
+def vocoder_layers(T):
+    """(name, Cout, Cin, k, frames) of every vocoder conv for T mel frames, in launch order:
+    conv_pre, then per stage the upsampler and 18 MRF convs, then conv_post."""
+    layers = [("pre", 512, 80, 7, T)]
+    ch, up, ks = [256, 128, 64, 32], [8, 8, 2, 2], [3, 7, 11]
+    cin, t = 512, T
+    for i in range(4):
+        layers.append((f"s{i}.up", up[i] * ch[i], cin, 2, t))
+        t *= up[i]
+        for k in ks:
+            for d in (1, 3, 5):
+                layers.append((f"s{i}.k{k}.c1", ch[i], ch[i], k, t))
+                layers.append((f"s{i}.k{k}.c2", ch[i], ch[i], k, t))
+        cin = ch[i]
+    layers.append(("post", 1, 32, 7, t))
+    return layers
+
 
 FAMILIES = ("conv_gemm", "conv_xres", "mrf_fused", "mrf_pair", "mrf_chain", "conv_post", "upsample_stream")
 

@@ -12,7 +12,7 @@ for S in "$@"; do
     ACOUSTIC_PROF_LAUNCHES=1 python3 $R/tools/acoustic_prof.py --summarize $O/ac${B}_s$i/run_kernel_trace.csv > $O/ac${B}_s$i.sum || exit 1
     echo "$S B=$B: $(head -1 $O/ac${B}_s$i.sum)"
   done
-  env $S timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/c2_s$i -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-full --no-c4 --no-streaming --no-cpu-baseline > $O/c2_s$i.log 2>&1 || exit 1
+  env $S timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/c2_s$i -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-full --no-c4 --no-streaming --no-cpu-baseline --no-c1 > $O/c2_s$i.log 2>&1 || exit 1
   python3 $R/tools/step_breakdown.py $O/c2_s$i/run_kernel_trace.csv > $O/bd_s$i.txt || exit 1
   rm -rf $O/ac32_s$i $O/ac8_s$i $O/c2_s$i
 done

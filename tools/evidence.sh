@@ -15,7 +15,7 @@ cp $O/${T}_pmc_traffic_c2.json $R/profiles/
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 900 python3 $R/bench.py > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rocprof -o run -- python3 $R/bench.py > $O/rocprof_bench.json 2> $O/rocprof.err || { tail -5 $O/rocprof.err; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/c2trace -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-full --no-c4 --no-streaming --no-cpu-baseline > $O/c2trace.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/c2trace -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-full --no-c4 --no-streaming --no-cpu-baseline --no-c1 > $O/c2trace.log 2>&1 || exit 1
 python3 $R/tools/step_breakdown.py $O/c2trace/run_kernel_trace.csv > $O/step_breakdown_c2.txt || exit 1
 bash $R/tools/pmc_clock.sh $T/clock || exit 1
 python3 $R/tools/pmc_clock.py $O/clock > $O/clock_mfma_c2.txt || exit 1

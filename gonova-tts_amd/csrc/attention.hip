@@ -598,52 +598,69 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
   float* gw = Gs + w * 48 * 16;
 
   // staging: fp32 pieces loaded for step s+1 during step s, split into the two planes after
-  // the barrier that ends it (every step), masks applied there
+  // the barrier that ends it (every step).  As in rel_attn_kernel: buffer descriptors stepped by
+  // scalar base arithmetic (K rows >= len and Vt columns past the block read 0, table rows past
+  // the last read 0 -- only masked keys use them), per-thread offsets and LDS destinations fixed,
+  // ring slots stepped by one unsigned min, masks only on the last key step
   constexpr int KP = AT_BK * (DK / 4) / 256;
   static_assert(AT_BK * (DK / 4) % 256 == 0 && DK * (AT_BK / 4) % 256 == 0, "staging split");
+  constexpr unsigned RING = AT_RW * KR;
   auto rslot = [](int m) { const int r = m % AT_RW; return r < 0 ? r + AT_RW : r; };
   auto rrow = [&](int m) { return min(max(rmax - 1 - m, 0), 2 * rmax - 1); };
+  auto ring_back = [](unsigned a) { return min(a - AT_BK * KR, a + (AT_RW - AT_BK) * KR); };
   auto put = [](char* plane_hi, int plane, int off, f32x4 v) __attribute__((always_inline)) {
     uint2 hi, lo;
     at_split4(v, hi, lo);
     *reinterpret_cast<uint2*>(plane_hi + off) = hi;
     *reinterpret_cast<uint2*>(plane_hi + plane + off) = lo;
   };
+  const int rowB = 3 * D * 4;  // QKV row bytes
+  int kofs[KP], vofs[KP], rofs[KP];
+  unsigned kdst[KP], vdst[KP], rdst[KP];
+#pragma unroll
+  for (int i = 0; i < KP; ++i) {
+    const int p = tid + 256 * i;
+    const int r = p / (DK / 4), c = p - r * (DK / 4);
+    kofs[i] = r * rowB + c * 16;
+    kdst[i] = r * KR + c * 8;
+    rofs[i] = r * D * 4 + c * 16;                        // table row row0 + r <-> m = i0 - j0 - r
+    rdst[i] = rslot(i0 - AT_BK - r) * KR + c * 8;        // slot for the first prefetch (j0 = 32)
+    const int d = p / (AT_BK / 4), cv = p - d * (AT_BK / 4);
+    vofs[i] = d * Sk * 4 + cv * 16;
+    vdst[i] = d * VR + cv * 8;
+  }
   f32x4 pkv[KP], pvt[KP], prr[KP];
   auto load_kv = [&](int j0) __attribute__((always_inline)) {
+    const auto kr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(qkv + ((long long)b * Tp + j0) * 3 * rowD + D + h * DK),
+                                                      0, max(len - j0, 0) * rowB, 0x00020000);
+    const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vt + ((long long)b * H + h) * DK * Sk + j0), 0,
+                                                      max(DK * Sk - j0, 0) * 4, 0x00020000);
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
-      const int p = tid + 256 * i;
-      const int r = p / (DK / 4), c = p - r * (DK / 4);
-      pkv[i] = *reinterpret_cast<const f32x4*>(qkv + ((long long)b * Tp + min(j0 + r, Tp - 1)) * 3 * rowD + D + h * DK + c * 4);
-      const int d = p / (AT_BK / 4), cv = p - d * (AT_BK / 4);
-      pvt[i] = *reinterpret_cast<const f32x4*>(vt + (((long long)b * H + h) * DK + d) * Sk + min(j0 + cv * 4, Sk - 4));
+      pkv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(kr, kofs[i], 0, 0));
+      pvt[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(vr, vofs[i], 0, 0));
     }
   };
   auto load_r = [&](int j0) __attribute__((always_inline)) {
+    const int row0 = rmax - 1 - i0 + j0;  // >= 0: i0 < len <= Tm <= rmax
+    const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ptab + (long long)row0 * rowD + h * DK), 0,
+                                                      max(rmax + i0 - j0, 0) * D * 4, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < KP; ++i)
+      prr[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, rofs[i], 0, 0));
+  };
+  auto write_kv = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
-      const int p = tid + 256 * i;
-      const int r = p / (DK / 4), c = p - r * (DK / 4);
-      prr[i] = *reinterpret_cast<const f32x4*>(ptab + (long long)rrow(i0 - j0 - (AT_BK - 1) + r) * rowD + h * DK + c * 4);
+      put(Ks, KPL, kdst[i], pkv[i]);
+      put(Vs, VPL, vdst[i], pvt[i]);
     }
   };
-  auto write_kv = [&](int j0) __attribute__((always_inline)) {
+  auto write_r = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
-      const int p = tid + 256 * i;
-      const int r = p / (DK / 4), c = p - r * (DK / 4);
-      put(Ks, KPL, r * KR + c * 8, j0 + r < len ? pkv[i] : f32x4{});
-      const int d = p / (AT_BK / 4), cv = p - d * (AT_BK / 4);
-      put(Vs, VPL, d * VR + cv * 8, j0 + cv * 4 < Sk ? pvt[i] : f32x4{});
-    }
-  };
-  auto write_r = [&](int j0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < KP; ++i) {
-      const int p = tid + 256 * i;
-      const int r = p / (DK / 4), c = p - r * (DK / 4);
-      put(Rs, RPL, rslot(i0 - j0 - (AT_BK - 1) + r) * KR + c * 8, prr[i]);
+      put(Rs, RPL, rdst[i], prr[i]);
+      rdst[i] = ring_back(rdst[i]);
     }
   };
   for (int p = tid; p < AT_RW * (DK / 4); p += 256) {
@@ -652,19 +669,23 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
     put(Rs, RPL, rslot(m) * KR + c * 8, *reinterpret_cast<const f32x4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 4));
   }
   load_kv(0);
-  write_kv(0);
+  write_kv();
   __syncthreads();
+  unsigned ra = rslot(i0w - (AT_BK - 1) + q) * KR + 16 * g;  // this lane's R rows (slot of m + 16 t) and column
 
   for (int j0 = 0; j0 < len; j0 += AT_BK) {
     load_kv(j0 + AT_BK);
     load_r(j0 + AT_BK);
     __builtin_amdgcn_sched_barrier(0);
-    const int mbw = i0w - j0 - (AT_BK - 1);
     f32x4 sacc[2] = {f32x4{}, f32x4{}}, saccx[2] = {f32x4{}, f32x4{}};
     f32x4 gacc[3] = {f32x4{}, f32x4{}, f32x4{}}, gaccx[3] = {f32x4{}, f32x4{}, f32x4{}};
-    int rs[3];
+    unsigned rs[3];
 #pragma unroll
-    for (int t = 0; t < 3; ++t) rs[t] = rslot(mbw + 16 * t + q) * KR;
+    for (int t = 0; t < 3; ++t) {
+      const unsigned y = ra + 16 * t * KR;
+      rs[t] = t ? min(y, y - RING) : y;
+    }
+    ra = ring_back(ra);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int co = (ks * 32 + 8 * g) * 2;
@@ -678,7 +699,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
       }
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        const char* rr = Rs + rs[t] + co;
+        const char* rr = Rs + rs[t] + ks * 64;
         const Frag ah = *reinterpret_cast<const Frag*>(rr), al = *reinterpret_cast<const Frag*>(rr + RPL);
         gacc[t] = MF::mma(ah, bv[ks], gacc[t]);
         gaccx[t] = MF::mma(ah, bvl[ks], gaccx[t]);
@@ -694,7 +715,6 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's scratch writes landed
     __builtin_amdgcn_wave_barrier();
     float sv[8];
-    float mloc = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       const f32x4 s4 = sacc[kt] + saccx[kt] * (1.f / AT_SPLIT);
@@ -702,13 +722,20 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
       for (int e = 0; e < 4; ++e) {
         const int kk = 16 * kt + 4 * g + e;
         const float bd = gw[(q - kk + AT_BK - 1) * 16 + q];
-        float sc = (s4[e] + bd) * sl2;
-        if (j0 + kk >= len) sc = -INFINITY;
-        sv[4 * kt + e] = sc;
-        mloc = fmaxf(mloc, sc);
+        sv[4 * kt + e] = (s4[e] + bd) * sl2;
       }
     }
     __builtin_amdgcn_wave_barrier();
+    if (j0 + AT_BK > len) {  // wave-uniform: only the last step has keys past len
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (j0 + 16 * kt + 4 * g + e >= len) sv[4 * kt + e] = -INFINITY;
+    }
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mloc = fmaxf(mloc, sv[e]);
     mloc = at_xor32_max(at_xor16_max(mloc));
     const float m_new = fmaxf(m_run, mloc);
     const float alpha = at_exp2(m_run - m_new);
@@ -740,8 +767,8 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
       oaccx[t] = MF::mma(al, bp, ox);
     }
     __syncthreads();
-    write_kv(j0 + AT_BK);
-    write_r(j0 + AT_BK);
+    write_kv();
+    write_r();
     __syncthreads();
   }
   const int i = i0w + q;

@@ -232,8 +232,7 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
   __syncthreads();
 
   T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
-  constexpr int NIT = BN * VPR / NTHR;
-  static_assert(BN * VPR % NTHR == 0, "row pass");
+  constexpr int NIT = (BN * VPR + NTHR - 1) / NTHR;  // row-pass pieces per thread (the last may be partial)
   uint4 sin[NIT];
   auto pair = [&](auto PI) __attribute__((always_inline)) {
     constexpr int Q = decltype(PI)::value;
@@ -346,7 +345,7 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
     const int idx = tid + it * NTHR;
     const int o = idx / VPR, c8 = idx % VPR;
     const int gr = n0 + o;
-    if (gr >= len) continue;
+    if ((BN * VPR % NTHR != 0 && idx >= BN * VPR) || gr >= len) continue;
     const int r = H0 + o;
     const int off = r * RS + ((c8 ^ swz(r)) << 4);
     T* dst = Y + (long long)gr * C + c8 * 8;

@@ -57,28 +57,71 @@ constexpr int PAIR_PO = 8;
 // stage 0 at batch 8: 48 blocks for 256 CUs; see pair_div).  A row's
 // arithmetic (k-step order, roundings) does not depend on the tile height, so the output is
 // bit-identical to the full-height launch (tests/test_vocoder_gpu.py).
-template <int C, int DIV>
+// Full-height output rows per block by (C, k).  A multiple of 16 spends most of a conv1 tile on
+// the 2*a2 halo rows (k = 3 at C = 256: five 16-row tiles for 66 rows, conv2 four for 64): a height
+// that makes conv1's BN + 2*a2 rows a whole number of tiles leaves the rounding to conv2 (k = 3
+// at C = 256: 78 rows, ten tiles in all for 78 rows instead of nine for 64; the weight stream
+// per row drops by the same 18 %).  At C = 64 (two waves along the rows) the height also makes
+// conv1's tile count even, so no wave repeats a tile.  Any height works: a row's arithmetic does
+// not depend on it.  Same-box A/B (profiles/r03i_ab_tile_heights.txt): C = 256 k = 3 / 7 pairs
+// 976 -> 1011 / 1087 -> 1142 TF/s, C = 128 k = 3 996 -> 1039, C = 32 k = 11 963 -> 980.
+#ifndef TTS_PBN_256_3
+#define TTS_PBN_256_3 78
+#endif
+#ifndef TTS_PBN_256_7
+#define TTS_PBN_256_7 74
+#endif
+#ifndef TTS_PBN_128_3
+#define TTS_PBN_128_3 142
+#endif
+#ifndef TTS_PBN_32_11
+#define TTS_PBN_32_11 502
+#endif
+#ifndef TTS_PBN_128_7
+#define TTS_PBN_128_7 138
+#endif
+#ifndef TTS_PBN_64_7
+#define TTS_PBN_64_7 282
+#endif
+#ifndef TTS_PBN_64_11
+#define TTS_PBN_64_11 278
+#endif
+template <int C, int K>
+constexpr int pair_bn() {
+  if (C == 256 && K == 3) return TTS_PBN_256_3;
+  if (C == 256 && K == 7) return TTS_PBN_256_7;
+  if (C == 128 && K == 3) return TTS_PBN_128_3;
+  if (C == 32 && K == 11) return TTS_PBN_32_11;
+  if (C == 128 && K == 7) return TTS_PBN_128_7;
+  if (C == 64 && K == 7) return TTS_PBN_64_7;
+  if (C == 64 && K == 11) return TTS_PBN_64_11;
+  return PairGeom<C>::BN;
+}
+
+template <int C, int DIV, int K = 0, bool POST = false>
 struct PairGeomS : PairGeom<C> {
-  static constexpr int BN = PairGeom<C>::BN / DIV;
+  static constexpr int BN = DIV == 1 && K > 0 && !POST ? pair_bn<C, K>() : PairGeom<C>::BN / DIV;
 };
 
-// LDS bytes of one launch (G tile incl. conv1 overrun rows, T tile; >= output staging tile)
-template <int C, int DIV = 1>
+// LDS bytes of one launch (G tile incl. conv1 overrun rows, T tile; >= output staging tile of
+// 16 * NT2 rows: conv2's last tile may run past the BO output rows)
+template <int C, int DIV = 1, int K = 0, bool POST = false>
 static size_t pair_lds_bytes(int k, int d, bool post) {
-  using G = PairGeomS<C, DIV>;
+  using G = PairGeomS<C, DIV, K, POST>;
   const int a1 = (k - 1) / 2 * d, a2 = (k - 1) / 2;
   const int bo = G::BN + (post ? 2 * PAIR_PO : 0);
   const int nt1 = (bo + 2 * a2 + 15) / 16;
+  const int nt2 = (bo + 15) / 16;
 
   const size_t g = (size_t)(16 * nt1 + 2 * a1) * G::RS;
   const size_t t = (size_t)16 * nt1 * G::RS;
-  return std::max(std::max(g, t), (size_t)bo * (C * 2 + 16));
+  return std::max(std::max(g, t), (size_t)16 * nt2 * (C * 2 + 16));
 }
 
 template <typename T, int C, int K, bool POST = false, int DIV = 1>
 __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom<C>::OCC)) void mrf_pair_kernel(
     MrfPairParams p) {
-  using G = PairGeomS<C, DIV>;
+  using G = PairGeomS<C, DIV, K, POST>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int BN = G::BN, WM = G::WM, WN = G::WN, RS = G::RS;
   constexpr int D = G::D;              // weight ring depth (k-steps)
@@ -93,7 +136,8 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   constexpr int RT = BO + 2 * A2;      // conv1 rows conv2 needs
   constexpr int NT1 = (RT + 15) / 16;  // conv1 tiles (block)
   constexpr int NU1 = (NT1 + WN - 1) / WN;  // conv1 tiles per wave (the last may be a repeat)
-  constexpr int NT2 = BO / 16;         // conv2 tiles (block)
+  constexpr int NT2 = (BO + 15) / 16;  // conv2 tiles (block; the last may run past BO: not stored)
+  static_assert(NT2 <= NT1, "conv2's overrun rows (past BO) read inside the G / T region");
   constexpr int NU2 = (NT2 + WN - 1) / WN;  // conv2 tiles per wave (the last may be a repeat)
   static_assert(!POST || (C == 32 && BN == 512 && NTHR == 256), "conv_post fusion: C = 32, two samples per thread");
   constexpr int VPR = C / 8;           // 16-byte pieces per row
@@ -227,7 +271,6 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   __syncthreads();
 
   constexpr int NIT = (BO * VPR + NTHR - 1) / NTHR;  // 16-byte row pieces per thread in the row pass
-  static_assert(POST || BO * VPR % NTHR == 0, "row pass");
 
   // ---- conv2 over the BN output rows: output row o reads T rows o .. o + 2*a2 ----
   f32x4 acc2[NU2][MT];
@@ -323,7 +366,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
     const int idx = tid + it * NTHR;
     const int o = idx / VPR, c8 = idx % VPR;
     const int gr = n0 + o;
-    if (gr >= len) continue;
+    if ((BO * VPR % NTHR != 0 && idx >= BO * VPR) || gr >= len) continue;
     T* dst = Y + (long long)gr * C + c8 * 8;
     const uint4 y = *reinterpret_cast<const uint4*>(smem + o * YS16 + c8 * 16);
     store16<TTS_ROW_STORE>(Y, (int)((dst - Y) * (long long)sizeof(T)), epi_row<T>(y, xin[it], p.accum, sin[it], p.scale));
@@ -351,8 +394,8 @@ static int pair_div(int C, const MrfPairParams& p, bool post) {
 
 template <typename T, int C, int K, bool POST, int DIV>
 static hipError_t launch_pair_g(const MrfPairParams& p, hipStream_t s) {
-  using G = PairGeomS<C, DIV>;
-  const size_t lds = pair_lds_bytes<C, DIV>(K, p.d, POST);
+  using G = PairGeomS<C, DIV, K, POST>;
+  const size_t lds = pair_lds_bytes<C, DIV, K, POST>(K, p.d, POST);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   dim3 grid(xcd_grid((p.T + G::BN - 1) / G::BN, p.B));
   hipLaunchKernelGGL((mrf_pair_kernel<T, C, K, POST, DIV>), grid, dim3(64 * G::WM * G::WN), lds, s, p);

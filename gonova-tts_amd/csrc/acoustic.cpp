@@ -80,27 +80,22 @@ struct AcousticModel::Impl {
     run_layer(L, x, x_rows, lens, y, y_rows, B, d, s, pr, in_slope, act, alpha, r1, nullptr, 1.f, 0, 0, cur_rpad,
               split_ws, split_ws_bytes, ln);
   }
-  // a residual GEMM followed by the block's post-LN: out = LN2?(LN1(y)).  The exact encoder's
-  // split-K projections apply the LayerNorm in their reduce (conv_split.hip); other paths run it
-  // as its own launch inside the same call.
+  // the LayerNorm fields (ConvParams) of a post-LN -- LN2?(LN1(y)) -> out -- with the row-tile
+  // counters that let the 16-bit X-resident and one-slice split GEMMs apply it in their own launch
+  // (ln_rows.h); the split-K fp32 GEMMs apply it in their reduce, and any other path runs it as a
+  // separate launch inside conv_gemm_launch (TTS_LN_FUSE=0: no counters)
+  ConvParams ln_params(void* out, const LNParam& a, const LNParam* b2) const {
+    ConvParams ln = conv_params_default();
+    ln.ln_out = out; ln.ln_g1 = a.g; ln.ln_b1 = a.b; ln.ln_g2 = b2 ? b2->g : nullptr; ln.ln_b2 = b2 ? b2->b : nullptr;
+    ln.ln_eps = eps;
+    if (sw(SW_LN_FUSE) != 0) { ln.ln_cnt = ln_cnt; ln.ln_cnt_n = ln_cnt_n; }
+    return ln;
+  }
+  // a residual GEMM followed by the block's post-LN: out = LN2?(LN1(y))
   void run_ln(const ConvLayer& L, const void* x, int x_rows, const int* lens, void* y, int y_rows, int B, int d,
               hipStream_t s, float alpha, const void* r1, void* out, const LNParam& a, const LNParam* b2) {
-    // the ConvParams this GEMM launches with (run_layer's), to ask whether its path fuses the LN
-    ConvParams q = conv_params_default();
-    q.x = x; q.sxb = (long long)x_rows * L.Cin; q.sxr = L.Cin; q.x_len = lens; q.x_rows = x_rows;
-    q.w = L.w; q.w_ld = L.taps * L.Cin; q.bias = L.bias; q.wpk = L.wpk;
-    q.y = y; q.syb = (long long)y_rows * L.M; q.syr = L.M; q.r1 = r1; q.srb = q.syb; q.srr = L.M;
-    q.y_len = lens; q.y_rows = y_rows; q.M = L.M; q.Cin = L.Cin; q.taps = L.taps; q.dil = L.dil; q.pad = L.pad;
-    q.alpha = alpha; q.B = B; q.rows_pad = cur_rpad; q.ws = split_ws; q.ws_bytes = split_ws_bytes;
-    if (d == DT_F32 && conv_split_fuses_ln(q)) {
-      ConvParams ln = conv_params_default();
-      ln.ln_out = out; ln.ln_g1 = a.g; ln.ln_b1 = a.b; ln.ln_g2 = b2 ? b2->g : nullptr; ln.ln_b2 = b2 ? b2->b : nullptr;
-      ln.ln_eps = eps;
-      run(L, x, x_rows, lens, y, y_rows, B, d, s, prof, 1.f, ACT_NONE, alpha, r1, &ln);
-      return;
-    }
-    run(L, x, x_rows, lens, y, y_rows, B, d, s, prof, 1.f, ACT_NONE, alpha, r1);
-    ln_rows(d, y, out, B * y_rows, D, a, b2, s, lens, y_rows);
+    const ConvParams ln = ln_params(out, a, b2);
+    run(L, x, x_rows, lens, y, y_rows, B, d, s, prof, 1.f, ACT_NONE, alpha, r1, &ln);
   }
   Profiler* prof = nullptr;
   int D = 384, H = 2, V = 78, NMEL = 80, FFN = 1536, PRED = 256;
@@ -129,6 +124,8 @@ struct AcousticModel::Impl {
   void *ENC = nullptr, *PB1 = nullptr, *PB2 = nullptr, *BEF = nullptr, *PN1 = nullptr, *PN2 = nullptr, *MELT = nullptr;
   float *f_pitch = nullptr, *f_energy = nullptr, *f_logd = nullptr;
   int *i_dur = nullptr, *i_tokmap = nullptr;
+  int* ln_cnt = nullptr;  // row-tile counters of the fused post-LNs (zeroed once; ln_rows.h)
+  int ln_cnt_n = 0;
 
   ~Impl() {
     for (void* p : allocs) hipFree(p);
@@ -286,6 +283,8 @@ struct AcousticModel::Impl {
     X = Y = O = G = Qu = Qv = H1 = QKV = A = Vt = ENC = SPK = PB1 = PB2 = BEF = PN1 = PN2 = MELT = nullptr;
     f_pitch = f_energy = f_logd = nullptr;
     i_dur = i_tokmap = nullptr;
+    ln_cnt = nullptr;
+    ln_cnt_n = 0;
     split_ws = nullptr;
     split_ws_bytes = 0;
     std::vector<void*> old;
@@ -353,6 +352,10 @@ struct AcousticModel::Impl {
     f_pitch = (float*)alloc_ws(nrows, 4); f_energy = (float*)alloc_ws(nrows, 4); f_logd = (float*)alloc_ws(nrows, 4);
     i_dur = (int*)alloc_ws((size_t)B * N, 4);
     i_tokmap = (int*)alloc_ws((size_t)B * T, 4);
+    // one counter per row tile of the fused post-LN launches: >= 64-row tiles per utterance (conv_xres)
+    // or over the packed encoder rows (conv_splitp)
+    ln_cnt_n = (int)std::max((size_t)B * (std::max(Tp, enc_rows(N)) / 32 + 2), nrows / 32 + 2);
+    ln_cnt = (int*)alloc_ws((size_t)ln_cnt_n, 4);
     // split-K partials of the encoder's packed split GEMMs (fp32 encoder of a 16-bit model)
     long long wsb = 0;
     if (dte == DT_F32 && dt != DT_F32) {
@@ -377,14 +380,6 @@ struct AcousticModel::Impl {
     if (prof) prof->launch(kind, flops, s, f);
     else HIP_CHECK(f());
   }
-  // LayerNorm over [B][stride] rows, skipping each utterance's padding rows (r >= lens[b])
-  void ln_rows(int d, const void* in, void* out, int rows, int C, const LNParam& a, const LNParam* b, hipStream_t s,
-               const int* lens, int stride) {
-    elem(s, [&] {
-      return launch_layernorm(d, in, out, rows, C, a.g, a.b, b ? b->g : nullptr, b ? b->b : nullptr, eps, s, lens, stride);
-    });
-  }
-
   // one head-batched attention GEMM: Y[b,h][n][m] = sum_c X[b,h][n][c] * W[b,h][m][c]
   void attn_gemm(int d, const void* x, long long sxb, long long sxh, int sxr, const int* lens, int x_rows, const void* w,
                  long long swb, long long swh, int w_ld, int M, int K, void* y, long long syb, long long syh,
@@ -422,8 +417,7 @@ struct AcousticModel::Impl {
         const bool split = dt == DT_F32 && this->dt != DT_F32 && sw(SW_ATTN_SPLIT) != 0;
         prof_launch(PK_ATTN, 6.0 * D * (double)B * Tm * Tm, s, [&] { return launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale,
                                   O, s); });
-        run(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
-        ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s, lens, Tp);
+        run_ln(L.out, O, Tp, lens, Y, Tp, B, dt, s, 1.f, Xb, Xb, L.ln_att, nullptr);
         conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
         continue;
       }
@@ -438,8 +432,7 @@ struct AcousticModel::Impl {
       // O[b][i][h*dk + d] = sum_j P[b,h][i][j] * Vt[b,h][d][j]
       attn_gemm(dt, P, (long long)H * Tm * Sk, (long long)Tm * Sk, Sk, lens, Tm, Vt, (long long)H * dk * Sk,
                 (long long)dk * Sk, Sk, dk, Sk, O, (long long)Tp * D, dk, D, B, s);
-      run(L.out, O, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
-      ln_rows(dt, Y, Xb, rows, D, L.ln_att, nullptr, s, lens, Tp);
+      run_ln(L.out, O, Tp, lens, Y, Tp, B, dt, s, 1.f, Xb, Xb, L.ln_att, nullptr);
       conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
     }
   }
@@ -449,8 +442,7 @@ struct AcousticModel::Impl {
     // conv module: x = LN(x + pw2(silu(bn(dw(glu(pw1(x)))))))
     run(L.pw1, Xb, Tp, lens, A, Tp, B, dt, s, prof);
     elem(s, [&] { return launch_glu_dwconv(dt, A, lens, B, Tp, D, L.dw_w, L.dw_k, L.dw_b, G, s); });
-    run(L.pw2, G, Tp, lens, Y, Tp, B, dt, s, prof, 1.f, ACT_NONE, 1.f, Xb);
-    ln_rows(dt, Y, Xb, rows, D, L.ln_conv, nullptr, s, lens, Tp);
+    run_ln(L.pw2, G, Tp, lens, Y, Tp, B, dt, s, 1.f, Xb, Xb, L.ln_conv, nullptr);
     // FFN: x = final_LN(LN(x + 0.5 * ffn(x)))
     run(L.ff1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
     run_ln(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, 0.5f, Xb, Xb, L.ln_ff, &L.ln_final);
@@ -467,9 +459,10 @@ struct AcousticModel::Impl {
     const int n = (int)Pr.convs.size();
     for (int i = 0; i < n; ++i) {
       void* o = bufs[i & 1];
-      run(Pr.convs[i], h, Np, lens, o, Np, B, dt, s, prof, 1.f, ACT_RELU);
-      if (i + 1 < n) ln_rows(dt, o, o, B * Np, PRED, Pr.lns[i], nullptr, s, lens, Np);
-      else elem(s, [&] { return launch_ln_linear1(dt, o, B * Np, PRED, Pr.lns[i].g, Pr.lns[i].b, eps, Pr.lin_w, Pr.lin_b, out, s); });
+      // conv + ReLU, then its LayerNorm in place (the last layer: LayerNorm + Linear(C -> 1) -> out)
+      ConvParams ln = ln_params(i + 1 < n ? o : nullptr, Pr.lns[i], nullptr);
+      if (i + 1 == n) { ln.ln_lin_w = Pr.lin_w; ln.ln_lin_b = Pr.lin_b; ln.ln_lin_out = out; }
+      run(Pr.convs[i], h, Np, lens, o, Np, B, dt, s, prof, 1.f, ACT_RELU, 1.f, nullptr, &ln);
       h = o;
     }
   }

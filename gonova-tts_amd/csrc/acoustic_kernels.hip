@@ -6,6 +6,7 @@
 // lengths `lens[b]` give B=1 semantics (rows >= len are never read by valid rows).
 #include "acoustic_kernels.h"
 #include "common.h"
+#include "ln_rows.h"
 
 namespace tts {
 
@@ -33,11 +34,6 @@ __global__ void embed_kernel(const int* __restrict__ ids, const int* __restrict_
 // LayerNorm over C (one wave per row), optional second LayerNorm applied after
 // (ff_layer_norm followed by final_layer_norm, HF:644-647).  Two-pass variance in fp32.
 // ---------------------------------------------------------------------------
-__device__ inline float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 
 // lens (optional): rows are [B][stride]; row r of utterance b is skipped when r >= lens[b] (the
 // padding past each utterance: no consumer reads it, every kernel masks rows >= len on load)
@@ -57,44 +53,19 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const T* __restrict__ in
   const int lane = threadIdx.x & 63;
   if (row >= rows || !ln_row_valid(row, lens, stride)) return;
   const T* x = in + (long long)row * C;
-  float v[PER];
+  int ch[PER];
+  bool on[PER];
+  ln_lanes64<PER>(ch, on, C, lane);  // ln_rows.h
+  float g[2][PER], bb[2][PER], v[1][PER];
+  ln_params<PER>(g, bb, ch, on, g1, b1, g2, b2);
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int c = lane + 64 * i;
-    v[i] = c < C ? to_f32(x[c]) : 0.f;
-  }
-  const float invC = 1.f / (float)C;
-  for (int pass = 0; pass < (g2 ? 2 : 1); ++pass) {
-    const float* g = pass ? g2 : g1;
-    const float* bb = pass ? b2 : b1;
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) s += v[i];
-    const float mu = wave_sum(s) * invC;
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = lane + 64 * i;
-      const float d = c < C ? v[i] - mu : 0.f;
-      q += d * d;
-    }
-    const float rstd = rsqrtf(wave_sum(q) * invC + eps);
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = lane + 64 * i;
-      if (c < C) {
-        float y = (v[i] - mu) * rstd * g[c] + bb[c];
-        if (pass == 0 && g2) y = to_f32(from_f32<T>(y));  // first LN output is materialised in T
-        v[i] = y;
-      }
-    }
-  }
+  for (int i = 0; i < PER; ++i) v[0][i] = on[i] ? to_f32(x[ch[i]]) : 0.f;
+  if (g2) ln_batch<T, 1, PER, true>(v, on, C, g, bb, eps);
+  else ln_batch<T, 1, PER, false>(v, on, C, g, bb, eps);
   T* o = out + (long long)row * C;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int c = lane + 64 * i;
-    if (c < C) o[c] = from_f32<T>(v[i]);
-  }
+  for (int i = 0; i < PER; ++i)
+    if (on[i]) o[ch[i]] = from_f32<T>(v[0][i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -363,34 +334,19 @@ __global__ __launch_bounds__(256) void ln_linear1_kernel(const T* __restrict__ i
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const T* x = in + (long long)row * C;
-  float v[PER];
-  float s = 0.f;
+  int ch[PER];
+  bool on[PER];
+  ln_lanes64<PER>(ch, on, C, lane);  // ln_rows.h
+  float gl[PER], bl[PER], wl[PER], v[1][PER], o[1];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int c = lane + 64 * i;
-    v[i] = c < C ? to_f32(x[c]) : 0.f;
-    s += v[i];
+    gl[i] = on[i] ? g[ch[i]] : 0.f;
+    bl[i] = on[i] ? bb[ch[i]] : 0.f;
+    wl[i] = on[i] ? w[ch[i]] : 0.f;
+    v[0][i] = on[i] ? to_f32(x[ch[i]]) : 0.f;
   }
-  const float mu = wave_sum(s) / (float)C;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int c = lane + 64 * i;
-    const float d = c < C ? v[i] - mu : 0.f;
-    q += d * d;
-  }
-  const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
-  float dot = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int c = lane + 64 * i;
-    if (c < C) {
-      const float y = to_f32(from_f32<T>((v[i] - mu) * rstd * g[c] + bb[c]));
-      dot = fmaf(y, w[c], dot);
-    }
-  }
-  dot = wave_sum(dot);
-  if (lane == 0) out[row] = dot + wb;
+  ln_linear1_batch<T, 1, PER>(v, on, C, gl, bl, wl, eps, wb, o);
+  if (lane == 0) out[row] = o[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -527,50 +483,17 @@ __global__ __launch_bounds__(256) void layernorm8_kernel(const T* __restrict__ i
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows || !ln_row_valid(row, lens, stride)) return;
-  const int c0 = 8 * lane;
-  const bool on = c0 < C;
-  float v[8];
-  {
-    uint4 u = uint4{0u, 0u, 0u, 0u};
-    if (on) u = *reinterpret_cast<const uint4*>(in + (long long)row * C + c0);
-    const T* e = reinterpret_cast<const T*>(&u);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = to_f32(e[i]);
-  }
-  const float invC = 1.f / (float)C;
-  for (int pass = 0; pass < (g2 ? 2 : 1); ++pass) {
-    const float* g = pass ? g2 : g1;
-    const float* bb = pass ? b2 : b1;
-    float sm = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) sm += v[i];
-    const float mu = wave_sum(sm) * invC;
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float d = on ? v[i] - mu : 0.f;
-      q += d * d;
-    }
-    const float rstd = rsqrtf(wave_sum(q) * invC + eps);
-    if (on) {
-      const f32x4 ga = *reinterpret_cast<const f32x4*>(g + c0), gb = *reinterpret_cast<const f32x4*>(g + c0 + 4);
-      const f32x4 ba = *reinterpret_cast<const f32x4*>(bb + c0), bc = *reinterpret_cast<const f32x4*>(bb + c0 + 4);
-      const float gg[8] = {ga[0], ga[1], ga[2], ga[3], gb[0], gb[1], gb[2], gb[3]};
-      const float be[8] = {ba[0], ba[1], ba[2], ba[3], bc[0], bc[1], bc[2], bc[3]};
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float y = (v[i] - mu) * rstd * gg[i] + be[i];
-        if (pass == 0 && g2) y = to_f32(from_f32<T>(y));  // first LN output is materialised in T
-        v[i] = y;
-      }
-    }
-  }
-  if (on) {
-    T o[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = from_f32<T>(v[i]);
-    *reinterpret_cast<uint4*>(out + (long long)row * C + c0) = *reinterpret_cast<const uint4*>(o);
-  }
+  int ch[8];
+  bool on[8];
+  ln_lanes8(ch, on, C, lane);  // ln_rows.h
+  float g[2][8], bb[2][8], v[1][8];
+  ln_params<8>(g, bb, ch, on, g1, b1, g2, b2);
+  uint4 u = uint4{0u, 0u, 0u, 0u};
+  if (on[0]) u = *reinterpret_cast<const uint4*>(in + (long long)row * C + ch[0]);
+  ln_unpack8<T>(u, v[0]);
+  if (g2) ln_batch<T, 1, 8, true>(v, on, C, g, bb, eps);
+  else ln_batch<T, 1, 8, false>(v, on, C, g, bb, eps);
+  if (on[0]) *reinterpret_cast<uint4*>(out + (long long)row * C + ch[0]) = ln_pack8<T>(v[0]);
 }
 
 hipError_t launch_layernorm(int dt, const void* in, void* out, int rows, int C, const float* g1, const float* b1,

@@ -29,6 +29,7 @@
 #include "conv_epilogue.h"
 #include "acoustic_kernels.h"
 #include "kernels.h"
+#include "ln_rows.h"
 #include "switches.h"
 
 #include <algorithm>
@@ -258,6 +259,92 @@ __device__ inline void ld8(const T* p, f32x4& a, f32x4& b) {
 __device__ int g_xres_stamp_target[3];
 __device__ unsigned long long g_xres_stamp[1 << 20];
 #endif
+
+#ifndef TTS_LN_TAIL
+#define TTS_LN_TAIL 1  // 0: timing-only probe builds -- fused post-LN tails load their rows but compute nothing
+#endif
+#ifndef TTS_LN_LOADPOL
+#define TTS_LN_LOADPOL -1  // diagnostic builds: cache-policy bits of the tail's row loads (buffer loads)
+#endif
+#ifndef TTS_LN_FUSE_MINBLK
+#define TTS_LN_FUSE_MINBLK 512  // GEMM blocks from which a launch applies its post-LN itself (same-box A/B: 0 slower at batch 8)
+#endif
+#ifndef TTS_LN_RB
+#define TTS_LN_RB 4    // rows per wave in flight in the fused post-LN tail (8 spills at three blocks per CU)
+#endif
+// The fused post-LN of a conv_xres launch (ConvParams::ln_cnt): rows [n0, min(n0 + BN, ylen)) of
+// utterance b's output Y (all M channels, written by the tile's M blocks), one wave per row, eight
+// rows in flight per wave; arithmetic of layernorm8_kernel / ln_linear1_kernel (ln_rows.h).
+template <typename T, int BN>
+__device__ inline void xres_tile_ln(const ConvParams& p, const T* Y, int b, int n0, int ylen, int wave, int lane) {
+  const int nrow = min(BN, ylen - n0);
+  const int C = p.M;
+  constexpr int RB = TTS_LN_RB;  // rows per wave in flight and normalised together
+  if (p.ln_lin_out) {    // LayerNorm + Linear(C -> 1): lane l owns channels l + 64 i
+    int ch[8];
+    bool on[8];
+    ln_lanes64<8>(ch, on, C, lane);
+    float gl[8], bl[8], wl[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      gl[i] = on[i] ? p.ln_g1[ch[i]] : 0.f;
+      bl[i] = on[i] ? p.ln_b1[ch[i]] : 0.f;
+      wl[i] = on[i] ? p.ln_lin_w[ch[i]] : 0.f;
+    }
+    float* out = p.ln_lin_out + (long long)b * p.y_rows + n0;
+    for (int r0 = wave; r0 < nrow; r0 += 4 * RB) {
+      float v[RB][8], o[RB];
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {  // unconditional loads at clamped rows / channels
+        const T* x = Y + (long long)(n0 + min(r0 + 4 * k, nrow - 1)) * p.syr;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[k][i] = to_f32(x[min(ch[i], C - 1)]);
+      }
+#pragma unroll
+      for (int k = 0; k < RB; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (!on[i]) v[k][i] = 0.f;
+      ln_linear1_batch<T, RB, 8>(v, on, C, gl, bl, wl, p.ln_eps, p.ln_lin_b, o);
+#pragma unroll
+      for (int k = 0; k < RB; ++k)
+        if (lane == 0 && r0 + 4 * k < nrow) out[r0 + 4 * k] = o[k];
+    }
+    return;
+  }
+  T* L = reinterpret_cast<T*>(p.ln_out) + (long long)b * p.syb;
+  int ch[8];
+  bool on[8];
+  ln_lanes8(ch, on, C, lane);
+  float g[2][8], bb[2][8];
+  ln_params<8>(g, bb, ch, on, p.ln_g1, p.ln_b1, p.ln_g2, p.ln_b2);
+  const int c0 = on[0] ? ch[0] : 0;  // lanes past C load a valid piece and discard it
+  // the next RB rows' loads are in flight while the current RB rows are normalised (one memory
+  // round trip for the tail instead of one per RB rows)
+  uint4 u[2][RB];
+  auto load = [&](uint4 (&d)[RB], int r0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+      d[k] = *reinterpret_cast<const uint4*>(Y + (long long)(n0 + min(r0 + 4 * k, nrow - 1)) * p.syr + c0);
+  };
+  load(u[0], wave);
+#pragma unroll
+  for (int it = 0; it < (BN + 4 * RB - 1) / (4 * RB); ++it) {
+    const int r0 = wave + it * 4 * RB;
+    if (r0 >= nrow) break;  // wave-uniform
+    if (it + 1 < (BN + 4 * RB - 1) / (4 * RB)) load(u[(it + 1) & 1], r0 + 4 * RB);
+    float v[RB][8];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) ln_unpack8<T>(on[0] ? u[it & 1][k] : uint4{0u, 0u, 0u, 0u}, v[k]);
+#if TTS_LN_TAIL
+    if (p.ln_g2) ln_batch<T, RB, 8, true>(v, on, C, g, bb, p.ln_eps);
+    else ln_batch<T, RB, 8, false>(v, on, C, g, bb, p.ln_eps);
+#endif
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+      if (on[0] && r0 + 4 * k < nrow) *reinterpret_cast<uint4*>(L + (long long)(n0 + r0 + 4 * k) * p.syr + c0) = ln_pack8<T>(v[k]);
+  }
+}
 
 // XF: the group's X loads all in flight at once (one round trip instead of three), the weight
 // ring primed after them so the registers fit at three blocks per CU.  Same values staged, same
@@ -495,6 +582,7 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
   }
   __syncthreads();
   const bool plain = !R1 && !R2 && p.out_scale == 1.0f;
+  const bool lnf = p.ln_cnt != nullptr;  // LayerNorm in this launch (the launcher checked the shape)
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int rl = tid / PPR + it * (NTHR / PPR);
@@ -514,7 +602,15 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
       if (p.out_scale != 1.0f) { v0 *= p.out_scale; v1 *= p.out_scale; }
       y = pack8<T>(v0, v1);
     }
-    store16<TTS_XRES_STORE>(Y, (int)(((long long)row * p.syr + col) * (long long)sizeof(T)), y);
+    const int yo = (int)(((long long)row * p.syr + col) * (long long)sizeof(T));
+    if (lnf) store16<16>(Y, yo, y);  // write-through: the tile's last block reads it (ln_rows.h)
+    else store16<TTS_XRES_STORE>(Y, yo, y);
+  }
+  if (lnf) {
+    // the row tile's last-arriving M block normalises rows [n0, ylen) of it over all M channels
+    if (!ln_tile_last(p.ln_cnt + blockIdx.z * gridDim.x + blockIdx.x, gridDim.y, reinterpret_cast<int*>(smem)))
+      return;
+    xres_tile_ln<T, BN>(p, Y, b, n0, ylen, wave, lane);
   }
 #if TTS_XRES_STAMP
   if (p.M == g_xres_stamp_target[0] && p.Cin == g_xres_stamp_target[1] && p.taps == g_xres_stamp_target[2]) {
@@ -674,18 +770,35 @@ static int xres_nt(const ConvParams& p, int wm) {
   return 4;
 }
 
+// whether a conv_xres launch of row-tile height BN applies p's LayerNorm itself (ln_cnt given,
+// rows of M <= 512 channels in whole 16-byte pieces, one counter per row tile)
+static bool xres_ln_ok(const ConvParams& p, int BN) {
+  if (!p.ln_cnt || !(p.ln_out || p.ln_lin_out) || !TTS_XRES_EPI16 || p.up_s || p.nh != 1) return false;
+  if (sw(SW_LN_FUSE) > 1 && sw(SW_LN_FUSE) != 2 && sw(SW_LN_FUSE) != 7 && sw(SW_LN_FUSE) != (p.ln_lin_out ? 6 : 5))
+    return false;  // (bisection: 2 = conv_xres only, 5 / 6 = its LayerNorm / LayerNorm + Linear launches only)
+  // small grids: every block runs at once, so the tile's LayerNorm tail is on the critical path
+  // and costs more than the separate launch (the result is the same either way)
+  if (sw(SW_LN_FUSE) != 7 && (long long)((p.y_rows + BN - 1) / BN) * p.B * ((p.M + 127) / 128) < TTS_LN_FUSE_MINBLK)
+    return false;  // (TTS_LN_FUSE=7: every eligible launch, tests)
+  if (p.M > 512 || p.M % 8 || (p.ln_lin_out && p.syb != (long long)p.y_rows * p.syr)) return false;
+  return (long long)((p.y_rows + BN - 1) / BN) * p.B <= p.ln_cnt_n;
+}
+
 template <typename T, int WM, int NT = 4, int OCC = TTS_XRES_OCC, bool XF = false>
-static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s) {
+static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s, bool* ln_done) {
   constexpr int BM = 32 * WM, BN = 32 * NT * (4 / WM);
   const size_t lds = std::max((size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16),
                               TTS_XRES_EPI16 ? (size_t)BN * (BM * 2 + 16) : (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
   dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
-  hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM, OCC, XF>), grid, dim3(256), lds, s, p, cg);
+  ConvParams q = p;
+  if (!xres_ln_ok(q, BN)) q.ln_cnt = nullptr;  // the kernel's LayerNorm switch
+  if (ln_done) *ln_done = q.ln_cnt != nullptr;
+  hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM, OCC, XF>), grid, dim3(256), lds, s, q, cg);
   return hipGetLastError();
 }
 
 template <typename T>
-static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err) {
+static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err, bool* ln_done) {
   if (!xres_mode()) return false;
   const int wm = xres_wm(p);
   const int nt = xres_nt(p, wm);
@@ -700,18 +813,18 @@ static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err) {
   const int cg = xres_group(p, 32 * 4 * (4 / wm), big ? XRES_LDS_BIG : XRES_LDS_MAX);
   if (!cg) return false;
   if (wm == 2)
-    *err = launch_xres_wm<T, 2>(p, cg, s);
+    *err = launch_xres_wm<T, 2>(p, cg, s, ln_done);
   else if (big)
-    *err = xres_narrow(p, nt) ? launch_xres_wm<T, 2, 1, 1>(p, cg, s)
-           : nt == 2          ? launch_xres_wm<T, 4, 2, 1>(p, cg, s)
-                              : launch_xres_wm<T, 4, 4, 1>(p, cg, s);
+    *err = xres_narrow(p, nt) ? launch_xres_wm<T, 2, 1, 1>(p, cg, s, ln_done)
+           : nt == 2          ? launch_xres_wm<T, 4, 2, 1>(p, cg, s, ln_done)
+                              : launch_xres_wm<T, 4, 4, 1>(p, cg, s, ln_done);
   else if (xres_narrow(p, nt))
-    *err = launch_xres_wm<T, 2, 1>(p, cg, s);
+    *err = launch_xres_wm<T, 2, 1>(p, cg, s, ln_done);
   else if (TTS_XRES_UPFIRST && p.up_s)
-    *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, true>(p, cg, s)
-                   : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, true>(p, cg, s);
+    *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, true>(p, cg, s, ln_done)
+                   : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, true>(p, cg, s, ln_done);
   else
-    *err = nt == 2 ? launch_xres_wm<T, 4, 2>(p, cg, s) : launch_xres_wm<T, 4>(p, cg, s);
+    *err = nt == 2 ? launch_xres_wm<T, 4, 2>(p, cg, s, ln_done) : launch_xres_wm<T, 4>(p, cg, s, ln_done);
   return true;
 }
 
@@ -800,25 +913,36 @@ static hipError_t conv_gemm_launch_noln(int dtype, const ConvParams& p, hipStrea
       return launch_t<float>(p, s);
     case DT_F16: {
       hipError_t e;
-      if (launch_xres<half_t>(p, s, &e)) return e;
+      if (launch_xres<half_t>(p, s, &e, ln_done)) return e;
       return launch_t<half_t>(p, s);
     }
     case DT_BF16: {
       hipError_t e;
-      if (launch_xres<bf16_t>(p, s, &e)) return e;
+      if (launch_xres<bf16_t>(p, s, &e, ln_done)) return e;
       return launch_t<bf16_t>(p, s);
     }
   }
   return hipErrorInvalidValue;
 }
 
+static thread_local int g_conv_kernels = 0;
+int conv_last_kernels() { return g_conv_kernels; }
+
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s) {
   bool ln_done = false;
+  g_conv_kernels = 1;
   const hipError_t e = conv_gemm_launch_noln(dtype, p, s, &ln_done);
-  if (e != hipSuccess || !p.ln_out || ln_done) return e;
-  // LayerNorm as its own launch over the whole [B][y_rows] output (contiguous rows of M)
+  if (dtype == DT_F32 && conv_split_eligible(p)) g_conv_kernels = conv_split_last_kernels();
+  if (e != hipSuccess || !(p.ln_out || p.ln_lin_out) || ln_done) return e;
+  ++g_conv_kernels;
+  // LayerNorm as its own launch over the [B][y_rows] output (contiguous rows of M); rows past an
+  // utterance's length are skipped (no consumer reads them)
   if (p.syr != p.M || p.syb != (long long)p.y_rows * p.syr || p.nh != 1) return hipErrorInvalidValue;
-  return launch_layernorm(dtype, p.y, p.ln_out, p.B * p.y_rows, p.M, p.ln_g1, p.ln_b1, p.ln_g2, p.ln_b2, p.ln_eps, s);
+  if (p.ln_lin_out)
+    return launch_ln_linear1(dtype, p.y, p.B * p.y_rows, p.M, p.ln_g1, p.ln_b1, p.ln_eps, p.ln_lin_w, p.ln_lin_b,
+                             p.ln_lin_out, s);
+  return launch_layernorm(dtype, p.y, p.ln_out, p.B * p.y_rows, p.M, p.ln_g1, p.ln_b1, p.ln_g2, p.ln_b2, p.ln_eps, s,
+                          p.y_len, p.y_rows);
 }
 
 }  // namespace tts

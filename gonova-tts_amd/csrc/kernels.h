@@ -36,11 +36,22 @@ struct ConvParams {
   long long ws_bytes;
   // optional LayerNorm of the result (post-LN residual blocks, HF:551-645): ln_out[row] =
   // LN2?(LN1(y[row])) with y's strides.  The split-K fp32 path applies it in its reduce
-  // (split_reduce_ln_kernel: y is never written); every other path writes y and then runs
-  // launch_layernorm(y -> ln_out) over the B * y_rows rows.
+  // (split_reduce_ln_kernel: y is never written); with ln_cnt (below) the conv_xres and one-slice
+  // conv_splitp launches apply it in their epilogue; every other path writes y and then runs
+  // launch_layernorm(y -> ln_out) over the rows inside each utterance's length (y_len).
   void* ln_out;
   const float *ln_g1, *ln_b1, *ln_g2, *ln_b2;
   float ln_eps;
+  // Row-tile counters (ln_cnt_n ints, zero; ln_rows.h): with them the X-resident (16-bit) and
+  // packed split-precision (fp32, one K slice) kernels apply the LayerNorm in the launch itself
+  // (the last-arriving M block of each row tile normalises its rows; rows past an utterance's
+  // length are left alone).  ln_lin_out: LN(y) . ln_lin_w + ln_lin_b per row instead of ln_out
+  // (the variance predictors' LayerNorm + Linear(C -> 1)).
+  int* ln_cnt;
+  int ln_cnt_n;
+  const float* ln_lin_w;
+  float ln_lin_b;
+  float* ln_lin_out;
 };
 
 inline ConvParams conv_params_default() {
@@ -52,6 +63,8 @@ inline ConvParams conv_params_default() {
 
 int conv_gemm_check(const ConvParams& p, int dtype, const char** why);
 hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s);
+// kernels the calling thread's last conv_gemm_launch enqueued (the GEMM, a split-K reduce, a LayerNorm)
+int conv_last_kernels();
 
 // kernel family a launch runs as (live profiling buckets; tts_engine_profile_read_kinds)
 enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_RETIRED = 2 /* mrf_fused, removed */, PK_MRF_PAIR = 3, PK_MRF_CHAIN = 4, PK_UPSAMPLE = 5,
@@ -63,10 +76,9 @@ int conv_gemm_kind(int dtype, const ConvParams& p);
 // fp32 conv as three f16 MFMAs (conv_split.hip): an fp32 layer whose ConvParams::wpk is a
 // split-packed copy (frag_pack_split) runs here when eligible (Cin % 64 == 0, no head batching)
 bool conv_split_eligible(const ConvParams& p);
-// whether conv_split_launch applies p.ln_out's LayerNorm in its split-K reduce (dtype f32)
-bool conv_split_fuses_ln(const ConvParams& p);
 // *ln_done: whether the launch applied p.ln_out's LayerNorm itself (the split-K reduce)
 hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done = nullptr);
+int conv_split_last_kernels();  // kernels the calling thread's last conv_split_launch enqueued
 // split-K workspace bytes a packed-row launch of this shape over `rows` flat rows can use (0: none)
 long long conv_split_ws_bytes(int taps, int Cin, int M, int rows);
 

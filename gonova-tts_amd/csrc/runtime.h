@@ -195,7 +195,7 @@ inline ConvLayer make_conv(const std::vector<float>& w, int co, int ci, int k, c
 // Live kernel timing (bench.py roofline): hipEvents around every implicit-GEMM launch.
 struct Profiler {
   bool on = false;
-  struct Rec { hipEvent_t a, b; double flops; int kind; };
+  struct Rec { hipEvent_t a, b; double flops; int kind; int nk = 1; };  // nk: kernels between a and b
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
   hipEvent_t get() {
@@ -211,7 +211,7 @@ struct Profiler {
       HIP_CHECK(hipEventSynchronize(r.b));
       float e = 0.f;
       HIP_CHECK(hipEventElapsedTime(&e, r.a, r.b));
-      if (r.kind < nk) { ms[r.kind] += e; fl[r.kind] += r.flops; ++n[r.kind]; }
+      if (r.kind < nk) { ms[r.kind] += e; fl[r.kind] += r.flops; n[r.kind] += r.nk; }
       pool.push_back(r.a); pool.push_back(r.b);
     }
     recs.clear();
@@ -255,6 +255,7 @@ inline void launch_conv_checked(const ConvParams& p, int dt, hipStream_t s, Prof
     HIP_CHECK(hipEventRecord(r.a, s));
     HIP_CHECK(conv_gemm_launch(dt, p, s));
     HIP_CHECK(hipEventRecord(r.b, s));
+    r.nk = conv_last_kernels();
     prof->recs.push_back(r);
   } else {
     HIP_CHECK(conv_gemm_launch(dt, p, s));
@@ -281,6 +282,8 @@ inline void run_layer(const ConvLayer& L, const void* x, int x_rows, const int* 
   if (ln) {  // the LayerNorm fields of *ln (ln_out, gains, biases, eps)
     p.ln_out = ln->ln_out; p.ln_g1 = ln->ln_g1; p.ln_b1 = ln->ln_b1; p.ln_g2 = ln->ln_g2; p.ln_b2 = ln->ln_b2;
     p.ln_eps = ln->ln_eps;
+    p.ln_cnt = ln->ln_cnt; p.ln_cnt_n = ln->ln_cnt_n;
+    p.ln_lin_w = ln->ln_lin_w; p.ln_lin_b = ln->ln_lin_b; p.ln_lin_out = ln->ln_lin_out;
   }
   launch_conv_checked(p, dt, s, prof, 2.0 * L.M * (double)L.Cin * L.taps * (double)B * y_rows);
 }

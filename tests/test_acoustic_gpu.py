@@ -305,6 +305,35 @@ def test_short_row_tiles_bit_identical(aw, dtype, switch):
         check(f"acoustic {dtype} short row tiles b={b}", auto[b, :L], ref["mel"], kind="ac_" + dtype)
 
 
+@pytest.mark.parametrize("dtype,precision", [("bf16", "exact"), ("f16", "exact"), ("bf16", "fast")])
+def test_fused_layernorm_bit_identical(aw, dtype, precision, switch):
+    """The post-LNs applied inside the GEMM launches (the row tile's last M block normalises its
+    rows: conv_xres for 16-bit stacks, the one-slice split GEMM for the exact encoder and its
+    predictors, LayerNorm + Linear(C -> 1) for each predictor's last layer) give the same bits as
+    the separate LayerNorm launches (TTS_LN_FUSE=0): predicted durations, frame counts and mel,
+    on the default rule (grids of >= 512 blocks) and forced on every eligible launch (7), twice
+    each.  A ragged batch whose lengths cross 64- and 128-row tile edges, and the C3 shape."""
+    eng = engine(dtype, aw) if precision == "exact" else HipEngine(DEV, vocoder_dtype="f32", acoustic_dtype=dtype,
+                                                                    encoder_precision="fast")
+    if precision == "fast":
+        eng.load_weights(acoustic=aw)
+    rng = np.random.default_rng(41)
+    cases = [[rng.integers(1, 78, size=n) for n in (144, 1, 65, 70, 127, 129, 9, 33)],
+             [rng.integers(1, 78, size=144) for _ in range(32)]]
+    for ids_list in cases:
+        switch("TTS_LN_FUSE", 0)
+        m0, l0, d0 = run(eng, ids_list, t_cap=8 * 144)
+        for mode in (None, 7):  # default (grids of >= 512 blocks), every eligible launch
+            switch("TTS_LN_FUSE", mode)
+            for _ in range(2):  # (the hand-off must not depend on timing)
+                m1, l1, d1 = run(eng, ids_list, t_cap=8 * 144)
+                assert np.array_equal(d0, d1) and np.array_equal(l0, l1), mode
+                assert np.array_equal(m0, m1), mode
+    # (every oracle test of this file runs the fused default path)
+    if precision == "fast":
+        eng.close()
+
+
 def test_failed_reserve_leaves_a_usable_engine(aw):
     """A workspace reservation that runs out of device memory partway (advisor finding: the
     caps must never describe freed memory) raises, and the next small forward re-reserves

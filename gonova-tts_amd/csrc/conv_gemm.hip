@@ -351,7 +351,24 @@ __device__ inline void xres_tile_ln(const ConvParams& p, const T* Y, int b, int 
 // MFMA order: bit-identical.  Measured (same box, tools/ab_xres.sh): the stage 0-1 upsamplers
 // 155.5 -> 145.9 us and 316.4 -> 298.2 us; the acoustic GEMMs +2 % (their MFMA loops then wait on
 // the ring's first quads), so only the upsampler launches use it.
-template <typename T, int NT, int WM, int OCC = TTS_XRES_OCC, bool XF = false>
+// DT > 0 (conv_xres "DMA" form, WM = 4, DT taps, 64-channel groups, no input activation): the X
+// tile of channel group g + NB - 1 is copied global -> LDS by buffer_load ... lds while group g's
+// MFMAs run (NB LDS buffers; no staging registers, no staging barriers besides one per group).
+// Rows are 128 bytes with chunk c of row r at slot c ^ ((r >> 1) & 7) (the DMA's lane-linear LDS
+// image: the swizzle goes on the source address; the B-fragment reads are conflict-free for every
+// row base); rows outside the utterance read 0 through the descriptor's range.  The weight ring
+// holds one quad per tap and is refilled with the next group's quads.  Same K order as the
+// register-staged kernel at CG = 64 (the launcher uses CG = 64 for every launch of these layers):
+// bit-identical to it.
+#ifndef TTS_XDMA_NB
+#define TTS_XDMA_NB 2  // LDS buffers of the DMA form (prefetch distance NB - 1 groups)
+#endif
+// one 16-byte-per-lane buffer load straight into LDS (lane i -> lds + 16 i), no VGPR destination
+__device__ inline void lds_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+
+template <typename T, int NT, int WM, int OCC = TTS_XRES_OCC, bool XF = false, int DT = 0>
 __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int CG) {
   using MF = Mfma<T>;
   typedef typename MF::frag Frag;
@@ -436,6 +453,77 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
     }                                                                                     \
   } while (0)
 
+  if constexpr (DT > 0) {
+    static_assert(WM == 4 && DT <= 3, "DMA form: 128-channel blocks, <= 3 taps (one ring slot per tap)");
+    constexpr int RD = BN + 32;         // staged rows per group: the tile + a halo of (taps - 1) * dil <= 32
+    constexpr int NPW = RD / 32;        // 1 KiB DMA pieces (8 rows) per wave per group
+    constexpr int BUFB = RD * 128;      // bytes per LDS buffer
+    constexpr int NB = TTS_XDMA_NB;
+    static_assert(NB == 2 || NB == 3, "2 or 3 LDS buffers");
+    const int G = p.Cin / 64;
+    // rows [0, xlen) of the utterance; anything else (rows before 0: negative offsets) reads 0
+    const auto xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(X), 0, xlen * p.sxr * (int)sizeof(T), 0x00020000);
+    int voff[NPW];  // this lane's source bytes of its pieces for group 0 (group g: + 128 g)
+#pragma unroll
+    for (int q = 0; q < NPW; ++q) {
+      const int row = 8 * (wave * NPW + q) + (lane >> 3);
+      voff[q] = ((x_start + row) * p.sxr + 8 * ((lane & 7) ^ ((row >> 1) & 7))) * (int)sizeof(T);
+    }
+    // group g's X tile -> buffer g % NB; past the last group the pieces read nothing (the count of
+    // outstanding memory operations stays the same every group)
+    auto dma = [&](int g) __attribute__((always_inline)) {
+      char* dst = smem + (g % NB) * BUFB + wave * NPW * 1024;
+      const int go = g < G ? g * 64 * (int)sizeof(T) : 0x40000000;
+#pragma unroll
+      for (int q = 0; q < NPW; ++q)
+        lds_dma16(xrs, dst + q * 1024, voff[q] + go);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // weight quad of (group g, tap t): k-steps t * KST + 4 g .. + 3; nothing past the last group
+    auto loadq = [&](Frag (&a)[4], int g, int t) __attribute__((always_inline)) {
+      const int o = (t * KST + 4 * g) * 1024 + (g < G ? 0 : 0x40000000);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        a[j] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lofs + j * 1024, o, 0));
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // B-fragment byte offsets of tap t, k-step j in a buffer (tile nt: + nt * 32 rows)
+    int boff[DT][4];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const int r = l31 + t * p.dil;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) boff[t][j] = r * 128 + (((2 * j + hh) ^ ((r >> 1) & 7)) << 4);
+    }
+    Frag ra[DT][4];
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i) dma(i);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) loadq(ra[t], 0, t);
+    for (int g = 0; g < G; ++g) {
+      // group g's pieces have landed (vmcnt: all but the youngest -- the ring refills and DMAs
+      // issued after them), then every wave's
+      if (NB == 2 || g == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * NPW + 4 * DT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * NPW + 8 * DT) : "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      dma(g + NB - 1);  // into the buffer group g - 1 read (every wave is past it)
+      const char* buf = smem + (g % NB) * BUFB;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          Frag bf[NT];
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) bf[nt] = *reinterpret_cast<const Frag*>(buf + boff[t][j] + nt * 32 * 128);
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) acc[nt] = MF::mma(ra[t][j], bf[nt], acc[nt]);
+        }
+        loadq(ra[t], g + 1, t);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing pieces land before the epilogue reuses LDS
+  } else {
   // X staging: thread owns 16-byte column cc of the group and rows r0, r0 + rstep, ...
   // (CG is a power of two: no per-vector division)
   const int lvpr = __builtin_ctz(VPR);
@@ -502,6 +590,7 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
     if (q < QT) TTS_MMAQ(a0, q);
     if (q + 1 < QT) TTS_MMAQ(a1, q + 1);
   }
+  }  // register-staged form
 #undef TTS_LOADQ
 #undef TTS_MMAQ
 
@@ -704,8 +793,19 @@ constexpr int XRES_LDS_BIG = 159 * 1024;
 
 // channel group for the X-resident kernel: largest power-of-two CG | Cin, CG >= 64, tile within
 // XRES_LDS_MAX; 0 = not eligible
+// layers the DMA form of conv_xres serves (3-tap convs without an input activation: the acoustic
+// FFN convs); every launch of them, whichever kernel runs it, uses 64-channel groups (one K order)
+#ifndef TTS_XRES_DMA
+#define TTS_XRES_DMA 1
+#endif
+static bool xres_dma_layer(const ConvParams& p) {
+  return TTS_XRES_DMA && sw(SW_XRES_DMA) != 0 && p.taps == 3 && p.in_slope == 1.0f && !p.up_s && p.nh == 1 &&
+         p.Cin % 64 == 0 && 2 * p.dil <= 32 && (long long)p.x_rows * p.sxr * 2 < (1LL << 31);
+}
+
 static int xres_group(const ConvParams& p, int BN, int lds_max = XRES_LDS_MAX) {
   if (!p.wpk || p.M < 64 || p.Cin % 64 || p.M % 8 || p.nh != 1) return 0;
+  if (xres_dma_layer(p)) return 64;
   if (p.syr % 8 || p.syb % 8 || ((p.r1 || p.r2) && (p.srr % 8 || p.srb % 8))) return 0;
   if (p.up_s && p.up_cout % 8) return 0;
   const int R = BN + (p.taps - 1) * p.dil;
@@ -784,16 +884,16 @@ static bool xres_ln_ok(const ConvParams& p, int BN) {
   return (long long)((p.y_rows + BN - 1) / BN) * p.B <= p.ln_cnt_n;
 }
 
-template <typename T, int WM, int NT = 4, int OCC = TTS_XRES_OCC, bool XF = false>
+template <typename T, int WM, int NT = 4, int OCC = TTS_XRES_OCC, bool XF = false, int DT = 0>
 static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s, bool* ln_done) {
   constexpr int BM = 32 * WM, BN = 32 * NT * (4 / WM);
-  const size_t lds = std::max((size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16),
-                              TTS_XRES_EPI16 ? (size_t)BN * (BM * 2 + 16) : (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
+  const size_t xt = DT ? (size_t)TTS_XDMA_NB * (BN + 32) * 128 : (size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16);
+  const size_t lds = std::max(xt, TTS_XRES_EPI16 ? (size_t)BN * (BM * 2 + 16) : (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
   dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
   ConvParams q = p;
   if (!xres_ln_ok(q, BN)) q.ln_cnt = nullptr;  // the kernel's LayerNorm switch
   if (ln_done) *ln_done = q.ln_cnt != nullptr;
-  hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM, OCC, XF>), grid, dim3(256), lds, s, q, cg);
+  hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM, OCC, XF, DT>), grid, dim3(256), lds, s, q, cg);
   return hipGetLastError();
 }
 
@@ -820,6 +920,9 @@ static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err, boo
                               : launch_xres_wm<T, 4, 4, 1>(p, cg, s, ln_done);
   else if (xres_narrow(p, nt))
     *err = launch_xres_wm<T, 2, 1>(p, cg, s, ln_done);
+  else if (xres_dma_layer(p) && sw(SW_XRES_DMA) != 2)  // (2: the same layers, K order and bits, register-staged)
+    *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, false, 3>(p, cg, s, ln_done)
+                   : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, false, 3>(p, cg, s, ln_done);
   else if (TTS_XRES_UPFIRST && p.up_s)
     *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, true>(p, cg, s, ln_done)
                    : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, true>(p, cg, s, ln_done);

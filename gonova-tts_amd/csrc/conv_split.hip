@@ -33,6 +33,12 @@
 #ifndef TTS_LN_FUSE_MINBLK
 #define TTS_LN_FUSE_MINBLK 512  // GEMM blocks from which a launch applies its post-LN itself (same-box A/B: 0 slower at batch 8)
 #endif
+#ifndef TTS_SPLIT_PROBE
+#define TTS_SPLIT_PROBE 0  // timing-only probe builds: every weight quad read from the first (L1/L2-hot, wrong results)
+#endif
+#ifndef TTS_SPLIT_WHOLE_MAXBLK
+#define TTS_SPLIT_WHOLE_MAXBLK 256  // packed split GEMMs of at most this many blocks stage their K slice at once
+#endif
 #ifndef TTS_SPLITK_FUSE
 #define TTS_SPLITK_FUSE 0
 #endif
@@ -432,6 +438,13 @@ __device__ inline void splitk_tile_ln(const ConvParams& p, int S, int F, int f0,
   }
 }
 
+// WHOLE: every channel group of the block's K slice (at most SPK_WG) is staged at once, their X
+// loads all in flight together, into LDS regions of their own (one block per CU), and the MFMA
+// loop runs over the groups with no restaging -- for grids of at most one block per CU (the
+// batch-8 encoder), where each group's load round trip and barriers were the block's critical
+// path.  Same groups, quads and MFMA order: bit-identical to the group-by-group form.
+constexpr int SPK_WG = 3;
+template <bool WHOLE>
 __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int CG, int S, int gps) {
   typedef half8 Frag;
   constexpr int NT = SPK_NT, BN = 32 * NT;
@@ -489,18 +502,19 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
   const int r0 = tid >> lvpr;
   const int rstep = 256 >> lvpr;
   f32x4 xv[SPK_SU];
-  auto load_x = [&](int g) {
+  auto load_x_to = [&](int g, f32x4 (&xd)[SPK_SU]) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < SPK_SU; ++i) {
       const int f = x_start + min(r0 + i * rstep, R - 1);
-      xv[i] = *reinterpret_cast<const f32x4*>(X + (long long)min(max(f, 0), F - 1) * p.sxr + g + c4 * 4);
+      xd[i] = *reinterpret_cast<const f32x4*>(X + (long long)min(max(f, 0), F - 1) * p.sxr + g + c4 * 4);
     }
   };
-  auto store_x = [&]() {
+  auto load_x = [&](int g) __attribute__((always_inline)) { load_x_to(g, xv); };
+  auto store_x_from = [&](const f32x4 (&xs)[SPK_SU], char* base) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < SPK_SU; ++i) {
       const int rr = r0 + i * rstep;
-      f32x4 v = xv[i];
+      f32x4 v = xs[i];
       if (!packed_valid(p, p.x_len, x_start + rr, F)) v = f32x4{};
       if (p.in_slope != 1.0f) {
 #pragma unroll
@@ -509,11 +523,12 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
       const half4 h = __builtin_convertvector(v, half4);
       const half4 l = __builtin_convertvector((v - __builtin_convertvector(h, f32x4)) * SPLIT_SCALE, half4);
       if (rr < R) {
-        *reinterpret_cast<uint2*>(smem + rr * RS + c4 * 8) = __builtin_bit_cast(uint2, h);
-        *reinterpret_cast<uint2*>(smem + PL + rr * RS + c4 * 8) = __builtin_bit_cast(uint2, l);
+        *reinterpret_cast<uint2*>(base + rr * RS + c4 * 8) = __builtin_bit_cast(uint2, h);
+        *reinterpret_cast<uint2*>(base + PL + rr * RS + c4 * 8) = __builtin_bit_cast(uint2, l);
       }
     }
   };
+  auto store_x = [&]() __attribute__((always_inline)) { store_x_from(xv, smem); };
 
   const int gbeg = sl * gps * CG, gend = min(p.Cin, (sl + 1) * gps * CG);
   // Weight quads form one ring over the slice: the two quads past a group's last are the next
@@ -526,7 +541,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
       const int nx_ = (QQ_) >= QT;                                                                   \
       const int kq_ = 4 * ((QQ_) - nx_ * QT);                                                        \
       const int gg_ = g0 + nx_ * CG;                                                                 \
-      const int o_ = (((kq_ >> lks) * KST + gg_ / 16 + (kq_ & (KS - 1))) * 1024) +                   \
+      const int o_ = TTS_SPLIT_PROBE ? 0 : (((kq_ >> lks) * KST + gg_ / 16 + (kq_ & (KS - 1))) * 1024) + \
                      (gg_ < gend ? 0 : 0x40000000);                                                  \
       _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                             \
         A_[j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_hi, lofs + j_ * 1024, o_, 0)); \
@@ -537,7 +552,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
 #define TTS_SPLIT_MMAQ(A_, QQ_)                                                                      \
     do {                                                                                             \
       const int kq_ = 4 * (QQ_);                                                                     \
-      const char* bq_ = xl + (kq_ >> lks) * p.dil * RS + (kq_ & (KS - 1)) * 32;                      \
+      const char* bq_ = xg + (kq_ >> lks) * p.dil * RS + (kq_ & (KS - 1)) * 32;                      \
       _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                             \
         _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_) {                                       \
           const Frag bh_ = *reinterpret_cast<const Frag*>(bq_ + nt_ * 32 * RS + j_ * 32);            \
@@ -550,14 +565,26 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     } while (0)
   TTS_SPLIT_LOADQ(a0, 0);
   TTS_SPLIT_LOADQ(a1, 1);
-  load_x(gbeg);
-  store_x();
+  const char* xg = xl;  // the current group's LDS tile
+  if constexpr (WHOLE) {
+    // every group's X loads in flight at once, then split into the groups' own LDS regions
+    f32x4 xw[SPK_WG][SPK_SU];
+    const int ng = (gend - gbeg) / CG;  // <= SPK_WG (launcher)
+#pragma unroll
+    for (int i = 0; i < SPK_WG; ++i) load_x_to(gbeg + min(i, ng - 1) * CG, xw[i]);
+#pragma unroll
+    for (int i = 0; i < SPK_WG; ++i)
+      if (i < ng) store_x_from(xw[i], smem + i * 2 * PL);
+  } else {
+    load_x(gbeg);
+    store_x();
+  }
   __syncthreads();
   for (; g0 < gend; g0 += CG) {
     const bool more = g0 + CG < gend;
     TTS_SPLIT_MMAQ(a0, 0);
     TTS_SPLIT_LOADQ(a0, 2);
-    load_x(more ? g0 + CG : g0);  // unconditional (a load under a branch is waited on at once)
+    if constexpr (!WHOLE) load_x(more ? g0 + CG : g0);  // unconditional (a load under a branch is waited on at once)
     TTS_SPLIT_MMAQ(a1, 1);
     TTS_SPLIT_LOADQ(a1, 3);
     for (int q = 2; q < QT; q += 2) {
@@ -568,12 +595,15 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     }
 #undef TTS_SPLIT_LOADQ
 #undef TTS_SPLIT_MMAQ
-    if (more) {
+    if constexpr (WHOLE) {
+      xg += 2 * PL;  // the next group's region
+    } else if (more) {
       __syncthreads();  // every wave is done with this group's tile
       store_x();
       __syncthreads();
     }
   }
+  if constexpr (WHOLE) __syncthreads();  // (the epilogue reuses LDS: every wave is past its MFMAs)
 
   const int m_w0 = (by * 4 + wave) * 32;
   if (S == 1) {
@@ -828,6 +858,12 @@ hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done) 
       const int nwg = (F + 32 * SPK_NT - 1) / (32 * SPK_NT) * ((p.M + 127) / 128) * S;
       const size_t lds = std::max((size_t)2 * (32 * SPK_NT + (p.taps - 1) * p.dil) * (cg * 2 + 16),
                                   (size_t)32 * SPK_NT * (128 * 4 + 16));  // X planes / epilogue tile
+      // one block per CU or fewer: stage the K slice's groups at once (no restaging; bit-identical)
+      const int ngs = gps;  // groups per slice
+      const bool whole = sw(SW_SPLIT_WHOLE) != 0 && ngs <= SPK_WG && nwg <= TTS_SPLIT_WHOLE_MAXBLK;
+      const size_t ldsw = whole ? std::max((size_t)ngs * 2 * (32 * SPK_NT + (p.taps - 1) * p.dil) * (cg * 2 + 16),
+                                           (size_t)32 * SPK_NT * (128 * 4 + 16))
+                                : lds;
       ConvParams q = p;
       // the kernel's LayerNorm switch: its epilogue (one slice) or its in-launch split-K reduce
       // (the in-launch split-K reduce, TTS_SPLITK_FUSE=1, is off by default: its results varied between
@@ -835,7 +871,10 @@ hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done) 
       bool fuse = splitp_ln_ok(p, F) && (S == 1 || (TTS_SPLITK_FUSE && p.ln_out && p.act_out == ACT_NONE && S <= SKMAX));
       if (sw(SW_LN_FUSE) > 1 && sw(SW_LN_FUSE) != 7 && sw(SW_LN_FUSE) != (S == 1 ? 3 : 4)) fuse = false;  // (bisection: 3 / 4 = one slice / split-K only)
       if (!fuse) q.ln_cnt = nullptr;
-      hipLaunchKernelGGL(conv_splitp_kernel, dim3(nwg), dim3(256), lds, s, q, cg, S, gps);
+      if (whole && ldsw <= 160 * 1024)
+        hipLaunchKernelGGL(conv_splitp_kernel<true>, dim3(nwg), dim3(256), ldsw, s, q, cg, S, gps);
+      else
+        hipLaunchKernelGGL(conv_splitp_kernel<false>, dim3(nwg), dim3(256), lds, s, q, cg, S, gps);
       if (q.ln_cnt) {
         if (ln_done) *ln_done = true;
         return hipGetLastError();

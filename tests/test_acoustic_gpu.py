@@ -363,6 +363,23 @@ def test_dma_staged_ffn_bit_identical(aw, dtype, switch):
         check(f"acoustic {dtype} DMA-staged FFN b={b}", forced[b, :L], ref["mel"], kind="ac_" + dtype)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_split_whole_slice_staging_bit_identical(aw, dtype, switch):
+    """Small split-precision GEMM grids (at most one block per CU: the batch-8 exact encoder and
+    predictors) stage every channel group of their K slice at once; the quads and their MFMA order
+    are those of the group-by-group form (TTS_SPLIT_WHOLE=0), so durations and mel match bit for
+    bit on a ragged batch-8 forward with predicted durations."""
+    eng = engine(dtype, aw)
+    rng = np.random.default_rng(44)
+    ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70, 127, 129, 9, 33)]
+    switch("TTS_SPLIT_WHOLE", 0)
+    m0, l0, d0 = run(eng, ids_list, t_cap=8 * 144)
+    switch("TTS_SPLIT_WHOLE", None)
+    m1, l1, d1 = run(eng, ids_list, t_cap=8 * 144)
+    assert np.array_equal(d0, d1) and np.array_equal(l0, l1)
+    assert np.array_equal(m0, m1)
+
+
 def test_failed_reserve_leaves_a_usable_engine(aw):
     """A workspace reservation that runs out of device memory partway (advisor finding: the
     caps must never describe freed memory) raises, and the next small forward re-reserves

@@ -793,14 +793,19 @@ constexpr int XRES_LDS_BIG = 159 * 1024;
 
 // channel group for the X-resident kernel: largest power-of-two CG | Cin, CG >= 64, tile within
 // XRES_LDS_MAX; 0 = not eligible
-// layers the DMA form of conv_xres serves (3-tap convs without an input activation: the acoustic
-// FFN convs); every launch of them, whichever kernel runs it, uses 64-channel groups (one K order)
+// layers the DMA form of conv_xres serves (2- and 3-tap convs: the acoustic FFN convs, the vocoder's
+// stage 0-1 upsamplers); every launch of them, whichever kernel runs it, uses 64-channel groups
+// (one K order: bit-identical across kernels, batch sizes and tile shapes)
 #ifndef TTS_XRES_DMA
 #define TTS_XRES_DMA 1
 #endif
 static bool xres_dma_layer(const ConvParams& p) {
-  return TTS_XRES_DMA && sw(SW_XRES_DMA) != 0 && p.taps == 3 && p.in_slope == 1.0f && !p.up_s && p.nh == 1 &&
-         p.Cin % 64 == 0 && 2 * p.dil <= 32 && (long long)p.x_rows * p.sxr * 2 < (1LL << 31);
+  return TTS_XRES_DMA && sw(SW_XRES_DMA) != 0 && (p.taps == 2 || p.taps == 3) && p.nh == 1 && p.Cin % 64 == 0 &&
+         (p.taps - 1) * p.dil <= 32 && (long long)p.x_rows * p.sxr * 2 < (1LL << 31);
+}
+// ... of which the DMA form runs the ones with no input activation (the DMA copies X as it is)
+static int xres_dma_taps(const ConvParams& p) {
+  return xres_dma_layer(p) && p.in_slope == 1.0f && sw(SW_XRES_DMA) != 2 ? p.taps : 0;
 }
 
 static int xres_group(const ConvParams& p, int BN, int lds_max = XRES_LDS_MAX) {
@@ -920,9 +925,12 @@ static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err, boo
                               : launch_xres_wm<T, 4, 4, 1>(p, cg, s, ln_done);
   else if (xres_narrow(p, nt))
     *err = launch_xres_wm<T, 2, 1>(p, cg, s, ln_done);
-  else if (xres_dma_layer(p) && sw(SW_XRES_DMA) != 2)  // (2: the same layers, K order and bits, register-staged)
+  else if (xres_dma_taps(p) == 3)  // (TTS_XRES_DMA=2: the same layers, K order and bits, register-staged)
     *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, false, 3>(p, cg, s, ln_done)
                    : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, false, 3>(p, cg, s, ln_done);
+  else if (xres_dma_taps(p) == 2)  // the polyphase upsamplers (k = 2 s): 2 taps
+    *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, false, 2>(p, cg, s, ln_done)
+                   : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, false, 2>(p, cg, s, ln_done);
   else if (TTS_XRES_UPFIRST && p.up_s)
     *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, true>(p, cg, s, ln_done)
                    : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, true>(p, cg, s, ln_done);

@@ -306,8 +306,9 @@ struct tts_engine {
   void run_conv(const ConvLayer& L, const void* x, long long sxb, int sxr, const int* x_len, int x_rows,
                 void* y, long long syb, int syr, const int* y_len, int y_rows, float in_slope,
                 const void* r1, const void* r2, long long srb, int srr, float out_scale, int B,
-                const int* up_len, int dt, hipStream_t s) {
+                const int* up_len, int dt, hipStream_t s, int act_out = ACT_NONE, float out_slope = 0.f) {
     ConvParams p = conv_params_default();
+    p.act_out = act_out; p.out_slope = out_slope;
     p.x = x; p.sxb = sxb; p.sxr = sxr; p.x_len = x_len; p.x_rows = x_rows;
     p.w = L.w; p.w_ld = L.taps * L.Cin; p.wpk = L.wpk;
     p.bias = L.bias;
@@ -353,12 +354,17 @@ struct tts_engine {
     void* HA = vbuf[2];
     void* HB = vbuf[3];
     void* S = vbuf[4];
-    // conv_pre: [B][T][80] -> S [B][T][512]
+    // conv_pre: [B][T][80] -> S [B][T][512], stored as lrelu(x, 0.1) -- the activation the first
+    // upsampler applies (HF:1455-1458), in the conv's fp32 epilogue: S feeds nothing else
     const int c0 = v.conv_pre.M;
-    run_conv(v.conv_pre, vmel, (long long)T * cin0, cin0, Lp(0), T, S, (long long)T * c0, c0, Lp(0), T, 1.f,
-             nullptr, nullptr, 0, 0, 1.f, B, nullptr, dt, s);
-    int Tin = T, cin = c0;
     const float slope = 0.1f;
+    run_conv(v.conv_pre, vmel, (long long)T * cin0, cin0, Lp(0), T, S, (long long)T * c0, c0, Lp(0), T, 1.f,
+             nullptr, nullptr, 0, 0, 1.f, B, nullptr, dt, s, ACT_LRELU, slope);
+    int Tin = T, cin = c0;
+    // whether S already holds lrelu(S) for the next upsampler (conv_pre, or a stage whose final MRF
+    // sum came from a pair launch that applied it, MrfPairParams::out_act); the upsampler then
+    // loads it as is, so the X-resident upsamplers can stage it by LDS-DMA
+    bool s_act = true;
     bool post_done = false;  // conv_post ran inside the last pair launch
     for (int i = 0; i < nst; ++i) {
       const int ch = v.stage_ch[i];
@@ -370,7 +376,7 @@ struct tts_engine {
         UpsampleParams up{};
         up.x = S; up.sxb = (long long)Tin * cin; up.len = Lp(i); up.up_len = Lp(i + 1);
         up.wpk = U.wup16; up.bias = U.bias; up.y = XS; up.syb = sb;
-        up.T = Tin; up.B = B; up.s = U.up_s; up.co = U.up_cout; up.pad = U.up_p; up.slope = slope;
+        up.T = Tin; up.B = B; up.s = U.up_s; up.co = U.up_cout; up.pad = U.up_p; up.slope = s_act ? 1.f : slope;
         const double fl = 2.0 * U.M * (double)U.Cin * U.taps * (double)B * Tin;
         if (prof.on) {
           Profiler::Rec r{prof.get(), prof.get(), fl, PK_UPSAMPLE};
@@ -382,9 +388,10 @@ struct tts_engine {
           HIP_CHECK(upsample_stream_launch(dt, U.Cin, U.M, up, s));
         }
       } else {
-        run_conv(U, S, (long long)Tin * cin, cin, Lp(i), Tin, XS, sb, ch, Up(i), Tin + 1, slope, nullptr, nullptr,
-                 0, 0, 1.f, B, Lp(i + 1), dt, s);
+        run_conv(U, S, (long long)Tin * cin, cin, Lp(i), Tin, XS, sb, ch, Up(i), Tin + 1, s_act ? 1.f : slope, nullptr,
+                 nullptr, 0, 0, 1.f, B, Lp(i + 1), dt, s);
       }
+      s_act = false;  // until this stage's final MRF sum says otherwise
       const int nk = (int)v.mrf[i].size();
       // resblock j as single convs: lrelu(h) -> T1 -> conv2 + h (the last one accumulates into S)
       auto convs_resblock = [&](int j) {
@@ -470,6 +477,11 @@ struct tts_engine {
             // C = 32 pairs without conv_post: the software-pipelined kernel (bit-identical)
             const int spsw = sw(SW_PAIR_SP);
             const bool sp = !pp.post_wpk && (spsw < 0 ? TTS_PAIR_SP_DEFAULT : spsw) != 0 && mrf_pair_sp_supported(dt, ch, pp.k);
+            // the stage's final MRF sum feeds only the next upsampler: store it activated
+            if (last && j == nk - 1 && i + 1 < nst && !pp.post_wpk && !sp && mrf_pair_outact_supported(dt, ch, pp.k)) {
+              pp.out_act = 1; pp.out_slope = slope;
+              s_act = true;
+            }
             auto launch = [&] { return sp ? mrf_pair_sp_launch(dt, ch, pp, s) : mrf_pair_launch(dt, ch, pp, s); };
             if (prof.on) {
               Profiler::Rec r{prof.get(), prof.get(), fl, PK_MRF_PAIR};

@@ -103,8 +103,13 @@ struct MrfPairParams {
   int post_k;
   float* wav;
   long long swb;
+  // out_act: the stored rows are LeakyReLU(out_slope) of h' / S (rounded to T first) -- the
+  // activation the next upsampler would apply on load, so a stage's last pair hands it lrelu(S)
+  int out_act;
+  float out_slope;
 };
 bool mrf_pair_supported(int dtype, int C, int k);
+bool mrf_pair_outact_supported(int dtype, int C, int k);  // the launch can carry out_act
 
 // Streaming ConvTranspose1d with two taps (k = 2s) for the small upsamplers (upsample.hip):
 // x [B][T][Cin] (len[b] valid rows) -> y [B][T*s][Co], rows s*u + r - pad for u = 0 .. len,

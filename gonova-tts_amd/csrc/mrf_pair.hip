@@ -118,7 +118,9 @@ static size_t pair_lds_bytes(int k, int d, bool post) {
   return std::max(std::max(g, t), (size_t)16 * nt2 * (C * 2 + 16));
 }
 
-template <typename T, int C, int K, bool POST = false, int DIV = 1>
+// OUTACT: the stored rows are LeakyReLU(p.out_slope) of the row pass's values (a stage's last
+// pair, whose MRF sum only the next upsampler reads; MrfPairParams::out_act)
+template <typename T, int C, int K, bool POST = false, int DIV = 1, bool OUTACT = false>
 __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom<C>::OCC)) void mrf_pair_kernel(
     MrfPairParams p) {
   using G = PairGeomS<C, DIV, K, POST>;
@@ -369,7 +371,9 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
     if ((BO * VPR % NTHR != 0 && idx >= BO * VPR) || gr >= len) continue;
     T* dst = Y + (long long)gr * C + c8 * 8;
     const uint4 y = *reinterpret_cast<const uint4*>(smem + o * YS16 + c8 * 16);
-    store16<TTS_ROW_STORE>(Y, (int)((dst - Y) * (long long)sizeof(T)), epi_row<T>(y, xin[it], p.accum, sin[it], p.scale));
+    uint4 v = epi_row<T>(y, xin[it], p.accum, sin[it], p.scale);
+    if constexpr (OUTACT) v = lrelu_unit<T>(v, p.out_slope);
+    store16<TTS_ROW_STORE>(Y, (int)((dst - Y) * (long long)sizeof(T)), v);
   }
 }
 
@@ -392,12 +396,23 @@ static int pair_div(int C, const MrfPairParams& p, bool post) {
   return (long long)((p.T + bn - 1) / bn) * p.B < TTS_PAIR_SHORT ? TTS_PAIR_SHORT_DIV : 1;
 }
 
+// output activation compiled for the stage-final pairs of HiFi-GAN V1 (k = 11 at C = 64 .. 256)
+template <int C, int K>
+constexpr bool pair_outact_compiled() { return K == 11 && (C == 64 || C == 128 || C == 256); }
+
 template <typename T, int C, int K, bool POST, int DIV>
 static hipError_t launch_pair_g(const MrfPairParams& p, hipStream_t s) {
   using G = PairGeomS<C, DIV, K, POST>;
   const size_t lds = pair_lds_bytes<C, DIV, K, POST>(K, p.d, POST);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   dim3 grid(xcd_grid((p.T + G::BN - 1) / G::BN, p.B));
+  if constexpr (!POST && pair_outact_compiled<C, K>()) {
+    if (p.out_act) {
+      hipLaunchKernelGGL((mrf_pair_kernel<T, C, K, POST, DIV, true>), grid, dim3(64 * G::WM * G::WN), lds, s, p);
+      return hipGetLastError();
+    }
+  }
+  if (p.out_act) return hipErrorInvalidValue;
   hipLaunchKernelGGL((mrf_pair_kernel<T, C, K, POST, DIV>), grid, dim3(64 * G::WM * G::WN), lds, s, p);
   return hipGetLastError();
 }
@@ -431,6 +446,10 @@ bool mrf_pair_supported(int dtype, int C, int k) {
          (k == 3 || k == 5 || k == 7 || k == 11);
 }
 
+bool mrf_pair_outact_supported(int dtype, int C, int k) {
+  return mrf_pair_supported(dtype, C, k) && k == 11 && (C == 64 || C == 128 || C == 256);
+}
+
 bool mrf_pair_post_supported(int dtype, int C, int post_k) {
   return (dtype == DT_F16 || dtype == DT_BF16) && C == 32 && post_k >= 1 && post_k % 2 == 1 &&
          post_k <= 2 * PAIR_PO + 1;
@@ -439,6 +458,7 @@ bool mrf_pair_post_supported(int dtype, int C, int post_k) {
 hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s) {
   if (!mrf_pair_supported(dtype, C, p.k) || p.d < 1) return hipErrorInvalidValue;
   if (!(p.slope >= 0.f && p.slope <= 1.f)) return hipErrorInvalidValue;  // lrelu_unit / epi_conv1
+  if (p.out_act && (!(p.out_slope >= 0.f && p.out_slope <= 1.f) || p.post_wpk)) return hipErrorInvalidValue;
   if (p.post_wpk && !(p.post_slope >= 0.f && p.post_slope <= 1.f)) return hipErrorInvalidValue;
   if (p.post_wpk) {
     if (!mrf_pair_post_supported(dtype, C, p.post_k) || !p.wav) return hipErrorInvalidValue;

@@ -281,6 +281,7 @@ bool mrf_pair_sp_supported(int dtype, int C, int k) {
 }
 
 hipError_t mrf_pair_sp_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s) {
+  if (p.out_act) return hipErrorInvalidValue;  // (no output activation in the pipelined form)
   if (!mrf_pair_sp_supported(dtype, C, p.k) || p.d < 1 || p.post_wpk) return hipErrorInvalidValue;
   if (!(p.slope >= 0.f && p.slope <= 1.f)) return hipErrorInvalidValue;  // lrelu_unit / epi_conv1
   const bool f16 = dtype == DT_F16;

@@ -22,7 +22,7 @@ enum Sw : int {
   SW_ATTN_KSPLIT,  // TTS_ATTN_KSPLIT=1: 16-bit attention with two key groups per block (8 waves)
   SW_PAIR_SP,      // TTS_PAIR_SP=0: C = 32 pairs on mrf_pair_kernel instead of the pipelined mrf_pair_sp_kernel
   SW_SPLIT_WHOLE,  // TTS_SPLIT_WHOLE=0: small split-precision GEMMs stage one channel group at a time
-  SW_XRES_DMA,     // TTS_XRES_DMA=0: acoustic FFN convs register-staged with round-2 channel groups; 2: register-staged, same bits
+  SW_XRES_DMA,     // TTS_XRES_DMA=0: FFN convs / upsamplers register-staged with round-2 channel groups; 2: register-staged, same bits
   SW_LN_FUSE,      // TTS_LN_FUSE=0: acoustic post-LNs as their own launches; 7: in every eligible GEMM launch (2-6: bisection)
   SW_N
 };

@@ -363,6 +363,10 @@ __device__ inline void xres_tile_ln(const ConvParams& p, const T* Y, int b, int 
 #ifndef TTS_XDMA_NB
 #define TTS_XDMA_NB 2  // LDS buffers of the DMA form (prefetch distance NB - 1 groups)
 #endif
+// DMA form geometry: LDS buffers (1-tap: 3, prefetch two groups ahead -- a group is a third of
+// the MFMA work of a 3-tap one) and staged rows per buffer (multi-tap: a 32-row halo)
+template <int DT> constexpr int xdma_nb() { return DT == 1 ? 3 : TTS_XDMA_NB; }
+template <int DT, int BN> constexpr int xdma_rows() { return BN + (DT > 1 ? 32 : 0); }
 // one 16-byte-per-lane buffer load straight into LDS (lane i -> lds + 16 i), no VGPR destination
 __device__ inline void lds_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
@@ -455,11 +459,18 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
 
   if constexpr (DT > 0) {
     static_assert(WM == 4 && DT <= 3, "DMA form: 128-channel blocks, <= 3 taps (one ring slot per tap)");
-    constexpr int RD = BN + 32;         // staged rows per group: the tile + a halo of (taps - 1) * dil <= 32
+    constexpr int RD = xdma_rows<DT, BN>();  // staged rows per group: the tile + a halo of (taps - 1) * dil <= 32
     constexpr int NPW = RD / 32;        // 1 KiB DMA pieces (8 rows) per wave per group
     constexpr int BUFB = RD * 128;      // bytes per LDS buffer
-    constexpr int NB = TTS_XDMA_NB;
+    constexpr int NB = xdma_nb<DT>();
+    constexpr int RSL = DT == 1 ? 2 : 1;  // weight ring depth in groups (one quad per tap and group)
+    constexpr int Q = 4 * DT;           // weight loads per group
     static_assert(NB == 2 || NB == 3, "2 or 3 LDS buffers");
+    // outstanding memory operations younger than group g's pieces at its wait: the DMAs of groups
+    // g + 1 .. g + NB - 2 and the ring loads issued after it -- RSL groups' at g = 0, then
+    // min(RSL + g, NB - 1) groups' (the smaller count of the two cases: waiting for more is safe)
+    constexpr int W0 = (NB - 2) * NPW + RSL * Q;
+    constexpr int W1 = (NB - 2) * NPW + (RSL + 1 < NB - 1 ? RSL + 1 : NB - 1) * Q;
     const int G = p.Cin / 64;
     // rows [0, xlen) of the utterance; anything else (rows before 0: negative offsets) reads 0
     const auto xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(X), 0, xlen * p.sxr * (int)sizeof(T), 0x00020000);
@@ -495,19 +506,22 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
 #pragma unroll
       for (int j = 0; j < 4; ++j) boff[t][j] = r * 128 + (((2 * j + hh) ^ ((r >> 1) & 7)) << 4);
     }
-    Frag ra[DT][4];
+    Frag ra[RSL][DT][4];
 #pragma unroll
     for (int i = 0; i < NB - 1; ++i) dma(i);
 #pragma unroll
-    for (int t = 0; t < DT; ++t) loadq(ra[t], 0, t);
-    for (int g = 0; g < G; ++g) {
-      // group g's pieces have landed (vmcnt: all but the youngest -- the ring refills and DMAs
-      // issued after them), then every wave's
-      if (NB == 2 || g == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * NPW + 4 * DT) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * NPW + 8 * DT) : "memory");
+    for (int s = 0; s < RSL; ++s)
+#pragma unroll
+      for (int t = 0; t < DT; ++t) loadq(ra[s][t], s, t);
+    // one group: its pieces have landed (vmcnt: all but the youngest), then every wave's; the
+    // next DMA goes into the buffer group g - 1 read (every wave is past it); the ring slot is
+    // refilled with group g + RSL's quads
+    auto group = [&](int g, Frag (&rs)[DT][4]) __attribute__((always_inline)) {
+      if (g == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W0) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W1) : "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      dma(g + NB - 1);  // into the buffer group g - 1 read (every wave is past it)
+      dma(g + NB - 1);
       const char* buf = smem + (g % NB) * BUFB;
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
@@ -517,10 +531,15 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) bf[nt] = *reinterpret_cast<const Frag*>(buf + boff[t][j] + nt * 32 * 128);
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[nt] = MF::mma(ra[t][j], bf[nt], acc[nt]);
+          for (int nt = 0; nt < NT; ++nt) acc[nt] = MF::mma(rs[t][j], bf[nt], acc[nt]);
         }
-        loadq(ra[t], g + 1, t);
+        loadq(rs[t], g + RSL, t);
       }
+    };
+    for (int g = 0; g < G; g += RSL) {
+      group(g, ra[0]);
+      if constexpr (RSL > 1)
+        if (g + 1 < G) group(g + 1, ra[1]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing pieces land before the epilogue reuses LDS
   } else {
@@ -808,6 +827,16 @@ static int xres_dma_taps(const ConvParams& p) {
   return xres_dma_layer(p) && p.in_slope == 1.0f && sw(SW_XRES_DMA) != 2 ? p.taps : 0;
 }
 
+// ... and the 1-tap convs (the acoustic projections: Q/K/V, attention output, pointwise convs) with
+// no input activation: with one tap the K order is the k-steps' own for every channel group, so
+// the DMA form is bit-identical to the register-staged kernel at the group that one would use
+// (TTS_XRES_DMA=3: multi-tap layers only)
+static bool xres_dma1(const ConvParams& p) {
+  return TTS_XRES_DMA && sw(SW_XRES_DMA) != 0 && sw(SW_XRES_DMA) != 2 && sw(SW_XRES_DMA) != 3 && p.taps == 1 &&
+         p.nh == 1 && p.Cin % 64 == 0 && p.in_slope == 1.0f && p.sxr % 8 == 0 && p.sxb % 8 == 0 &&
+         (long long)p.x_rows * p.sxr * 2 < (1LL << 31);
+}
+
 static int xres_group(const ConvParams& p, int BN, int lds_max = XRES_LDS_MAX) {
   if (!p.wpk || p.M < 64 || p.Cin % 64 || p.M % 8 || p.nh != 1) return 0;
   if (xres_dma_layer(p)) return 64;
@@ -892,7 +921,7 @@ static bool xres_ln_ok(const ConvParams& p, int BN) {
 template <typename T, int WM, int NT = 4, int OCC = TTS_XRES_OCC, bool XF = false, int DT = 0>
 static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s, bool* ln_done) {
   constexpr int BM = 32 * WM, BN = 32 * NT * (4 / WM);
-  const size_t xt = DT ? (size_t)TTS_XDMA_NB * (BN + 32) * 128 : (size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16);
+  const size_t xt = DT ? (size_t)xdma_nb<DT>() * xdma_rows<DT, BN>() * 128 : (size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16);
   const size_t lds = std::max(xt, TTS_XRES_EPI16 ? (size_t)BN * (BM * 2 + 16) : (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
   dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
   ConvParams q = p;
@@ -931,6 +960,9 @@ static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err, boo
   else if (xres_dma_taps(p) == 2)  // the polyphase upsamplers (k = 2 s): 2 taps
     *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, false, 2>(p, cg, s, ln_done)
                    : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, false, 2>(p, cg, s, ln_done);
+  else if (xres_dma1(p))
+    *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, false, 1>(p, cg, s, ln_done)
+                   : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, false, 1>(p, cg, s, ln_done);
   else if (TTS_XRES_UPFIRST && p.up_s)
     *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, true>(p, cg, s, ln_done)
                    : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, true>(p, cg, s, ln_done);

@@ -336,21 +336,24 @@ def test_fused_layernorm_bit_identical(aw, dtype, precision, switch):
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_dma_staged_ffn_bit_identical(aw, dtype, switch):
-    """The FFN convs' LDS-DMA form of conv_xres (X tiles copied global -> LDS a channel group ahead,
-    swizzled 128-byte rows) gives the register-staged kernel's bits at the same 64-channel groups
-    (TTS_XRES_DMA=2), at both tile heights, on a ragged batch with predicted durations; and the
-    mel stays within the oracle tolerance."""
+    """The LDS-DMA form of conv_xres (X tiles copied global -> LDS one or two channel groups ahead,
+    swizzled 128-byte rows) for the FFN convs and the 1-tap projections gives the register-staged
+    kernel's bits (TTS_XRES_DMA=2; =3: the 1-tap projections register-staged), at both tile
+    heights, on a ragged batch with predicted durations (narrow tiles off, so every eligible launch
+    takes the 128-channel kernel); and the mel stays within the oracle tolerance."""
     eng = engine(dtype, aw)
     rng = np.random.default_rng(43)
     ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70, 127, 129, 9, 33)]
     outs = {}
-    for dma in (None, 2):
+    switch("TTS_XRES_NARROW", 0)
+    for dma in (None, 3, 2):
         for nt in (2, 4):
             switch("TTS_XRES_DMA", dma)
             switch("TTS_XRES_NT", nt)
             outs[(dma, nt)] = run(eng, ids_list, t_cap=8 * 144)
     switch("TTS_XRES_NT", None)
     switch("TTS_XRES_DMA", None)
+    switch("TTS_XRES_NARROW", None)
     ref_m, ref_l, ref_d = outs[(2, 4)]
     for k, (m, l, d) in outs.items():
         assert np.array_equal(d, ref_d) and np.array_equal(l, ref_l), k

@@ -66,6 +66,10 @@ __device__ inline void ln_batch(float (&v)[RB][PER], const bool (&on)[PER], int 
       for (int i = 0; i < PER; ++i)
         if (on[i]) {
           float y = fmaf((v[r][i] - mu[r]) * rstd[r], g[pass][i], bb[pass][i]);
+          // the fp32 result is what gets rounded to T: without this the compiler may fold the
+          // multiply-add and the rounding into one v_fma_mix (a single rounding to f16 -- other
+          // bits than fp32-then-f16), and does so in some instances only
+          asm volatile("" : "+v"(y));
           if (LN2 && pass == 0) y = to_f32(from_f32<T>(y));  // first LN output is materialised in T
           v[r][i] = y;
         }
@@ -83,6 +87,25 @@ __device__ inline void ln_params(float (&g)[2][PER], float (&bb)[2][PER], const 
     g[1][i] = on[i] && g2 ? g2[ch[i]] : 0.f;
     bb[1][i] = on[i] && g2 ? b2[ch[i]] : 0.f;
   }
+}
+
+// the same for a lane owning the contiguous channels c0 .. c0 + 7 (ln_lanes8), 16-byte-aligned
+// arrays: two 16-byte loads per array instead of eight 4-byte ones
+__device__ inline void ln_load8v(float (&d)[8], bool on, const float* src, int c0) {
+  float4 x = float4{0.f, 0.f, 0.f, 0.f}, y = x;
+  if (on && src) {
+    x = *reinterpret_cast<const float4*>(src + c0);
+    y = *reinterpret_cast<const float4*>(src + c0 + 4);
+  }
+  d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
+  d[4] = y.x; d[5] = y.y; d[6] = y.z; d[7] = y.w;
+}
+__device__ inline void ln_params8v(float (&g)[2][8], float (&bb)[2][8], bool on, int c0, const float* g1,
+                                   const float* b1, const float* g2, const float* b2) {
+  ln_load8v(g[0], on, g1, c0);
+  ln_load8v(bb[0], on, b1, c0);
+  ln_load8v(g[1], on, g2, c0);
+  ln_load8v(bb[1], on, b2, c0);
 }
 
 // LayerNorm + Linear(C -> 1) of RB rows (the variance predictors' last layer, HF:176-181): the LN
@@ -120,7 +143,9 @@ __device__ inline void ln_linear1_batch(float (&v)[RB][PER], const bool (&on)[PE
 #pragma unroll
     for (int i = 0; i < PER; ++i)
       if (on[i]) {
-        const float y = to_f32(from_f32<T>(fmaf((v[r][i] - mu[r]) * rstd[r], g[i], bb[i])));
+        float y = fmaf((v[r][i] - mu[r]) * rstd[r], g[i], bb[i]);
+        asm volatile("" : "+v"(y));  // rounded from fp32 (see ln_batch)
+        y = to_f32(from_f32<T>(y));
         dot = fmaf(y, w[i], dot);
       }
     out[r] = dot;

@@ -33,6 +33,9 @@
 #ifndef TTS_LN_FUSE_MINBLK
 #define TTS_LN_FUSE_MINBLK 512  // GEMM blocks from which a launch applies its post-LN itself (same-box A/B: 0 slower at batch 8)
 #endif
+#ifndef TTS_SPLIT_STAMP
+#define TTS_SPLIT_STAMP 0  // diagnostic builds: per-block phase timestamps of one launch shape (tools/xres_stamps.py)
+#endif
 #ifndef TTS_SPLIT_PROBE
 #define TTS_SPLIT_PROBE 0  // timing-only probe builds: every weight quad read from the first (L1/L2-hot, wrong results)
 #endif
@@ -286,6 +289,8 @@ __device__ inline void splitp_tile_ln(const ConvParams& p, int f0, int BN, int F
   ln_params<8>(g, bb, ch, on, p.ln_g1, p.ln_b1, p.ln_g2, p.ln_b2);
 #pragma unroll
   for (int i = 0; i < 8; ++i) wl[i] = on[i] && p.ln_lin_w ? p.ln_lin_w[ch[i]] : 0.f;
+  const auto ylrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.y_len ? p.y_len : reinterpret_cast<const int*>(p.y)),
+                                                      0, p.y_len ? p.B * 4 : 0, 0x00020000);
   for (int r0 = wave; r0 < BN; r0 += 4 * RB) {
     float v[RB][8];
     long long ro[RB];
@@ -294,7 +299,9 @@ __device__ inline void splitp_tile_ln(const ConvParams& p, int f0, int BN, int F
     for (int k = 0; k < RB; ++k) {  // unconditional loads at clamped rows / channels
       const int f = min(f0 + min(r0 + 4 * k, BN - 1), F - 1);
       const int b = f / p.x_rows, r = f - b * p.x_rows;
-      ok[k] = r0 + 4 * k < BN && f0 + r0 + 4 * k < F && r < (p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows);
+      // (the length through a descriptor, OR-ed to "no limit" when absent: an unconditional load)
+      const int L = __builtin_amdgcn_raw_buffer_load_b32(ylrs, b * 4, 0, 0) | (p.y_len ? 0 : 0x7fffffff);
+      ok[k] = r0 + 4 * k < BN && f0 + r0 + 4 * k < F && r < min(L, p.y_rows);
       ro[k] = p.ln_lin_out ? (long long)b * p.y_rows + r : (long long)b * p.syb + (long long)r * p.syr;
       const float* x = reinterpret_cast<const float*>(p.y) + (long long)b * p.syb + (long long)r * p.syr;
 #pragma unroll
@@ -328,13 +335,17 @@ __device__ inline void splitp_tile_ln(const ConvParams& p, int f0, int BN, int F
   }
 }
 
-// one flat row f of the split-K reduce + LayerNorm, by one wave (rows past an utterance: nothing)
+// one flat row f of the split-K reduce + LayerNorm, by one wave (rows past an utterance: nothing).
+// Every load is unconditional (clamped channels, the length through a descriptor) and the slices
+// go one at a time with all of the lane's channels in flight: the first form returned early on
+// the row's length and loaded each channel's slices under its own branch -- a wait per load.
 __device__ inline void split_reduce_ln_row(const ConvParams& p, int S, int F, int f, int lane) {
   constexpr int PER = 8;
   const int b = f / p.x_rows;
   const int r = f - b * p.x_rows;
-  const int ylen = p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows;
-  if (r >= ylen) return;
+  const auto ylrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.y_len ? p.y_len : reinterpret_cast<const int*>(p.ws)),
+                                                      0, p.y_len ? p.B * 4 : 0, 0x00020000);
+  const int ylen = min(__builtin_amdgcn_raw_buffer_load_b32(ylrs, b * 4, 0, 0) | (p.y_len ? 0 : 0x7fffffff), p.y_rows);
   const int C = p.M;
   const long long ro = (long long)b * p.srb + (long long)r * p.srr;
   int ch[PER];
@@ -342,23 +353,43 @@ __device__ inline void split_reduce_ln_row(const ConvParams& p, int S, int F, in
   ln_lanes64<PER>(ch, on, C, lane);
   float g[2][PER], bb[2][PER], v[1][PER];
   ln_params<PER>(g, bb, ch, on, p.ln_g1, p.ln_b1, p.ln_g2, p.ln_b2);
+  float x[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) x[i] = p.ws[(long long)f * C + min(ch[i], C - 1)];
+  for (int sl = 1; sl < S; ++sl) {
+    float w[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) w[i] = p.ws[((long long)sl * F + f) * C + min(ch[i], C - 1)];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) x[i] += w[i];
+  }
+  // bias / residuals through descriptors with no records when absent (unconditional loads, the
+  // adds selected by the uniform flags: the same operations as the branches they replace)
+  const auto mk = [&](const void* q, long long n) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(q ? q : (const void*)p.ws), 0, q ? (int)min(n, 0x7fffffffLL) : 0, 0x00020000);
+  };
+  const auto bs = mk(p.bias, (long long)C * 4), r1s = mk(p.r1, 0x7fffffffLL), r2s = mk(p.r2, 0x7fffffffLL);
+  float bv[PER], r1v[PER], r2v[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int c = ch[i];
-    float x = 0.f;
-    if (on[i]) {
-      x = p.ws[(long long)f * C + c];
-      for (int sl = 1; sl < S; ++sl) x += p.ws[((long long)sl * F + f) * C + c];
-      if (p.bias) x += p.bias[c];
-      if (p.alpha != 1.0f) x *= p.alpha;
-      if (p.r1) x += reinterpret_cast<const float*>(p.r1)[ro + c];
-      if (p.r2) x += reinterpret_cast<const float*>(p.r2)[ro + c];
-      if (p.out_scale != 1.0f) x *= p.out_scale;
-    }
-    v[0][i] = x;
+    const int c = min(ch[i], C - 1);
+    bv[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bs, c * 4, 0, 0));
+    r1v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1s, (int)((ro + c) * 4), 0, 0));
+    r2v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2s, (int)((ro + c) * 4), 0, 0));
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    float y = x[i];
+    if (p.bias) y += bv[i];
+    if (p.alpha != 1.0f) y *= p.alpha;
+    if (p.r1) y += r1v[i];
+    if (p.r2) y += r2v[i];
+    if (p.out_scale != 1.0f) y *= p.out_scale;
+    v[0][i] = on[i] ? y : 0.f;
   }
   if (p.ln_g2) ln_batch<float, 1, PER, true>(v, on, C, g, bb, p.ln_eps);
   else ln_batch<float, 1, PER, false>(v, on, C, g, bb, p.ln_eps);
+  if (r >= ylen) return;
   float* o = reinterpret_cast<float*>(p.ln_out) + (long long)b * p.syb + (long long)r * p.syr;
 #pragma unroll
   for (int i = 0; i < PER; ++i)
@@ -444,6 +475,12 @@ __device__ inline void splitk_tile_ln(const ConvParams& p, int S, int F, int f0,
 // batch-8 encoder), where each group's load round trip and barriers were the block's critical
 // path.  Same groups, quads and MFMA order: bit-identical to the group-by-group form.
 constexpr int SPK_WG = 3;
+#if TTS_SPLIT_STAMP
+// records of the launches whose (M, Cin, taps) match g_split_stamp_target: conv_xres's layout
+// (st0, staging done, MFMA loop done, row pass done, staging cycles, realtime start / end, hw id)
+__device__ int g_split_stamp_target[3];
+__device__ unsigned long long g_split_stamp[1 << 18];
+#endif
 template <bool WHOLE>
 __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int CG, int S, int gps) {
   typedef half8 Frag;
@@ -487,6 +524,22 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
   const int x_start = f0 - p.pad;
   const char* xl = smem + l31 * RS + hh * 16;
   const float* X = reinterpret_cast<const float*>(p.x);
+#if TTS_SPLIT_STAMP
+  const unsigned long long st0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long st1 = 0, st2 = 0;
+  auto stamp = [&]() __attribute__((always_inline)) {
+    if (p.M == g_split_stamp_target[0] && p.Cin == g_split_stamp_target[1] && p.taps == g_split_stamp_target[2]) {
+      __syncthreads();
+      if (tid == 0 && blockIdx.x < (1u << 15)) {
+        unsigned long long* r = g_split_stamp + blockIdx.x * 8;
+        r[0] = st0; r[1] = st1; r[2] = st2; r[3] = __builtin_amdgcn_s_memtime();
+        r[4] = st1 - st0; r[5] = rt0; r[6] = __builtin_amdgcn_s_memrealtime();
+        r[7] = ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11)) << 32) |
+               (unsigned)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+      }
+    }
+  };
+#endif
 
   f32x16 acc[NT], accx[NT];
 #pragma unroll
@@ -502,6 +555,29 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
   const int r0 = tid >> lvpr;
   const int rstep = 256 >> lvpr;
   f32x4 xv[SPK_SU];
+  // Validity of this thread's staged rows (the same rows for every group), bit i for row
+  // r0 + i * rstep: computed once, after the first group's X loads are issued, with the length
+  // loads through a descriptor (no branch around them).  Computing it per row inside the LDS
+  // stores made the compiler wait for every outstanding load (vmcnt(0)) once per staged row:
+  // at batch 8, 27 serialized round trips, 59 % of a K = 384 block's time (tools/xres_stamps.py).
+  int vm = 0;
+  auto row_mask = [&]() __attribute__((always_inline)) {
+    const auto lrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.x_len ? p.x_len : reinterpret_cast<const int*>(X)),
+                                                       0, p.x_len ? p.B * 4 : 0, 0x00020000);
+    int m = 0;
+#pragma unroll
+    for (int i = 0; i < SPK_SU; ++i) {
+      const int f = x_start + r0 + i * rstep;
+      const int fc = min(max(f, 0), F - 1);
+      const int b = fc / p.x_rows, r = fc - b * p.x_rows;
+      // (no length array: the descriptor reads 0 and the OR makes the limit x_rows -- the load
+      // stays unconditional, not sunk into a branch with a wait of its own)
+      const int L = __builtin_amdgcn_raw_buffer_load_b32(lrs, b * 4, 0, 0) | (p.x_len ? 0 : 0x7fffffff);
+      const int lim = min(L, p.x_rows);
+      m |= (f >= 0 && f < F && r < lim ? 1 : 0) << i;
+    }
+    return m;
+  };
   auto load_x_to = [&](int g, f32x4 (&xd)[SPK_SU]) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < SPK_SU; ++i) {
@@ -515,7 +591,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     for (int i = 0; i < SPK_SU; ++i) {
       const int rr = r0 + i * rstep;
       f32x4 v = xs[i];
-      if (!packed_valid(p, p.x_len, x_start + rr, F)) v = f32x4{};
+      if (!((vm >> i) & 1)) v = f32x4{};
       if (p.in_slope != 1.0f) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = leaky(v[e], p.in_slope);
@@ -572,14 +648,21 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     const int ng = (gend - gbeg) / CG;  // <= SPK_WG (launcher)
 #pragma unroll
     for (int i = 0; i < SPK_WG; ++i) load_x_to(gbeg + min(i, ng - 1) * CG, xw[i]);
+    __builtin_amdgcn_sched_barrier(0);  // the X loads issue before the length loads
+    vm = row_mask();
 #pragma unroll
     for (int i = 0; i < SPK_WG; ++i)
       if (i < ng) store_x_from(xw[i], smem + i * 2 * PL);
   } else {
     load_x(gbeg);
+    __builtin_amdgcn_sched_barrier(0);
+    vm = row_mask();
     store_x();
   }
   __syncthreads();
+#if TTS_SPLIT_STAMP
+  st1 = __builtin_amdgcn_s_memtime();
+#endif
   for (; g0 < gend; g0 += CG) {
     const bool more = g0 + CG < gend;
     TTS_SPLIT_MMAQ(a0, 0);
@@ -604,6 +687,9 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     }
   }
   if constexpr (WHOLE) __syncthreads();  // (the epilogue reuses LDS: every wave is past its MFMAs)
+#if TTS_SPLIT_STAMP
+  st2 = __builtin_amdgcn_s_memtime();
+#endif
 
   const int m_w0 = (by * 4 + wave) * 32;
   if (S == 1) {
@@ -617,11 +703,18 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     const int m4 = by * 128 + pc * 4;
     const bool mok = m4 < p.M;
     f32x4 res[NIT];
+    // row-pass validity, bit it (rows inside F and the utterance's output length): the length
+    // loads go with the residual prefetch, not one wait per row in the row pass
+    int ym = 0;
+    const auto ylrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.y_len ? p.y_len : reinterpret_cast<const int*>(X)),
+                                                        0, p.y_len ? p.B * 4 : 0, 0x00020000);
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int rl = (tid >> 5) + it * 8;
       const int f = min(f0 + rl, F - 1);
       const int b = f / p.x_rows, r = f - b * p.x_rows;
+      const int L = __builtin_amdgcn_raw_buffer_load_b32(ylrs, b * 4, 0, 0) | (p.y_len ? 0 : 0x7fffffff);
+      ym |= (f0 + rl < F && r < min(L, p.y_rows) ? 1 : 0) << it;
       res[it] = f32x4{};
       if (p.r1 && mok) res[it] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.r1) +
                                                                  (long long)b * p.srb + (long long)r * p.srr + m4);
@@ -646,9 +739,8 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
       for (int it = 0; it < NIT; ++it) {
         const int rl = (tid >> 5) + it * 8;
         const int f = f0 + rl;
-        if (f >= F || !mok) continue;
+        if (!((ym >> it) & 1) || !mok) continue;
         const int b = f / p.x_rows, r = f - b * p.x_rows;
-        if (r >= (p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows)) continue;
         f32x4 v = (*reinterpret_cast<const f32x4*>(smem + rl * OSR + pc * 16) + bias) * p.alpha;  // x * 1.0f exact
         if constexpr (ACT != ACT_NONE) {
 #pragma unroll
@@ -672,6 +764,9 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
       case ACT_SILU: row_pass(ActC<ACT_SILU>{}); break;
       default: row_pass(ActC<ACT_NONE>{}); break;
     }
+#if TTS_SPLIT_STAMP
+    stamp();
+#endif
     // the row tile's last-arriving M block normalises its valid flat rows over all M channels
     if (lnf && ln_tile_last(p.ln_cnt + tx, nmb, reinterpret_cast<int*>(smem))) splitp_tile_ln(p, f0, BN, F, wave, lane);
     return;
@@ -699,6 +794,9 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
         *reinterpret_cast<f32x4*>(P + (long long)f * p.M + m) = e;
     }
   }
+#if TTS_SPLIT_STAMP
+  stamp();
+#endif
   if (lnf && ln_tile_last(p.ln_cnt + tx, nmb * S, reinterpret_cast<int*>(smem)))
     splitk_tile_ln(p, S, F, f0, BN, wave, lane);
 }
@@ -894,5 +992,17 @@ hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done) 
   }
   return split_tile(p) == 2 ? launch_tile<2>(p, s) : launch_tile<1>(p, s);
 }
+
+#if TTS_SPLIT_STAMP
+extern "C" int tts_debug_split_target(int M, int Cin, int taps) {
+  const int t[3] = {M, Cin, taps};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_split_stamp_target), t, sizeof(t)) == hipSuccess ? 0 : -1;
+}
+extern "C" int tts_debug_split_stamps(unsigned long long* host, long long words) {
+  const long long n = words < (1LL << 18) ? words : (1LL << 18);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_split_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace tts

@@ -1,7 +1,8 @@
 """Per-block phase timeline of one conv_xres launch (diagnostic build only).
 
-Build:  python -m gonova_tts_amd.build --variant stamp -DTTS_XRES_STAMP=1
-Run:    TTS_LIB=<repo>/gonova-tts_amd/libtts_hip_stamp.so python3 tools/xres_stamps.py {ffn_up|ffn_down|qkv|s0up|s1up}
+Build:  python -m gonova_tts_amd.build --variant stamp -DTTS_XRES_STAMP=1 -DTTS_SPLIT_STAMP=1
+Run:    TTS_LIB=<repo>/gonova-tts_amd/libtts_hip_stamp.so python3 tools/xres_stamps.py {ffn_up|ffn_down|qkv|s0up|s1up|e_*}
+The e_* targets are the exact encoder's split-precision GEMMs (conv_split.hip) at batch 8.
 
 The target launch shape (M, Cin, taps) is set in the library; the last launch of that shape in
 the workload (acoustic forward at batch 32, or the C2 vocoder step) leaves one record per block.
@@ -23,6 +24,12 @@ TARGETS = {  # (M, Cin, taps, workload)
     "qkv": (1152, 384, 1, "acoustic"),
     "s0up": (2048, 512, 2, "vocoder"),
     "s1up": (1024, 256, 2, "vocoder"),
+    # exact encoder (fp32 split GEMMs) in a batch-8 forward
+    "e_qkv": (1152, 384, 1, "acoustic8"),
+    "e_out": (384, 384, 1, "acoustic8"),
+    "e_pw1": (768, 384, 1, "acoustic8"),
+    "e_ffn_up": (1536, 384, 3, "acoustic8"),
+    "e_ffn_down": (384, 1536, 3, "acoustic8"),
 }
 
 
@@ -32,12 +39,15 @@ def run(which):
     from gonova_tts_amd.weights import make_acoustic_weights, make_vocoder_weights
     M, Cin, taps, wl = TARGETS[which]
     lib = load_library()
-    lib.tts_debug_xres_target.argtypes = [ctypes.c_int] * 3
-    lib.tts_debug_xres_stamps.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
-    assert lib.tts_debug_xres_target(M, Cin, taps) == 0
+    kind = "split" if wl == "acoustic8" else "xres"
+    set_target = getattr(lib, f"tts_debug_{kind}_target")
+    read = getattr(lib, f"tts_debug_{kind}_stamps")
+    set_target.argtypes = [ctypes.c_int] * 3
+    read.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
+    assert set_target(M, Cin, taps) == 0
     g = torch.Generator(device="cpu").manual_seed(3)
-    if wl == "acoustic":
-        B, N = 32, 144
+    if wl.startswith("acoustic"):
+        B, N = (8, 144) if wl == "acoustic8" else (32, 144)
         eng = HipEngine("cuda:0", acoustic_dtype="bf16", vocoder_dtype="bf16", max_batch=B, max_frames=N * 6, max_tokens=N)
         eng.load_weights(acoustic=make_acoustic_weights(seed=0, fixed_duration=6))
         tok = torch.randint(1, 78, (B, N), generator=g, dtype=torch.int32).cuda()
@@ -52,8 +62,8 @@ def run(which):
     for _ in range(4):
         step()
     torch.cuda.synchronize()
-    buf = np.zeros(1 << 20, np.uint64)
-    assert lib.tts_debug_xres_stamps(buf.ctypes.data, buf.size) == 0
+    buf = np.zeros(1 << (18 if kind == "split" else 20), np.uint64)
+    assert read(buf.ctypes.data, buf.size) == 0
     eng.close()
     rec = buf.reshape(-1, 8)
     rec = rec[rec[:, 0] != 0]
@@ -92,5 +102,5 @@ def analyze(rec, which):
 
 
 if __name__ == "__main__":
-    w = sys.argv[1] if len(sys.argv) > 1 else "ffn_up"
-    analyze(run(w), w)
+    for w in sys.argv[1:] or ["ffn_up"]:
+        analyze(run(w), w)

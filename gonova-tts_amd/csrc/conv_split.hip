@@ -36,6 +36,9 @@
 #ifndef TTS_SPLIT_STAMP
 #define TTS_SPLIT_STAMP 0  // diagnostic builds: per-block phase timestamps of one launch shape (tools/xres_stamps.py)
 #endif
+#ifndef TTS_SPLIT_NT1_MAXBLK
+#define TTS_SPLIT_NT1_MAXBLK 128  // 64-row grids below this many blocks run 32-row tiles (0: never)
+#endif
 #ifndef TTS_SPLIT_PROBE
 #define TTS_SPLIT_PROBE 0  // timing-only probe builds: every weight quad read from the first (L1/L2-hot, wrong results)
 #endif
@@ -481,10 +484,11 @@ constexpr int SPK_WG = 3;
 __device__ int g_split_stamp_target[3];
 __device__ unsigned long long g_split_stamp[1 << 18];
 #endif
-template <bool WHOLE>
+// NT: 32-row MFMA tiles per wave (SPK_NT; 1 for grids the 64-row tiles leave under-filled)
+template <bool WHOLE, int NT = SPK_NT>
 __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int CG, int S, int gps) {
   typedef half8 Frag;
-  constexpr int NT = SPK_NT, BN = 32 * NT;
+  constexpr int BN = 32 * NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int F = p.B * p.x_rows;  // flat rows
@@ -905,13 +909,13 @@ static int packed_group(const ConvParams& p) {
 }
 
 // whether a one-slice packed launch over F flat rows applies p's LayerNorm itself: a counter per
-// 64-row tile, rows of M <= 512 channels, y / ln_out in the packed [B][x_rows][M] layout
-static bool splitp_ln_ok(const ConvParams& p, int F) {
+// BN-row tile, rows of M <= 512 channels, y / ln_out in the packed [B][x_rows][M] layout
+static bool splitp_ln_ok(const ConvParams& p, int F, int BN) {
   if (!p.ln_cnt || !(p.ln_out || p.ln_lin_out) || p.M > 512) return false;
   // small grids: the tile's LayerNorm tail is on the critical path (the same bits either way)
-  if (sw(SW_LN_FUSE) != 7 && (long long)((F + 32 * SPK_NT - 1) / (32 * SPK_NT)) * ((p.M + 127) / 128) < TTS_LN_FUSE_MINBLK)
+  if (sw(SW_LN_FUSE) != 7 && (long long)((F + BN - 1) / BN) * ((p.M + 127) / 128) < TTS_LN_FUSE_MINBLK)
     return false;  // (TTS_LN_FUSE=7: every eligible launch, tests)
-  return (F + 32 * SPK_NT - 1) / (32 * SPK_NT) <= p.ln_cnt_n;
+  return (F + BN - 1) / BN <= p.ln_cnt_n;
 }
 
 // packed-row form: usable when the caller promises enough masked rows after every utterance for
@@ -953,26 +957,34 @@ hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done) 
       const int S = split_slices(p, cg);
       const int gps = p.Cin / cg / S;
       const int F = p.B * p.x_rows;
-      const int nwg = (F + 32 * SPK_NT - 1) / (32 * SPK_NT) * ((p.M + 127) / 128) * S;
-      const size_t lds = std::max((size_t)2 * (32 * SPK_NT + (p.taps - 1) * p.dil) * (cg * 2 + 16),
-                                  (size_t)32 * SPK_NT * (128 * 4 + 16));  // X planes / epilogue tile
+      // 32-row tiles where the 64-row grid would leave most CUs idle (the batch-8 encoder's
+      // M = 384 projections: 60 blocks): twice the blocks, each with half the staging and MFMA
+      // latency.  A row's K order does not depend on the tile: bit-identical.
+      const int mbs = (p.M + 127) / 128 * S;
+      const int nt = sw(SW_SPLIT_NT1) == 1 || (sw(SW_SPLIT_NT1) != 0 && (F + 63) / 64 * mbs < TTS_SPLIT_NT1_MAXBLK) ? 1 : SPK_NT;
+      const int nwg = (F + 32 * nt - 1) / (32 * nt) * mbs;
+      const size_t lds = std::max((size_t)2 * (32 * nt + (p.taps - 1) * p.dil) * (cg * 2 + 16),
+                                  (size_t)32 * nt * (128 * 4 + 16));  // X planes / epilogue tile
       // one block per CU or fewer: stage the K slice's groups at once (no restaging; bit-identical)
       const int ngs = gps;  // groups per slice
       const bool whole = sw(SW_SPLIT_WHOLE) != 0 && ngs <= SPK_WG && nwg <= TTS_SPLIT_WHOLE_MAXBLK;
-      const size_t ldsw = whole ? std::max((size_t)ngs * 2 * (32 * SPK_NT + (p.taps - 1) * p.dil) * (cg * 2 + 16),
-                                           (size_t)32 * SPK_NT * (128 * 4 + 16))
+      const size_t ldsw = whole ? std::max((size_t)ngs * 2 * (32 * nt + (p.taps - 1) * p.dil) * (cg * 2 + 16),
+                                           (size_t)32 * nt * (128 * 4 + 16))
                                 : lds;
       ConvParams q = p;
       // the kernel's LayerNorm switch: its epilogue (one slice) or its in-launch split-K reduce
       // (the in-launch split-K reduce, TTS_SPLITK_FUSE=1, is off by default: its results varied between
       // runs at batch 32 -- an ordering problem of the hand-off not yet found; the separate reduce runs)
-      bool fuse = splitp_ln_ok(p, F) && (S == 1 || (TTS_SPLITK_FUSE && p.ln_out && p.act_out == ACT_NONE && S <= SKMAX));
+      bool fuse = splitp_ln_ok(p, F, 32 * nt) && (S == 1 || (TTS_SPLITK_FUSE && p.ln_out && p.act_out == ACT_NONE && S <= SKMAX));
       if (sw(SW_LN_FUSE) > 1 && sw(SW_LN_FUSE) != 7 && sw(SW_LN_FUSE) != (S == 1 ? 3 : 4)) fuse = false;  // (bisection: 3 / 4 = one slice / split-K only)
       if (!fuse) q.ln_cnt = nullptr;
-      if (whole && ldsw <= 160 * 1024)
-        hipLaunchKernelGGL(conv_splitp_kernel<true>, dim3(nwg), dim3(256), ldsw, s, q, cg, S, gps);
-      else
-        hipLaunchKernelGGL(conv_splitp_kernel<false>, dim3(nwg), dim3(256), lds, s, q, cg, S, gps);
+      if (whole && ldsw <= 160 * 1024) {
+        if (nt == 1) hipLaunchKernelGGL((conv_splitp_kernel<true, 1>), dim3(nwg), dim3(256), ldsw, s, q, cg, S, gps);
+        else hipLaunchKernelGGL((conv_splitp_kernel<true, SPK_NT>), dim3(nwg), dim3(256), ldsw, s, q, cg, S, gps);
+      } else {
+        if (nt == 1) hipLaunchKernelGGL((conv_splitp_kernel<false, 1>), dim3(nwg), dim3(256), lds, s, q, cg, S, gps);
+        else hipLaunchKernelGGL((conv_splitp_kernel<false, SPK_NT>), dim3(nwg), dim3(256), lds, s, q, cg, S, gps);
+      }
       if (q.ln_cnt) {
         if (ln_done) *ln_done = true;
         return hipGetLastError();

@@ -24,6 +24,7 @@ enum Sw : int {
   SW_SPLIT_WHOLE,  // TTS_SPLIT_WHOLE=0: small split-precision GEMMs stage one channel group at a time
   SW_XRES_DMA,     // TTS_XRES_DMA=0: FFN convs / upsamplers register-staged with round-2 channel groups; 2: register-staged, same bits
   SW_LN_FUSE,      // TTS_LN_FUSE=0: acoustic post-LNs as their own launches; 7: in every eligible GEMM launch (2-6: bisection)
+  SW_SPLIT_NT1,    // TTS_SPLIT_NT1=0: split GEMMs always on 64-row tiles; 1: 32-row tiles wherever eligible (default: small grids)
   SW_N
 };
 

@@ -367,6 +367,29 @@ def test_dma_staged_ffn_bit_identical(aw, dtype, switch):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_split_tile_height_bit_identical(aw, dtype, switch):
+    """The split-precision GEMMs' 32-row tiles (small grids: the batch-8 exact encoder) give the
+    64-row tiles' bits (TTS_SPLIT_NT1=0) and those of 32-row tiles everywhere (=1), with the
+    post-LNs fused in every eligible launch as well (TTS_LN_FUSE=7: the tail on 32-row tiles), on
+    a ragged batch-8 forward with predicted durations."""
+    eng = engine(dtype, aw)
+    rng = np.random.default_rng(45)
+    ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70, 127, 129, 9, 33)]
+    outs = {}
+    for nt1 in (0, None, 1):
+        for ln in (None, 7):
+            switch("TTS_SPLIT_NT1", nt1)
+            switch("TTS_LN_FUSE", ln)
+            outs[(nt1, ln)] = run(eng, ids_list, t_cap=8 * 144)
+    switch("TTS_SPLIT_NT1", None)
+    switch("TTS_LN_FUSE", None)
+    ref_m, ref_l, ref_d = outs[(0, None)]
+    for k, (m, l, d) in outs.items():
+        assert np.array_equal(d, ref_d) and np.array_equal(l, ref_l), k
+        assert np.array_equal(m, ref_m), k
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_split_whole_slice_staging_bit_identical(aw, dtype, switch):
     """Small split-precision GEMM grids (at most one block per CU: the batch-8 exact encoder and
     predictors) stage every channel group of their K slice at once; the quads and their MFMA order

@@ -34,6 +34,14 @@ def main():
             valid = torch.arange(m.shape[1], device=m.device)[None, :] < ml[:, None].long()
             out["mel_ragged_b8"] = torch.where(valid[..., None], m, torch.zeros_like(m)).cpu().numpy()
         e.close()
+    # fp32 engine (C1's): one 71-token utterance, tokens -> mel -> waveform
+    e = HipEngine("cuda:0", vocoder_dtype="f32", acoustic_dtype="f32", max_batch=1, max_frames=426, max_tokens=71)
+    e.load_weights(vocoder=vw, acoustic=aw)
+    tok = torch.randint(1, 78, (1, 71), generator=g, dtype=torch.int32).cuda()
+    m, ml = e.acoustic(tok, torch.full((1,), 71, dtype=torch.int32).cuda(), 426)
+    out["c1_f32_mel"] = m.cpu().numpy()
+    out["c1_f32_wav"] = e.vocoder(m, ml).cpu().numpy()
+    e.close()
     for k, v in out.items():
         print(k, v.shape, hashlib.sha256(v.tobytes()).hexdigest()[:16])
 

@@ -710,6 +710,9 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     // row-pass validity, bit it (rows inside F and the utterance's output length): the length
     // loads go with the residual prefetch, not one wait per row in the row pass
     int ym = 0;
+    const auto r1rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.r1 ? p.r1 : p.y), 0, p.r1 ? 0x7fffffff : 0, 0x00020000);
+    const auto brs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.bias ? p.bias : reinterpret_cast<const float*>(X)), 0,
+                                                       p.bias ? p.M * 4 : 0, 0x00020000);
     const auto ylrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.y_len ? p.y_len : reinterpret_cast<const int*>(X)),
                                                         0, p.y_len ? p.B * 4 : 0, 0x00020000);
 #pragma unroll
@@ -718,11 +721,12 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
       const int f = min(f0 + rl, F - 1);
       const int b = f / p.x_rows, r = f - b * p.x_rows;
       const int L = __builtin_amdgcn_raw_buffer_load_b32(ylrs, b * 4, 0, 0) | (p.y_len ? 0 : 0x7fffffff);
-      ym |= (f0 + rl < F && r < min(L, p.y_rows) ? 1 : 0) << it;
-      res[it] = f32x4{};
-      if (p.r1 && mok) res[it] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.r1) +
-                                                                 (long long)b * p.srb + (long long)r * p.srr + m4);
+      ym |= ((int)(f0 + rl < F) & (int)(r < min(L, p.y_rows))) << it;  // (no short-circuit: no branch)
+      // the first residual (0 when absent or past M), through a descriptor: an unconditional load
+      const long long ro = (long long)b * p.srb + (long long)r * p.srr + m4;
+      res[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r1rs, mok ? (int)(ro * 4) : 0x7ffffff0, 0, 0));
     }
+    const f32x4 bias = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(brs, m4 * 4, 0, 0));  // 0 past M
     __syncthreads();  // X tile no longer read
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -733,7 +737,6 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
             f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
     }
     __syncthreads();
-    const f32x4 bias = (p.bias && mok) ? *reinterpret_cast<const f32x4*>(p.bias + m4) : f32x4{};
     const bool lnf = p.ln_cnt != nullptr;  // LayerNorm in this launch (the launcher checked the shape)
     const auto yrsrc = __builtin_amdgcn_make_buffer_rsrc(p.y, 0, 0x7fffffff, 0x00020000);
     // the activation kind is dispatched once, outside the row loop (conv_xres's epilogue)

@@ -182,9 +182,20 @@ class GonovaTTS:
         spk = speaker_embedding
         mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True,
                                                   speaker_embedding=spk)
+        first = None  # (window end, kept frames, chunk) enqueued ahead of the host read
         if durations is None:
+            # The first chunk's window needs no host value when the longest utterance covers it
+            # (frames >= chunk + ctx, the usual case): enqueue it before the one host read of the
+            # frame counts, so the GPU runs it instead of idling through the round trip.  It is
+            # used only if the loop below would make exactly the same call (else recomputed).
+            w1 = min(t_cap, chunk_frames + ctx)
+            tc = min(chunk_frames, t_cap)
+            if os.environ.get("TTS_STREAM_EARLY", "1") != "0":  # (0: the host read first, A/B runs)
+                win_lens = torch.clamp(mel_lens, min=0, max=w1).to(torch.int32)
+                first = (w1, tc, self.engine.vocoder_chunk(mel[:, :w1].contiguous(), win_lens, 0, tc, stream=stream))
             need, lens_h = _need_and_lens(dur, mel_lens)  # one host read before the first chunk
             if need > t_cap:
+                first = None
                 mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
                                                           return_durations=True, speaker_embedding=spk)
                 need, lens_h = _need_and_lens(dur, mel_lens)
@@ -199,9 +210,13 @@ class GonovaTTS:
             tc = min(chunk_frames, T - c0)
             w0 = max(0, c0 - ctx)
             w1 = min(T, c0 + tc + ctx)
-            win = mel[:, w0:w1].contiguous()
-            win_lens = torch.clamp(mel_lens - w0, min=0, max=w1 - w0).to(torch.int32)
-            wav = self.engine.vocoder_chunk(win, win_lens, c0 - w0, tc, stream=stream)
+            if c0 == 0 and first is not None and first[:2] == (w1, tc):
+                wav = first[2]
+            else:
+                win = mel[:, w0:w1].contiguous()
+                win_lens = torch.clamp(mel_lens - w0, min=0, max=w1 - w0).to(torch.int32)
+                wav = self.engine.vocoder_chunk(win, win_lens, c0 - w0, tc, stream=stream)
+            first = None
             valid = np.clip(lens_h - c0, 0, tc) * hop
             yield c0, wav, valid
 

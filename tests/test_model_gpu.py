@@ -83,6 +83,30 @@ def test_streaming_chunks_equal_full_utterance(dtype):
         np.testing.assert_array_equal(got, full[b, :full_lens[b]])
 
 
+@pytest.mark.parametrize("lens", [[60, 5, 33], [5, 3, 7]])
+def test_streaming_predicted_durations_equal_full_utterance(lens):
+    """With predicted durations the first chunk is enqueued before the host reads the frame
+    counts (used when the longest utterance covers its window, recomputed otherwise: the second
+    case, 18-42 frames); the chunks still reproduce the full pass bit for bit."""
+    m = GonovaTTS.from_pretrained("cuda:0", vocoder_dtype="f16", acoustic_dtype="bf16", fixed_duration=6)
+    rng = np.random.default_rng(3)
+    lens = np.array(lens, np.int32)
+    tok = np.zeros((3, int(lens.max())), np.int32)
+    for i, L in enumerate(lens):
+        tok[i, :L] = rng.integers(1, 78, size=L)
+    full, full_lens = m.synthesize_tokens(tok, lens)
+    full = full.cpu().numpy()
+    pieces = [[] for _ in range(3)]
+    for c0, wav, valid in m.stream_tokens(tok, lens, chunk_frames=32):
+        w = wav.cpu().numpy()
+        for b in range(3):
+            pieces[b].append(w[b, :valid[b]])
+    for b in range(3):
+        got = np.concatenate(pieces[b])
+        assert got.shape[0] == full_lens[b] == 6 * 256 * lens[b]
+        np.testing.assert_array_equal(got, full[b, :full_lens[b]])
+
+
 def test_generate_at_24khz_is_resampled_native_output(model32):
     """sample_rate=24000 (the rate the reference's clients assume, synthesizer.py:119): the
     22,050 Hz waveform converted on the device == scipy.signal.resample_poly of it."""

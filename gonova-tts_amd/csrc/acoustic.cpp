@@ -74,11 +74,20 @@ struct AcousticModel::Impl {
   int cur_rpad = 0;            // rows_pad of the convs being launched (encoder side only)
   float* split_ws = nullptr;   // split-K partial sums of the packed split GEMMs
   long long split_ws_bytes = 0;
+  // Range guard of the exact encoder (tts_hip.h, TTS_ENCODER_EXACT): the split GEMMs and the
+  // split attention OR 1 into this device word when a staged fp32 operand is outside f16's range;
+  // the host reads and clears it (tts_acoustic_range_flag) and reruns with enc_f32 set, which
+  // sends the same fp32 layers through the exact fp32 MFMA kernels (no split form).
+  int* range_flag = nullptr;
+  bool enc_f32 = false;
   void run(const ConvLayer& L, const void* x, int x_rows, const int* lens, void* y, int y_rows, int B, int d,
            hipStream_t s, Profiler* pr, float in_slope = 1.f, int act = ACT_NONE, float alpha = 1.f,
            const void* r1 = nullptr, const ConvParams* ln = nullptr) {
+    ConvParams ex = ln ? *ln : conv_params_default();
+    ex.range_flag = range_flag;
+    ex.no_split = enc_f32 ? 1 : 0;
     run_layer(L, x, x_rows, lens, y, y_rows, B, d, s, pr, in_slope, act, alpha, r1, nullptr, 1.f, 0, 0, cur_rpad,
-              split_ws, split_ws_bytes, ln);
+              split_ws, split_ws_bytes, &ex);
   }
   // the LayerNorm fields (ConvParams) of a post-LN -- LN2?(LN1(y)) -> out -- with the row-tile
   // counters that let the 16-bit X-resident and one-slice split GEMMs apply it in their own launch
@@ -414,9 +423,9 @@ struct AcousticModel::Impl {
       if (fused_attn) {
         // fused flash-style relative-position attention (attention.hip); Qu / Qv formed in it
         // fp32 layers of a 16-bit model (the exact-duration encoder) in split precision, like their GEMMs
-        const bool split = dt == DT_F32 && this->dt != DT_F32 && sw(SW_ATTN_SPLIT) != 0;
+        const bool split = dt == DT_F32 && this->dt != DT_F32 && sw(SW_ATTN_SPLIT) != 0 && !enc_f32;
         prof_launch(PK_ATTN, 6.0 * D * (double)B * Tm * Tm, s, [&] { return launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale,
-                                  O, s); });
+                                  O, s, range_flag); });
         run_ln(L.out, O, Tp, lens, Y, Tp, B, dt, s, 1.f, Xb, Xb, L.ln_att, nullptr);
         conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
         continue;
@@ -494,6 +503,7 @@ struct AcousticModel::Impl {
       p.y_len = tok_lens; p.y_rows = Np;
       p.M = D; p.Cin = D; p.B = B;
       p.rows_pad = cur_rpad; p.ws = split_ws; p.ws_bytes = split_ws_bytes;
+      p.range_flag = range_flag; p.no_split = enc_f32 ? 1 : 0;
       launch_conv_checked(p, dte, s, prof, 2.0 * D * (double)D * B * Np);
       HIP_CHECK(hipMemcpyAsync(ENC, Y, (size_t)B * Np * D * dtype_size(dte), hipMemcpyDeviceToDevice, s));
     }
@@ -620,6 +630,12 @@ void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtyp
     m->postnet.push_back(m->conv(get, shape, p + "conv.weight", "", (k - 1) / 2, &sc, &bb));
   }
   m->build_ptabs(1024, nullptr);
+  {
+    void* f = nullptr;
+    HIP_CHECK(hipMalloc(&f, 16));
+    HIP_CHECK(hipMemset(f, 0, 16));
+    m->range_flag = (int*)m->track(f);
+  }
   impl = m.release();
   loaded = true;
 }
@@ -636,6 +652,21 @@ void AcousticModel::forward(const int32_t* tokens, const int32_t* tok_lens, int 
 }
 
 int AcousticModel::speaker_dim() const { return impl ? impl->E : 0; }
+
+bool AcousticModel::split_encoder() const { return impl && impl->dte == DT_F32 && impl->dt != DT_F32; }
+
+void AcousticModel::set_encoder_f32(bool on) {
+  if (!impl) throw TtsError(TTS_ERR_STATE, "acoustic model not loaded");
+  impl->enc_f32 = on;
+}
+
+bool AcousticModel::encoder_f32() const { return impl && impl->enc_f32; }
+
+void AcousticModel::range_flag_to(int32_t* dst, hipStream_t s) {
+  if (!impl) throw TtsError(TTS_ERR_STATE, "acoustic model not loaded");
+  HIP_CHECK(hipMemcpyAsync(dst, impl->range_flag, 4, hipMemcpyDefault, s));
+  HIP_CHECK(hipMemsetAsync(impl->range_flag, 0, 4, s));
+}
 
 void AcousticModel::free_all() {
   delete impl;

@@ -23,6 +23,14 @@ struct AcousticModel {
   void forward(const int32_t* tokens, const int32_t* tok_lens, int B, int N, const int32_t* dur_override,
                float* mel, int32_t* mel_lens, int Tcap, int32_t* durations, const float* spk, hipStream_t s);
   int speaker_dim() const;
+  // exact encoder of a 16-bit model (split-precision GEMMs and attention)
+  bool split_encoder() const;
+  // run that encoder on the exact fp32 MFMA kernels instead (the range guard's fallback)
+  void set_encoder_f32(bool on);
+  bool encoder_f32() const;
+  // enqueue on s: copy the range-guard word (1 = a split operand was outside f16's range since the
+  // last call) to dst (device or host-pinned), then clear it
+  void range_flag_to(int32_t* dst, hipStream_t s);
   void free_all();
   struct Impl;
   Impl* impl = nullptr;

@@ -36,6 +36,6 @@ hipError_t launch_spk_bias(int dt, const float* e, int B, int E, const float* We
 bool rel_attn_supported(int dt, int D, int H);
 hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* pos_v, const void* qkv, const void* vt,
                            const void* ptab, const int* lens, int B, int Tm, int Tp, int D, int H, int Sk, int rmax,
-                           float scale, void* out, hipStream_t s);
+                           float scale, void* out, hipStream_t s, int* range_flag = nullptr);
 
 }  // namespace tts

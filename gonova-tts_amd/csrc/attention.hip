@@ -554,7 +554,8 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
                                                                const float* __restrict__ qkv, const float* __restrict__ vt,
                                                                const float* __restrict__ ptab, const int* __restrict__ lens,
                                                                int Tp, int D, int H, int Sk, int rmax, float scale,
-                                                               float* __restrict__ out, int nqb, int nbatch) {
+                                                               float* __restrict__ out, int nqb, int nbatch,
+                                                               int* __restrict__ range_flag) {
   using MF = Mfma16<half_t>;
   typedef half8 Frag;
   constexpr int KS = DK / 32;         // k-steps over dk
@@ -582,6 +583,11 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
   const int iq = min(i0w + q, Tp - 1);
   // Qu = q + pos_bias_u, Qv = q + pos_bias_v (HF:420-423) in fp32, then split
   Frag bu[KS], bul[KS], bv[KS], bvl[KS];
+  unsigned rng = 0;  // range guard over the split operands' hi halves (common.h f16x2_nonfinite)
+  auto guard8 = [&](const Frag& f) __attribute__((always_inline)) {
+    const uint4 u = __builtin_bit_cast(uint4, f);
+    rng |= f16x2_nonfinite(u.x) | f16x2_nonfinite(u.y) | f16x2_nonfinite(u.z) | f16x2_nonfinite(u.w);
+  };
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     const int c = h * DK + ks * 32 + 8 * g;
@@ -589,6 +595,8 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
     const f32x4 q0 = *reinterpret_cast<const f32x4*>(qr), q1 = *reinterpret_cast<const f32x4*>(qr + 4);
     at_split8(q0 + *reinterpret_cast<const f32x4*>(pu + c), q1 + *reinterpret_cast<const f32x4*>(pu + c + 4), bu[ks], bul[ks]);
     at_split8(q0 + *reinterpret_cast<const f32x4*>(pv + c), q1 + *reinterpret_cast<const f32x4*>(pv + c + 4), bv[ks], bvl[ks]);
+    guard8(bu[ks]);
+    guard8(bv[ks]);
   }
   f32x4 oacc[DT], oaccx[DT];
 #pragma unroll
@@ -608,9 +616,10 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
   auto rslot = [](int m) { const int r = m % AT_RW; return r < 0 ? r + AT_RW : r; };
   auto rrow = [&](int m) { return min(max(rmax - 1 - m, 0), 2 * rmax - 1); };
   auto ring_back = [](unsigned a) { return min(a - AT_BK * KR, a + (AT_RW - AT_BK) * KR); };
-  auto put = [](char* plane_hi, int plane, int off, f32x4 v) __attribute__((always_inline)) {
+  auto put = [&rng](char* plane_hi, int plane, int off, f32x4 v) __attribute__((always_inline)) {
     uint2 hi, lo;
     at_split4(v, hi, lo);
+    rng |= f16x2_nonfinite(hi.x) | f16x2_nonfinite(hi.y);
     *reinterpret_cast<uint2*>(plane_hi + off) = hi;
     *reinterpret_cast<uint2*>(plane_hi + plane + off) = lo;
   };
@@ -779,6 +788,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
     for (int t = 0; t < DT; ++t)
       *reinterpret_cast<f32x4*>(orow + 16 * t + 4 * g) = (oacc[t] + oaccx[t] * (1.f / AT_SPLIT)) * inv;
   }
+  range_report(range_flag, rng);
 }
 
 template <int DK>
@@ -806,14 +816,14 @@ bool rel_attn_supported(int dt, int D, int H) {
 
 hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* pos_v, const void* qkv, const void* vt,
                            const void* ptab, const int* lens, int B, int Tm, int Tp, int D, int H, int Sk, int rmax,
-                           float scale, void* out, hipStream_t s) {
+                           float scale, void* out, hipStream_t s, int* range_flag) {
   if (!rel_attn_supported(dt, D, H) || Tm > rmax || Sk % 8) return hipErrorInvalidValue;
   const int nqb = (Tm + AT_BQ - 1) / AT_BQ;
   dim3 grid(xcd_grid(nqb, H * B));
   if (dt == DT_F32 && split) {
     hipLaunchKernelGGL((rel_attn_split_kernel<192>), grid, dim3(256), rel_attn_split_lds<192>(), s, pos_u, pos_v,
                        (const float*)qkv, (const float*)vt, (const float*)ptab, lens, Tp, D, H, Sk, rmax, scale,
-                       (float*)out, nqb, B);
+                       (float*)out, nqb, B, range_flag);
     return hipGetLastError();
   }
   if (dt == DT_F32) {

@@ -103,6 +103,20 @@ template <typename T> struct Chunk16 {
 
 __device__ inline float leaky(float x, float slope) { return x >= 0.f ? x : x * slope; }
 
+// Range guard of the split-precision (three-f16) paths (conv_split.hip, the split attention): an
+// fp32 operand is held as hi = f16(x) plus a scaled remainder, so |x| >= 65520 (hi = inf) or a
+// NaN cannot be represented.  f16x2_nonfinite(w) has bit 15 / 31 set iff the low / high half of
+// the f16 pair w has an all-ones exponent (inf or NaN): (e & 0x7c00) + 0x0400 reaches 0x8000 only
+// for e = 0x7c00, with no carry out of the half.  A kernel ORs these over its hi halves and, at
+// its end, reports a hit to a device word the host reads (range_report).
+#ifndef TTS_RANGE_GUARD
+#define TTS_RANGE_GUARD 1  // 0: A/B builds without the guard (the word is never set)
+#endif
+__device__ inline unsigned f16x2_nonfinite(unsigned w) { return TTS_RANGE_GUARD ? (w & 0x7c007c00u) + 0x04000400u : 0u; }
+__device__ inline void range_report(int* flag, unsigned acc) {
+  if (TTS_RANGE_GUARD && (acc & 0x80008000u) && flag) __hip_atomic_fetch_or(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // bf16 pairs.  One 32-bit word holds elements (lo, hi); as f32 they are w << 16 and
 // w & 0xffff0000 (exact), and a pair rounds back with one v_cvt_pk_bf16_f32 (RNE).  Element-wise
 // (T)float casts instead cost a one-sided cvt per element plus an SDWA or to merge the halves.

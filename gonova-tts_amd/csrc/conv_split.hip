@@ -131,6 +131,7 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
   f32x16 acc[NT], accx[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) { acc[j] = f32x16{}; accx[j] = f32x16{}; }
+  unsigned rng = 0;  // range guard over the staged hi halves (common.h f16x2_nonfinite)
 
   // staging: thread owns 8-channel column cc of the group and staged rows r0, r0 + rstep, ...
   // (staged row rr = utterance u * R + local row), SPLIT_SU loads in flight per batch
@@ -167,6 +168,7 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
         }
         uint4 hi, lo;
         split8(va, vb, hi, lo);
+        rng |= f16x2_nonfinite(hi.x) | f16x2_nonfinite(hi.y) | f16x2_nonfinite(hi.z) | f16x2_nonfinite(hi.w);
         if (rr < RU) {
           *reinterpret_cast<uint4*>(smem + rr * RS + cc * 16) = hi;
           *reinterpret_cast<uint4*>(smem + PL + rr * RS + cc * 16) = lo;
@@ -252,6 +254,7 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
 #undef TTS_SPLIT_MMAQ
   }
 
+  range_report(p.range_flag, rng);
   if (b >= p.B) return;
   f32x16 out[1][NT];
 #pragma unroll
@@ -548,6 +551,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
   f32x16 acc[NT], accx[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) { acc[j] = f32x16{}; accx[j] = f32x16{}; }
+  unsigned rng = 0;  // range guard over the staged hi halves (common.h f16x2_nonfinite)
 
   // X staging: thread owns 4-channel column c4 of the group and staged rows r0, r0 + rstep, ...
   // (at most SPK_SU: split_group sizes CG for that).  The next group's rows are loaded into
@@ -602,6 +606,8 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
       }
       const half4 h = __builtin_convertvector(v, half4);
       const half4 l = __builtin_convertvector((v - __builtin_convertvector(h, f32x4)) * SPLIT_SCALE, half4);
+      const uint2 hb = __builtin_bit_cast(uint2, h);
+      rng |= f16x2_nonfinite(hb.x) | f16x2_nonfinite(hb.y);
       if (rr < R) {
         *reinterpret_cast<uint2*>(base + rr * RS + c4 * 8) = __builtin_bit_cast(uint2, h);
         *reinterpret_cast<uint2*>(base + PL + rr * RS + c4 * 8) = __builtin_bit_cast(uint2, l);
@@ -691,6 +697,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     }
   }
   if constexpr (WHOLE) __syncthreads();  // (the epilogue reuses LDS: every wave is past its MFMAs)
+  range_report(p.range_flag, rng);
 #if TTS_SPLIT_STAMP
   st2 = __builtin_amdgcn_s_memtime();
 #endif
@@ -877,7 +884,7 @@ static int split_group(const ConvParams& p, int BN, int UW) {
 }
 
 bool conv_split_eligible(const ConvParams& p) {
-  return p.wpk && p.Cin % 128 == 0 && p.M % 4 == 0 && p.nh == 1 && p.sxr % 4 == 0 && p.sxb % 4 == 0 &&
+  return !p.no_split && p.wpk && p.Cin % 128 == 0 && p.M % 4 == 0 && p.nh == 1 && p.sxr % 4 == 0 && p.sxb % 4 == 0 &&
          split_group(p, 64, 1) > 0 && split_group(p, 32, 1) > 0;
 }
 
@@ -948,6 +955,19 @@ long long conv_split_ws_bytes(int taps, int Cin, int M, int rows) {
   return cg ? (long long)split_slices(q, cg) * rows * M * 4 : 0;
 }
 
+// The packed kernel and the reduce + LayerNorm kernels it hands to address y, the residuals and
+// the split-K partials through buffer descriptors with 32-bit byte offsets (num_records
+// 0x7fffffff): past 2 GiB a load would read 0 and a store would be dropped.  Launches whose
+// arrays reach that take the per-utterance kernel (64-bit pointer arithmetic) instead.
+static bool packed_i32_ok(const ConvParams& p, int S) {
+  const long long lim = 0x7fffff00LL;
+  const long long F = (long long)p.B * p.x_rows;
+  if ((long long)S * F * p.M * 4 >= lim) return false;             // split-K partials ws[S][F][M]
+  if ((long long)p.B * p.syb * 4 >= lim) return false;             // y / ln_out
+  if ((p.r1 || p.r2) && (long long)p.B * p.srb * 4 >= lim) return false;  // residuals
+  return true;
+}
+
 static thread_local int g_split_kernels = 1;
 int conv_split_last_kernels() { return g_split_kernels; }
 
@@ -956,7 +976,7 @@ hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done) 
   g_split_kernels = 1;
   if (packed_ok(p)) {
     const int cg = packed_group(p);
-    if (cg) {
+    if (cg && packed_i32_ok(p, split_slices(p, cg))) {
       const int S = split_slices(p, cg);
       const int gps = p.Cin / cg / S;
       const int F = p.B * p.x_rows;

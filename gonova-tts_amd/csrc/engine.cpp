@@ -698,6 +698,26 @@ int tts_acoustic_speaker_dim(tts_engine* eng, int* dim) {
   });
 }
 
+int tts_acoustic_range_flag(tts_engine* eng, int32_t* dst, void* stream) {
+  return guarded(eng, [&] {
+    if (!eng->finalized || !eng->ac.loaded) throw TtsError(TTS_ERR_STATE, "acoustic weights not loaded");
+    if (!dst) throw TtsError(TTS_ERR_INVALID, "null dst");
+    tts_engine::CallOrder order(eng, (hipStream_t)stream);
+    eng->ac.range_flag_to(dst, (hipStream_t)stream);
+  });
+}
+
+int tts_acoustic_set_precision(tts_engine* eng, int precision) {
+  return guarded(eng, [&] {
+    if (!eng->finalized || !eng->ac.loaded) throw TtsError(TTS_ERR_STATE, "acoustic weights not loaded");
+    if (precision != TTS_ENCODER_EXACT && precision != TTS_ENCODER_F32)
+      throw TtsError(TTS_ERR_INVALID, "precision must be TTS_ENCODER_EXACT or TTS_ENCODER_F32");
+    if (!eng->ac.split_encoder())
+      throw TtsError(TTS_ERR_INVALID, "only a 16-bit model created with TTS_ENCODER_EXACT switches encoder precision");
+    eng->ac.set_encoder_f32(precision == TTS_ENCODER_F32);
+  });
+}
+
 int tts_engine_profile(tts_engine* eng, int enable) {
   return guarded(eng, [&] { eng->prof.on = enable != 0; });
 }

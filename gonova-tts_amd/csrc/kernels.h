@@ -52,6 +52,12 @@ struct ConvParams {
   const float* ln_lin_w;
   float ln_lin_b;
   float* ln_lin_out;
+  // Range guard of the split-precision fp32 GEMMs (conv_split.hip): a staged operand outside f16's
+  // range (|x| >= 65520 or NaN) ORs 1 into *range_flag (nullable).  no_split: run an fp32 conv on
+  // the exact fp32 MFMA path (conv_gemm_kernel<float>) even where the split form is eligible --
+  // the fallback of the exact encoder when its range guard tripped (tts_acoustic_set_precision).
+  int* range_flag;
+  int no_split;
 };
 
 inline ConvParams conv_params_default() {

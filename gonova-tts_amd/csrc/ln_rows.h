@@ -4,13 +4,16 @@
 // reduction everywhere, so a fused LayerNorm is bit-identical to the separate launch.
 //
 // Fused form: the blocks that produce one row tile (its M blocks) each store their part with
-// write-through (sc1) stores, drain them and add to the tile's counter; the last to arrive
-// acquires at agent scope and normalises the tile's rows (cdna_hip_programming.md Guideline 16,
+// write-through (sc1) stores, drain them, release at agent scope and add to the tile's counter;
+// the last to arrive acquires at agent scope and normalises the tile's rows (cdna_hip_programming.md Guideline 16,
 // the counter form of the R1 hand-off).  Counters start at 0 (the workspace is zeroed when it is
 // allocated) and the last arriver puts its counter back to 0 for the next launch.
 #pragma once
 #include "common.h"
 
+#ifndef TTS_LN_RELEASE
+#define TTS_LN_RELEASE 1  // 0: A/B builds -- the sc1 parts + relaxed ticket of round 3, no release fence
+#endif
 #ifndef TTS_LN_FENCE
 #define TTS_LN_FENCE 0  // diagnostic builds: __threadfence() in the last arriver instead of the agent acquire
 #endif
@@ -188,6 +191,13 @@ __device__ inline bool ln_tile_last(int* cnt, int parts, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
   __syncthreads();
   if (threadIdx.x == 0) {
+    // agent-scope release before the ticket (cdna_hip_programming.md Guideline 16 recipe): the
+    // parts are write-through already, the release makes the hand-off correct under the memory
+    // model and not only under sc1 semantics; the asm wait stays after the fence (Pitfall 12)
+#if TTS_LN_RELEASE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = t == parts - 1;
     if (last) {

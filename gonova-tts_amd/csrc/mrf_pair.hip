@@ -46,7 +46,20 @@
 
 #include <algorithm>
 
+#ifndef TTS_PAIR_STAMP
+#define TTS_PAIR_STAMP 0  // diagnostic builds only: per-block phase timestamps (tools/pair_stamps.py)
+#endif
+
 namespace tts {
+
+#if TTS_PAIR_STAMP
+// Phase timestamps of the pair launches whose (C, k, d) match g_pair_stamp_target (the last such
+// launch of the workload wins), one record of 16 words per block: s_memtime at entry / input tile
+// staged / conv1 done / T written / conv2 done / output tile staged / row pass issued,
+// s_memrealtime at entry and end, and the hardware ids (XCC, SE, CU).  Never built into the product library.
+__device__ int g_pair_stamp_target[3];
+__device__ unsigned long long g_pair_stamp[1 << 21];
+#endif
 
 // conv_post fused into the vocoder's last pair (POST): the block computes PAIR_PO extra output
 // rows per side so conv_post's halo (post_k <= 2*PAIR_PO + 1 taps) is in the block
@@ -149,6 +162,14 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   static_assert(2 * A2 <= 16, "conv1 overrun within one tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
+#if TTS_PAIR_STAMP
+  unsigned long long stp[7] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0, 0, 0};
+  const unsigned long long rtp0 = __builtin_amdgcn_s_memrealtime();
+  const bool stamp_on = C == g_pair_stamp_target[0] && p.k == g_pair_stamp_target[1] && p.d == g_pair_stamp_target[2];
+#define TTS_PSTAMP(i_) stp[i_] = __builtin_amdgcn_s_memtime()
+#else
+#define TTS_PSTAMP(i_) (void)0
+#endif
   int b, tile0;
   if (!xcd_tile((p.T + BN - 1) / BN, p.B, b, tile0)) return;
   const int n0 = tile0 * BN;
@@ -226,6 +247,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
     }
   }
   __syncthreads();
+  TTS_PSTAMP(1);
 
   // ---- conv1 over T rows [0, 16*NT1): T row t <-> global row n0 - PO - a2 + t ----
   // Tiles are dealt round-robin to the WN waves of an M slice; a wave whose share is one
@@ -240,6 +262,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   pair_conv<T, C, S, NU1, D, MT, (C >= TTS_PAIR_MTO_MIN), 16 * WN * RS>(acc1, ring, w1, Gs + (16 * wn + l15) * RS, d * RS,
                                                                         d, l15, lq, last_off(NT1, NU1));
   __builtin_amdgcn_sched_barrier(0);
+  TTS_PSTAMP(2);
   // conv2's bias first, then its first weight steps (in flight during the conv1 epilogue): vmcnt
   // retires in order, so waiting for the bias does not wait for the weights
   f32x4 bias2[MT];
@@ -271,6 +294,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
       }
   }
   __syncthreads();
+  TTS_PSTAMP(3);
 
   constexpr int NIT = (BO * VPR + NTHR - 1) / NTHR;  // 16-byte row pieces per thread in the row pass
 
@@ -283,6 +307,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   pair_conv<T, C, S, NU2, D, MT, (C >= TTS_PAIR_MTO_MIN), 16 * WN * RS>(acc2, ring, w2, Ts + (16 * wn + l15) * RS, RS, 1,
                                                                         l15, lq, last_off(NT2, NU2));
   __builtin_amdgcn_sched_barrier(0);  // keep the epilogue's loads out of the MFMA tail
+  TTS_PSTAMP(4);
   // residual h (input rows) and, for accumulating launches, the MRF-sum rows in flight while
   // the tile is staged.  The sum is read through a buffer descriptor with no records when the
   // launch does not accumulate: the load is issued unconditionally (no branch for the waitcnt
@@ -315,6 +340,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
       }
   }
   __syncthreads();
+  TTS_PSTAMP(5);
   if constexpr (POST) {
     // final MRF-sum rows (rounded to T as the unfused path stores them) -> lrelu -> LDS tile
     // [BO][32] (chunk c of row r at c ^ ((r >> 2) & 3), conv_post16's layout), then conv_post
@@ -375,7 +401,19 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
     if constexpr (OUTACT) v = lrelu_unit<T>(v, p.out_slope);
     store16<TTS_ROW_STORE>(Y, (int)((dst - Y) * (long long)sizeof(T)), v);
   }
+#if TTS_PAIR_STAMP
+  TTS_PSTAMP(6);
+  if (stamp_on && tid == 0 && blockIdx.x < (1u << 17)) {
+    unsigned long long* r = g_pair_stamp + blockIdx.x * 16;
+    for (int i = 0; i < 7; ++i) r[i] = stp[i];
+    r[7] = rtp0;
+    r[8] = __builtin_amdgcn_s_memrealtime();
+    r[9] = ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11)) << 32) |
+           (unsigned)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+  }
+#endif
 }
+#undef TTS_PSTAMP
 
 #ifndef TTS_PAIR_SHORT
 #define TTS_PAIR_SHORT 128             // short tiles below this many full-height blocks (0: never)
@@ -475,5 +513,21 @@ hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t
   if (C == 256) return launch_pair_k<bf16_t, 256>(p, s);
   return launch_pair_k<bf16_t, 128>(p, s);
 }
+
+#if TTS_PAIR_STAMP
+extern "C" int tts_debug_pair_target(int C, int k, int d) {  // also clears the records
+  const int t[3] = {C, k, d};
+  void* buf = nullptr;
+  if (hipDeviceSynchronize() != hipSuccess || hipGetSymbolAddress(&buf, HIP_SYMBOL(g_pair_stamp)) != hipSuccess ||
+      hipMemset(buf, 0, sizeof(unsigned long long) << 21) != hipSuccess)
+    return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_pair_stamp_target), t, sizeof(t)) == hipSuccess ? 0 : -1;
+}
+extern "C" int tts_debug_pair_stamps(unsigned long long* host, long long words) {
+  const long long n = words < (1LL << 21) ? words : (1LL << 21);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pair_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace tts

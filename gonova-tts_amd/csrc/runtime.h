@@ -267,7 +267,7 @@ inline void run_layer(const ConvLayer& L, const void* x, int x_rows, const int* 
                       int dt, hipStream_t s, Profiler* prof, float in_slope = 1.f, int act = ACT_NONE,
                       float alpha = 1.f, const void* r1 = nullptr, const void* r2 = nullptr, float out_scale = 1.f,
                       int x_ld = 0, int y_ld = 0, int rows_pad = 0, float* ws = nullptr, long long ws_bytes = 0,
-                      const ConvParams* ln = nullptr) {
+                      const ConvParams* ln = nullptr) {  // ln: LayerNorm fields, range_flag, no_split
   ConvParams p = conv_params_default();
   const int xl = x_ld ? x_ld : L.Cin, yl = y_ld ? y_ld : L.M;
   p.x = x; p.sxb = (long long)x_rows * xl; p.sxr = xl; p.x_len = lens; p.x_rows = x_rows;
@@ -284,6 +284,7 @@ inline void run_layer(const ConvLayer& L, const void* x, int x_rows, const int* 
     p.ln_eps = ln->ln_eps;
     p.ln_cnt = ln->ln_cnt; p.ln_cnt_n = ln->ln_cnt_n;
     p.ln_lin_w = ln->ln_lin_w; p.ln_lin_b = ln->ln_lin_b; p.ln_lin_out = ln->ln_lin_out;
+    p.range_flag = ln->range_flag; p.no_split = ln->no_split;  // (the split path's guard / fallback)
   }
   launch_conv_checked(p, dt, s, prof, 2.0 * L.M * (double)L.Cin * L.taps * (double)B * y_rows);
 }

@@ -35,6 +35,7 @@ class TtsConfig(ctypes.Structure):
 
 
 ENCODER_PRECISION = {"exact": 0, "fast": 1}
+ENCODER_F32 = 2  # TTS_ENCODER_F32: run-time fallback of "exact" (tts_acoustic_set_precision)
 
 
 class TtsConvDesc(ctypes.Structure):
@@ -72,6 +73,8 @@ C_API = [
     ("tts_acoustic_forward", _I, [_VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _I, _VP, _VP]),
     ("tts_acoustic_forward_spk", _I, [_VP, _VP, _VP, _I, _I, _VP, _VP, _I, _VP, _VP, _I, _VP, _VP]),
     ("tts_acoustic_speaker_dim", _I, [_VP, ctypes.POINTER(ctypes.c_int)]),
+    ("tts_acoustic_range_flag", _I, [_VP, _VP, _VP]),
+    ("tts_acoustic_set_precision", _I, [_VP, _I]),
     ("tts_engine_profile", _I, [_VP, _I]),
     ("tts_engine_profile_read", _I, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_int)]),
@@ -198,6 +201,11 @@ class HipEngine:
         check(self.lib.tts_engine_create_sized(self.device_index, ctypes.byref(cfg), ctypes.sizeof(cfg),
                                                ctypes.byref(h)), "tts_engine_create")
         self.handle = h
+        # range guard of the exact encoder of a 16-bit model (include/tts_hip.h, ABI 4): every
+        # acoustic forward also enqueues a copy of the engine's range word, which the caller reads
+        # at its next host sync (GonovaTTS) and answers with an fp32-MFMA rerun when it is set
+        self.range_guard = encoder_precision == "exact" and DTYPES[acoustic_dtype] != 0
+        self.range_fallbacks = 0
         self.hop = 256
         self._finalized = False
         self.has_vocoder = False
@@ -291,10 +299,28 @@ class HipEngine:
         check(self.lib.tts_acoustic_speaker_dim(self.handle, ctypes.byref(d)), "tts_acoustic_speaker_dim")
         return d.value
 
+    def set_encoder_precision(self, precision: str):
+        """"exact" (split-precision, the default) or "f32" (exact fp32 MFMA: the range guard's
+        fallback) for later acoustic forwards of a 16-bit model created with "exact"."""
+        code = {"exact": ENCODER_PRECISION["exact"], "f32": ENCODER_F32}[precision]
+        check(self.lib.tts_acoustic_set_precision(self.handle, code), "tts_acoustic_set_precision")
+
+    @contextlib.contextmanager
+    def encoder_f32(self):
+        """Acoustic forwards inside the block run the encoder on the fp32 MFMA path."""
+        self.set_encoder_precision("f32")
+        try:
+            yield
+        finally:
+            self.set_encoder_precision("exact")
+
     def acoustic(self, tokens, tok_lens, t_cap: int, durations=None, stream=None, return_durations=False,
-                 speaker_embedding=None):
+                 speaker_embedding=None, return_range=False):
         """tokens: cuda int32 [B, N]; returns (mel [B, t_cap, 80] f32, mel_lens int32 [B]).
-        speaker_embedding: optional float32 [B, E] (HF:1192-1196), E = speaker_dim."""
+        speaker_embedding: optional float32 [B, E] (HF:1192-1196), E = speaker_dim.
+        return_range: also return the range word of this forward (cuda int32 [1], nonzero when a
+        split-precision operand was outside f16's range; None without the guard), enqueued on the
+        same stream -- read it at the next host sync."""
         import torch
         tokens = tokens.to(dtype=torch.int32).contiguous()
         tok_lens = tok_lens.to(device=tokens.device, dtype=torch.int32).contiguous()
@@ -316,9 +342,13 @@ class HipEngine:
                                                 ctypes.c_void_p(mel.data_ptr()), ctypes.c_void_p(mel_lens.data_ptr()),
                                                 t_cap, ctypes.c_void_p(dur_out.data_ptr()), _stream_ptr(stream)),
               "tts_acoustic_forward")
-        if return_durations:
-            return mel, mel_lens, dur_out
-        return mel, mel_lens
+        rw = None
+        if self.range_guard:
+            rw = torch.empty((1,), dtype=torch.int32, device=tokens.device)
+            check(self.lib.tts_acoustic_range_flag(self.handle, ctypes.c_void_p(rw.data_ptr()), _stream_ptr(stream)),
+                  "tts_acoustic_range_flag")
+        out = (mel, mel_lens, dur_out) if return_durations else (mel, mel_lens)
+        return out + (rw,) if return_range else out
 
     def profile(self, enable: bool = True):
         check(self.lib.tts_engine_profile(self.handle, int(enable)), "profile")

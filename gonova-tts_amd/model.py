@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import os
 import threading
+from contextlib import contextmanager
 from math import gcd
 from typing import Dict, List, Optional
 
@@ -123,7 +124,13 @@ class GonovaTTS:
                           stream=None, speaker_embedding: Optional[np.ndarray] = None, host_lens: bool = True):
         """tokens int32 [B, N], lens [B] -> (wav cuda float32 [B, T*256], wav_lens np.int64 [B]).
         host_lens=False returns wav_lens as a cuda int64 tensor instead: no host sync, so a caller
-        can queue several batches back to back (dist.ShardedSynthesis)."""
+        can queue several batches back to back (dist.ShardedSynthesis).
+
+        Range guard (include/tts_hip.h, ABI 4): with the exact encoder of a 16-bit model the
+        acoustic forward's range word travels with the one host read this path makes anyway; when a
+        split-precision operand was outside f16's range the batch is synthesized again with the
+        encoder on the exact fp32 MFMA kernels (`range_fallbacks` counts these).  host_lens=False
+        makes no host read, so no word is read there."""
         import torch
         dev = self.engine.torch_device
         B, N = tokens.shape
@@ -133,28 +140,69 @@ class GonovaTTS:
         t_cap = max(64, int(self.FRAMES_PER_TOKEN_CAP * N))
         if durations is not None:
             t_cap = max(1, int(np.asarray(durations).sum(axis=1).max()))
-        spk = speaker_embedding
-        mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True,
-                                                  speaker_embedding=spk)
+        args = (tok, tl, dd, t_cap, stream, speaker_embedding, host_lens)
+        # the engine's device is the current one for this thread (the streams torch hands out, the
+        # ops below): an executor thread of a multi-GPU service starts on device 0
+        with torch.cuda.device(self.engine.device_index):
+            wav, wav_lens, tripped = self._synthesize_once(*args)
+            if tripped:
+                with self._range_fallback():
+                    wav, wav_lens, _ = self._synthesize_once(*args)
+        return wav, wav_lens
+
+    @property
+    def range_fallbacks(self) -> int:
+        """Forwards rerun on the fp32 encoder because the exact encoder's range guard tripped."""
+        return self.engine.range_fallbacks
+
+    @contextmanager
+    def _range_fallback(self):
+        import warnings
+        self.engine.range_fallbacks += 1
+        warnings.warn("acoustic encoder activations outside the f16 range of the split-precision GEMMs: "
+                      "rerunning this batch with the encoder on fp32 MFMA (include/tts_hip.h, TTS_ENCODER_F32)",
+                      RuntimeWarning, stacklevel=3)
+        with self.engine.encoder_f32():
+            yield
+
+    def _synthesize_once(self, tok, tl, dd, t_cap, stream, spk, host_lens):
+        """-> (wav, wav_lens, range guard tripped: bool, or None when nothing was read)"""
+        import torch
+        mel, mel_lens, dur, rw = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream,
+                                                      return_durations=True, speaker_embedding=spk, return_range=True)
         lens_known = None
-        if durations is None:
-            # one host read for both the frames the durations need and the frame counts
-            need, lens_known = _need_and_lens(dur, mel_lens)
+        tripped = None
+        if dd is None:
+            # one host read for the frames the durations need, the frame counts and the range word
+            need, lens_known, tripped = _need_and_lens(dur, mel_lens, rw)
+            if tripped:
+                return None, None, True
             if need > t_cap:  # exact second pass with the predicted durations and a fitting cap
-                mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
-                                                          return_durations=True, speaker_embedding=spk)
-                need, lens_known = _need_and_lens(dur, mel_lens)
+                mel, mel_lens, dur, rw = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
+                                                              return_durations=True, speaker_embedding=spk,
+                                                              return_range=True)
+                need, lens_known, tripped = _need_and_lens(dur, mel_lens, rw)
+                if tripped:
+                    return None, None, True
         wav = self.engine.vocoder(mel, mel_lens, stream=stream)
         if self.sr != self.native_sr:
             g = gcd(self.sr, self.native_sr)
             wav, out_lens = self.engine.resample(wav, mel_lens * self.vocoder_cfg.hop, self.sr // g,
                                                  self.native_sr // g, stream=stream)
             out_lens = out_lens.to(torch.int64)
-            return wav, (out_lens.cpu().numpy() if host_lens else out_lens)
+            if not host_lens:
+                return wav, out_lens, None
+            if tripped is None:
+                h, tripped = _read_with_range(out_lens, rw)
+                return wav, h, tripped
+            return wav, out_lens.cpu().numpy(), tripped
         if host_lens and lens_known is not None:  # already on the host: no second sync
-            return wav, lens_known * self.vocoder_cfg.hop
+            return wav, lens_known * self.vocoder_cfg.hop, tripped
         wav_lens = mel_lens.to(torch.int64) * self.vocoder_cfg.hop
-        return wav, (wav_lens.cpu().numpy() if host_lens else wav_lens)
+        if not host_lens:
+            return wav, wav_lens, None
+        h, tripped = _read_with_range(wav_lens, rw)
+        return wav, h, tripped
 
     # -------------------------------------------------------------- streaming
     STREAM_CONTEXT = 16  # mel frames of context per side; HiFi-GAN V1's receptive field is < 13
@@ -171,6 +219,11 @@ class GonovaTTS:
         Chunks are at the vocoder's native 22,050 Hz whatever `sr` is (a resampled stream would
         need the resampler's own filter context across chunk edges)."""
         import torch
+        with torch.cuda.device(self.engine.device_index):  # (see synthesize_tokens)
+            yield from self._stream_tokens(tokens, lens, chunk_frames, context, durations, stream, speaker_embedding)
+
+    def _stream_tokens(self, tokens, lens, chunk_frames, context, durations, stream, speaker_embedding):
+        import torch
         ctx = self.STREAM_CONTEXT if context is None else context
         dev = self.engine.torch_device
         B, N = tokens.shape
@@ -180,8 +233,8 @@ class GonovaTTS:
         t_cap = max(64, int(self.FRAMES_PER_TOKEN_CAP * N)) if durations is None else \
             max(1, int(np.asarray(durations).sum(axis=1).max()))
         spk = speaker_embedding
-        mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True,
-                                                  speaker_embedding=spk)
+        mel, mel_lens, dur, rw = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream, return_durations=True,
+                                                      speaker_embedding=spk, return_range=True)
         first = None  # (window end, kept frames, chunk) enqueued ahead of the host read
         if durations is None:
             # The first chunk's window needs no host value when the longest utterance covers it
@@ -193,12 +246,25 @@ class GonovaTTS:
             if os.environ.get("TTS_STREAM_EARLY", "1") != "0":  # (0: the host read first, A/B runs)
                 win_lens = torch.clamp(mel_lens, min=0, max=w1).to(torch.int32)
                 first = (w1, tc, self.engine.vocoder_chunk(mel[:, :w1].contiguous(), win_lens, 0, tc, stream=stream))
-            need, lens_h = _need_and_lens(dur, mel_lens)  # one host read before the first chunk
+            need, lens_h, tripped = _need_and_lens(dur, mel_lens, rw)  # one host read before the first chunk
+            fell_back = False
+            if tripped:  # range guard: the acoustic pass again on the fp32 encoder
+                first, fell_back = None, True
+                with self._range_fallback():
+                    mel, mel_lens, dur = self.engine.acoustic(tok, tl, t_cap, durations=None, stream=stream,
+                                                              return_durations=True, speaker_embedding=spk)
+                need, lens_h, _ = _need_and_lens(dur, mel_lens)
             if need > t_cap:
                 first = None
-                mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
-                                                          return_durations=True, speaker_embedding=spk)
-                need, lens_h = _need_and_lens(dur, mel_lens)
+                mel, mel_lens, dur, rw = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
+                                                              return_durations=True, speaker_embedding=spk,
+                                                              return_range=True)
+                need, lens_h, tripped = _need_and_lens(dur, mel_lens, rw)
+                if tripped and not fell_back:
+                    with self._range_fallback():
+                        mel, mel_lens, dur = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
+                                                                  return_durations=True, speaker_embedding=spk)
+                    need, lens_h, _ = _need_and_lens(dur, mel_lens)
         else:
             # given durations fix the frame counts on the host: no device sync between the
             # acoustic pass and the first chunk's vocoder launches (same-box C5: neutral, the
@@ -216,6 +282,16 @@ class GonovaTTS:
                 win = mel[:, w0:w1].contiguous()
                 win_lens = torch.clamp(mel_lens - w0, min=0, max=w1 - w0).to(torch.int32)
                 wav = self.engine.vocoder_chunk(win, win_lens, c0 - w0, tc, stream=stream)
+            if c0 == 0 and durations is not None and rw is not None:
+                # given durations made no host read so far: the range word is read here, where the
+                # consumer would wait for this chunk anyway; out of range -> fp32 encoder, chunk again
+                if int(rw.item()) != 0:
+                    with self._range_fallback():
+                        mel, mel_lens = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream,
+                                                             speaker_embedding=spk)
+                    win = mel[:, w0:w1].contiguous()
+                    win_lens = torch.clamp(mel_lens - w0, min=0, max=w1 - w0).to(torch.int32)
+                    wav = self.engine.vocoder_chunk(win, win_lens, c0 - w0, tc, stream=stream)
             first = None
             valid = np.clip(lens_h - c0, 0, tc) * hop
             yield c0, wav, valid
@@ -278,7 +354,7 @@ class GonovaTTS:
             for idx, spk in groups:
                 tokens, lens = tokenize_batch([texts[i] for i in idx])
                 wav, wav_lens = self.synthesize_tokens(tokens, lens, speaker_embedding=spk)
-                host = wav.cpu().numpy()
+                host = wav.cpu().numpy()  # (a tensor's copy runs on its own device's stream)
                 for r, i in enumerate(idx):
                     out[i] = host[r, : int(wav_lens[r])].astype(np.float32, copy=False)
         return out
@@ -332,14 +408,27 @@ class GonovaTTS:
 ChatterboxTTS = GonovaTTS
 
 
-def _need_and_lens(dur, mel_lens):
+def _need_and_lens(dur, mel_lens, rw=None):
     """One device -> host read: (frames the used durations add up to at most, the frame counts
-    np.int64 [B]) -- the durations kernel's all-zero rule gives an utterance len frames, so the
-    need is the larger of the two per utterance."""
+    np.int64 [B], the range word is set) -- the durations kernel's all-zero rule gives an
+    utterance len frames, so the need is the larger of the two per utterance."""
     import torch
-    h = torch.stack([dur.sum(dim=1).to(torch.int64), mel_lens.to(torch.int64)]).cpu().numpy()
-    need = int(np.maximum(h[0], h[1]).max()) if h.shape[1] else 0
-    return need, h[1].astype(np.int64)
+    rows = torch.stack([dur.sum(dim=1).to(torch.int64), mel_lens.to(torch.int64)]).reshape(-1)
+    if rw is not None:
+        rows = torch.cat([rows, rw.to(torch.int64)])
+    h = rows.cpu().numpy()
+    B = mel_lens.shape[0]
+    need = int(np.maximum(h[:B], h[B:2 * B]).max()) if B else 0
+    return need, h[B:2 * B].astype(np.int64), bool(rw is not None and h[2 * B] != 0)
+
+
+def _read_with_range(lens, rw=None):
+    """lens (cuda int64 [B]) and the range word in one device -> host read."""
+    import torch
+    if rw is None:
+        return lens.cpu().numpy(), False
+    h = torch.cat([lens, rw.to(torch.int64)]).cpu().numpy()
+    return h[:-1], bool(h[-1] != 0)
 
 
 def _mel_lens_host(lens: np.ndarray, durations: np.ndarray, t_cap: int) -> np.ndarray:

@@ -13,6 +13,13 @@ Requests that ask for sub-sentence frames (`stream_frames` > 0) run through
 `synth_stream` (`GonovaTTS.stream_batch`) in batches of their own: each vocoder chunk's
 pieces go out as soon as they reach the host, still in sentence order per request.
 
+Several GPUs (opt-in, `synth_batches` with one callable per local engine): the per-sentence
+engine batches of a round are dealt across the engines with `dist.plan_buckets` (longest
+sentence first to the least-loaded engine, each engine's share cut into length-sorted batches of
+`max_sentences`), and the engines run at the same time, one executor thread each; frames still
+leave in per-request sentence order.  The reference can only run one server process per GPU
+behind a load balancer (`server.py:397-400,486-488`).  Streamed requests stay on the first engine.
+
 Failure: the reference logs and swallows synthesis errors, so the client never gets a
 final marker (`server.py:173-179`).  That stays the default; `notify_errors=True` sends
 `{"type": "synthesis_error", "message": ...}` plus the final marker instead.
@@ -34,9 +41,13 @@ logger = logging.getLogger(__name__)
 class DynamicBatcher:
     def __init__(self, queues, synth_batch: Callable[[List[str]], List[np.ndarray]], max_sentences: int = 32,
                  max_requests: int = 64, max_wait: float = 0.004, notify_errors: bool = False,
-                 send_error: Optional[Callable] = None, synth_stream: Optional[Callable] = None):
+                 send_error: Optional[Callable] = None, synth_stream: Optional[Callable] = None,
+                 sample_rate: int = 22050, synth_batches: Optional[List[Callable]] = None):
         self.queues = queues
+        self.sample_rate = float(sample_rate)  # the rate the engine's audio is in (model.sr)
         self.synth_batch = synth_batch
+        # one synth_batch per local engine (GPU); a single engine is the reference-shaped default
+        self.synth_batches = list(synth_batches) if synth_batches else [synth_batch]
         self.max_sentences = max_sentences
         self.max_requests = max_requests
         self.max_wait = max_wait
@@ -45,7 +56,8 @@ class DynamicBatcher:
         self.synth_stream = synth_stream  # model.stream_batch: sub-sentence frames (opt-in per request)
         self.running = False
         self.stats = {"rounds": 0, "engine_batches": 0, "sentences": 0, "requests": 0, "errors": 0,
-                      "audio_seconds": 0.0, "busy_seconds": 0.0, "max_batch_seen": 0}
+                      "audio_seconds": 0.0, "busy_seconds": 0.0, "max_batch_seen": 0,
+                      "engine_sentences": [0] * len(self.synth_batches)}
 
     async def run(self):
         self.running = True
@@ -81,7 +93,13 @@ class DynamicBatcher:
         sent = [0] * len(reqs)    # frames sent: the chunk_id of the next frame / the final marker
         finished = [False] * len(reqs)
 
+        flush_lock = asyncio.Lock()  # engines finishing together must not send a piece twice
+
         async def flush():
+            async with flush_lock:
+                await flush_locked()
+
+        async def flush_locked():
             for i, r in enumerate(reqs):
                 if finished[i]:
                     continue
@@ -113,28 +131,32 @@ class DynamicBatcher:
         batches = []
         for f in sorted(groups, key=lambda f: (f == 0, f)):
             ks = sorted(groups[f], key=lambda k: len(work[k][2]))
-            batches += [(f, ks[b0:b0 + self.max_sentences]) for b0 in range(0, len(ks), self.max_sentences)]
+            if f == 0 and len(self.synth_batches) > 1:
+                continue  # dealt across the engines below
+            batches += [(f, ks[b0:b0 + self.max_sentences], 0) for b0 in range(0, len(ks), self.max_sentences)]
 
-        for frames, chunk in batches:
+        async def one_batch(frames, chunk, eng):
             texts = [work[k][2] for k in chunk]
             voices = [getattr(reqs[work[k][0]], "voice", None) for k in chunk]
             # per-sentence voice (registered embedding) only when one is set
             kw = {"speaker_embeddings": voices} if any(v is not None for v in voices) else {}
+            synth = self.synth_batches[eng]
             try:
                 if frames == 0:
-                    audios = await loop.run_in_executor(None, lambda: self.synth_batch(texts, **kw))
+                    audios = await loop.run_in_executor(None, lambda: synth(texts, **kw))
                     for k, a in zip(chunk, audios):
                         i, j, _ = work[k]
                         pending[i][j].append(a)
                         done[i][j] = True
-                        self.stats["audio_seconds"] += len(a) / 22050.0
+                        self.stats["audio_seconds"] += len(a) / self.sample_rate
+                    self.stats["engine_sentences"][eng] += len(chunk)
                 else:
                     async def deliver(pieces):
                         for t, a, fin in pieces:
                             i, j, _ = work[chunk[t]]
                             if len(a):
                                 pending[i][j].append(a)
-                                self.stats["audio_seconds"] += len(a) / 22050.0
+                                self.stats["audio_seconds"] += len(a) / self.sample_rate
                             done[i][j] = done[i][j] or fin
                         await flush()
                     await self._stream(loop, texts, frames, kw, deliver)
@@ -148,39 +170,69 @@ class DynamicBatcher:
                         if self.notify_errors and self.send_error is not None:
                             await self.send_error(reqs[i].connection_id, str(e))
                 await flush()
-                continue
+                return
             self.stats["engine_batches"] += 1
             self.stats["sentences"] += len(chunk)
             self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(chunk))
             await flush()
+
+        for frames, chunk, eng in batches:
+            await one_batch(frames, chunk, eng)
+        if len(self.synth_batches) > 1 and 0 in groups:
+            # per-sentence batches across the engines: longest-first to the least-loaded engine
+            # (load = characters), each engine's share in length-sorted batches, engines concurrent
+            from ..dist import plan_buckets
+            ks = groups[0]
+            plan = plan_buckets([len(work[k][2]) for k in ks], len(self.synth_batches), self.max_sentences)
+
+            async def engine_run(eng, buckets):
+                for bk in buckets:
+                    await one_batch(0, [ks[u] for u in bk], eng)
+
+            await asyncio.gather(*(engine_run(e, bks) for e, bks in enumerate(plan) if bks))
         await flush()
 
     async def _stream(self, loop, texts, frames, kw, deliver):
         """Run `synth_stream` (a generator of per-chunk pieces) on an executor thread and hand
         each chunk to `deliver` on the event loop as soon as it is on the host, so the first
-        frames go out while the vocoder still works on the rest of the batch."""
+        frames go out while the vocoder still works on the rest of the batch.
+
+        If `deliver` raises or this coroutine is cancelled, the producer is told to stop: it
+        checks the event between chunks and closes the generator (which releases the model's
+        lock), so no thread keeps synthesizing for nobody and the next engine batch is not
+        held behind it.  The producer's future is always awaited, so its exception is read."""
+        import threading
         q: asyncio.Queue = asyncio.Queue()
         end = object()
+        stop = threading.Event()
 
         def produce():
+            gen = self.synth_stream(texts, frames, **kw)
             try:
-                for item in self.synth_stream(texts, frames, **kw):
+                for item in gen:
+                    if stop.is_set():
+                        break
                     loop.call_soon_threadsafe(q.put_nowait, item)
             except BaseException as e:  # noqa: BLE001 -- re-raised on the loop
                 loop.call_soon_threadsafe(q.put_nowait, e)
                 return
+            finally:
+                gen.close()
             loop.call_soon_threadsafe(q.put_nowait, end)
 
         fut = loop.run_in_executor(None, produce)
-        while True:
-            item = await q.get()
-            if item is end:
-                break
-            if isinstance(item, BaseException):
-                await fut
-                raise item
-            await deliver(item)
-        await fut
+        try:
+            while True:
+                item = await q.get()
+                if item is end:
+                    break
+                if isinstance(item, BaseException):
+                    raise item
+                await deliver(item)
+        finally:
+            stop.set()
+            # the producer ends within one chunk; its own exception (if any) was raised above
+            await asyncio.shield(asyncio.gather(fut, return_exceptions=True))
 
     def stop(self):
         self.running = False

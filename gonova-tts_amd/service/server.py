@@ -38,6 +38,11 @@ from .queues import TTSQueueManager
 logger = logging.getLogger(__name__)
 
 
+# smallest sub-sentence frame (mel frames) a request gets: 2 x GonovaTTS.STREAM_CONTEXT, so a
+# chunk's window is at most half context
+MIN_STREAM_FRAMES = 32
+
+
 # the sentences the reference warms its model up with, in order (synthesizer.py:197-207)
 WARMUP_TEXTS = ("Hello.", "Hello, this is a warmup test.",
                 "The quick brown fox jumps over the lazy dog, and this is a longer sentence to warm up the model properly.")
@@ -65,8 +70,15 @@ class RateLimiter:
 class TTSService:
     def __init__(self, model_factory: Callable, max_connections: int = 50, chunk_size: int = 50,
                  max_sentences: int = 32, max_wait: float = 0.004, notify_errors: bool = False,
-                 device: str = "cuda", device_index: int = 0, stream_frames: int = 0):
+                 device: str = "cuda", device_index: int = 0, stream_frames: int = 0,
+                 min_stream_frames: int = MIN_STREAM_FRAMES, devices: Optional[list] = None):
+        """devices: opt-in fan-out over the node's GPUs, e.g. ["cuda:0", "cuda:1"]: model_factory is
+        then called once per device (model_factory(device)) and the batcher deals each round's
+        sentences across the engines (batcher.py); default None = one model_factory() model, the
+        reference's one-GPU-per-process shape (server.py:397-400)."""
         self.model_factory = model_factory
+        self.devices = list(devices) if devices else None
+        self.models = []
         self.max_connections = max_connections
         self.chunk_size = chunk_size
         self.device = device
@@ -83,22 +95,49 @@ class TTSService:
         self.max_sentences = max_sentences
         self.max_wait = max_wait
         self.notify_errors = notify_errors
-        self.stream_frames = _frames(stream_frames)
+        self.min_stream_frames = max(1, int(min_stream_frames))
+        self.stream_frames = self._stream_frames(stream_frames)
         self._task = None
 
     async def start(self):
         loop = asyncio.get_running_loop()
-        self.model = await loop.run_in_executor(None, self.model_factory)
-        for text in WARMUP_TEXTS:  # the reference's three warmups (synthesizer.py:197-207)
-            await loop.run_in_executor(None, self.model.generate_batch, [text])
-        self.queues = TTSQueueManager(sample_rate=getattr(self.model, "sr", 22050))
+        if self.devices:
+            self.models = [await loop.run_in_executor(None, self.model_factory, d) for d in self.devices]
+        else:
+            self.models = [await loop.run_in_executor(None, self.model_factory)]
+        self.model = self.models[0]
+        for m in self.models:
+            for text in WARMUP_TEXTS:  # the reference's three warmups (synthesizer.py:197-207)
+                await loop.run_in_executor(None, m.generate_batch, [text])
+        if self.stream_frames and not self.can_stream():
+            raise ValueError("stream_frames needs the vocoder's native sample rate: this model resamples "
+                             f"to {getattr(self.model, 'sr', None)} Hz, which needs filter context across frames")
+        sr = getattr(self.model, "sr", 22050)
+        self.queues = TTSQueueManager(sample_rate=sr)
         await self.queues.start()
         self.batcher = DynamicBatcher(self.queues, self.model.generate_batch, max_sentences=self.max_sentences,
                                       max_wait=self.max_wait, notify_errors=self.notify_errors,
                                       send_error=self._send_error,
-                                      synth_stream=getattr(self.model, "stream_batch", None))
+                                      synth_stream=getattr(self.model, "stream_batch", None), sample_rate=sr,
+                                      synth_batches=[m.generate_batch for m in self.models])
         self._task = asyncio.create_task(self.batcher.run())
         self.is_loaded = True
+
+    def can_stream(self) -> bool:
+        """Sub-sentence frames come straight from the vocoder's chunks, at its native rate; a
+        model that resamples (e.g. to the 24 kHz the reference's clients assume) cannot cut its
+        output at chunk edges without the resampler's filter context (model.stream_batch)."""
+        m = self.model
+        return getattr(m, "stream_batch", None) is not None and getattr(m, "sr", 0) == getattr(m, "native_sr", getattr(m, "sr", 0))
+
+    def _stream_frames(self, v) -> int:
+        """A request's (or the service default's) `stream_frames`: 0 = one frame per sentence;
+        otherwise at least `min_stream_frames`.  Each vocoder chunk runs a window of the chunk plus
+        2 x STREAM_CONTEXT frames and one device-to-host copy, so a tiny value (1 frame: a 33-frame
+        window and a host sync per mel frame, ~860 chunks for a 10 s sentence) would let one
+        request hold the shared batcher for every other connection; smaller values round up."""
+        f = _frames(v)
+        return 0 if f == 0 else max(f, self.min_stream_frames)
 
     async def _send_error(self, conn_id: str, message: str):
         ws = self.sockets.get(conn_id)
@@ -118,9 +157,10 @@ class TTSService:
             await asyncio.gather(self._task, return_exceptions=True)
         if self.queues is not None:
             await self.queues.stop()
-        eng = getattr(self.model, "engine", None)
-        if eng is not None:
-            eng.close()
+        for m in self.models:
+            eng = getattr(m, "engine", None)
+            if eng is not None:
+                eng.close()
         self.is_loaded = False
 
     async def handle_connection(self, ws, conn_id: str):
@@ -180,7 +220,16 @@ class TTSService:
             text = data.get("text", "")
             if not isinstance(text, str):
                 raise ValueError("text must be a string")
-            frames = _frames(data.get("stream_frames", self.stream_frames))
+            try:
+                frames = self._stream_frames(data.get("stream_frames", self.stream_frames))
+                if frames and not self.can_stream():
+                    raise ValueError("stream_frames is not available: this model resamples to "
+                                     f"{getattr(self.model, 'sr', None)} Hz; omit it for one frame per sentence")
+            except ValueError as e:
+                # a request refused before it is queued: the client is told (reference error shape,
+                # server.py:244-247), instead of waiting for a marker that never comes
+                await ws.send_json({"type": "error", "message": f"Synthesis request refused: {e}"})
+                return
             # unknown voices fall back to the default voice (reference server.py:127-138)
             await self.queues.enqueue_request(
                 connection_id=conn_id, text=text, voice_id=vid,
@@ -221,6 +270,7 @@ class TTSService:
 
     def health(self):
         info = {"status": "healthy", "device": f"{self.device}:{self.device_index}",
+                "devices": list(self.devices) if self.devices else [f"{self.device}:{self.device_index}"],
                 "sample_rate": getattr(self.model, "sr", 22050), "active_connections": self.active_connections,
                 "queue_metrics": self.queues.get_metrics(), "synthesizer_stats": dict(self.batcher.stats),
                 "voice_stats": {"total_voices": len(self.voices)}}
@@ -248,11 +298,14 @@ def create_app(model_factory: Optional[Callable] = None, **service_kwargs):
     from fastapi.responses import JSONResponse
 
     if model_factory is None:
-        def model_factory():
+        def model_factory(device: str = "cuda:0"):
             from ..model import GonovaTTS
             sr = os.environ.get("TTS_SAMPLE_RATE")  # e.g. 24000: the rate the reference's clients assume
-            return GonovaTTS.from_pretrained(device="cuda:0", ckpt_dir=os.environ.get("TTS_CKPT_DIR"),
+            return GonovaTTS.from_pretrained(device=device, ckpt_dir=os.environ.get("TTS_CKPT_DIR"),
                                              sample_rate=int(sr) if sr else None)
+        if "devices" not in service_kwargs and os.environ.get("TTS_DEVICES"):
+            # e.g. TTS_DEVICES=cuda:0,cuda:1: one engine per listed GPU in this process
+            service_kwargs["devices"] = [d.strip() for d in os.environ["TTS_DEVICES"].split(",") if d.strip()]
 
     app = FastAPI(title="TTS Service (MI355X)", version="0.1.0")
     svc = TTSService(model_factory, **service_kwargs)

@@ -60,8 +60,10 @@ typedef struct tts_engine tts_engine;
  *   2  tts_config gains encoder_precision (sixth int)
  *   3  tts_engine_create_sized / tts_abi_version / tts_get_switch; stream ordering records
  *      on the caller's stream at the end of each call (a caller may destroy its stream after
- *      the call returns) */
-#define TTS_ABI_VERSION 3
+ *      the call returns)
+ *   4  range guard of the exact encoder: tts_acoustic_range_flag / tts_acoustic_set_precision,
+ *      TTS_ENCODER_F32 */
+#define TTS_ABI_VERSION 4
 int tts_abi_version(void);
 
 /* Engine configuration.  Fields are only ever appended; a caller built against an older
@@ -82,12 +84,18 @@ typedef struct tts_config {
  * clamp(round(exp(x) - 1), 0) (HF:181-183) match an fp32 evaluation; the decoder and postnet run in
  * acoustic_dtype.  FAST (1): the whole acoustic model runs in acoustic_dtype (durations can
  * round differently near .5).  With acoustic_dtype = F32 both are plain fp32. */
-enum { TTS_ENCODER_EXACT = 0, TTS_ENCODER_FAST = 1 };
+enum { TTS_ENCODER_EXACT = 0, TTS_ENCODER_FAST = 1, TTS_ENCODER_F32 = 2 };
 /* Range limit of EXACT: its split GEMMs and attention hold every fp32 operand as two f16 halves,
  * so activations and encoder-side weights must stay below 65504 in magnitude (f16 max).
  * tts_engine_finalize rejects encoder-side weights outside that range (TTS_ERR_INVALID naming
- * the tensor; use FAST or an fp32 acoustic_dtype for such a checkpoint); activations are not
- * checked on the device (LayerNorm bounds the residual stream to O(sqrt(D)) times its gain). */
+ * the tensor; use FAST or an fp32 acoustic_dtype for such a checkpoint).  Activations are
+ * checked on the device (ABI 4): every split GEMM and the split attention test the f16 high half
+ * of each operand they stage and, when one is inf or NaN (|x| >= 65520, or a NaN input), set the
+ * engine's range word.  The forward itself stays asynchronous; the caller reads the word with
+ * tts_acoustic_range_flag after its next sync and, when it is set, reruns the acoustic forward
+ * with TTS_ENCODER_F32 (the same fp32 layers on the exact fp32 MFMA kernels, ~3x slower on the
+ * encoder side, no range limit).  TTS_ENCODER_F32 is a run-time setting only
+ * (tts_acoustic_set_precision), not a tts_config value. */
 
 /* Number of HIP devices visible to this process. */
 int tts_device_count(void);
@@ -142,6 +150,16 @@ int tts_acoustic_forward_spk(tts_engine* eng, const int32_t* d_tokens, const int
                              int32_t* d_durations, void* stream);
 /* Speaker-embedding size E of the loaded acoustic model (0: single speaker). */
 int tts_acoustic_speaker_dim(tts_engine* eng, int* dim);
+
+/* Range guard (ABI 4, TTS_ENCODER_EXACT above): enqueue on `stream` a copy of the engine's
+ * range word into *dst (device or host-pinned int32; 1 = some split-precision operand of an
+ * acoustic forward enqueued before this call was outside f16's range, 0 = none), then clear the
+ * word.  Read *dst after synchronising the stream. */
+int tts_acoustic_range_flag(tts_engine* eng, int32_t* dst, void* stream);
+/* Encoder precision of later acoustic forwards of a 16-bit model created with EXACT:
+ * TTS_ENCODER_EXACT (split-precision, the default) or TTS_ENCODER_F32 (exact fp32 MFMA: the
+ * range guard's fallback).  Other models: TTS_ERR_INVALID. */
+int tts_acoustic_set_precision(tts_engine* eng, int precision);
 
 /* Live kernel timing for bench.py: with profiling on, every implicit-GEMM launch is
  * bracketed by hipEvents on its own stream; _read() waits for them and returns the summed

@@ -498,3 +498,54 @@ def test_fast_encoder_precision_bounded():
     print(f"[parity] durations bf16 fast-encoder: {int((diff != 0).sum())} of {diff.size} tokens differ")
     assert (diff != 0).mean() < 0.05 and np.abs(diff).max() <= 1
     e.close()
+
+
+def test_range_guard_falls_back_to_fp32_encoder(aw):
+    """Range guard of the exact encoder (include/tts_hip.h, ABI 4).  The split-precision GEMMs hold
+    each fp32 operand as f16 halves, so an activation past 65504 would turn into inf.  Layer 0's
+    macaron FFN up-projection is scaled by 2e4 (weights up to ~3,000, inside the finalize check)
+    so its ReLU output reaches ~7.5e4: the forward sets the range word, the same forward on the
+    fp32 MFMA encoder (TTS_ENCODER_F32) does not and matches the fp32 oracle (durations exact
+    outside the .5 carve-out, bf16 mel through parity.py), GonovaTTS reruns the batch by itself
+    (one RuntimeWarning, range_fallbacks == 1, finite audio), and the seeded weights never trip it."""
+    from gonova_tts_amd.config import AcousticConfig, VocoderConfig
+    from gonova_tts_amd.model import GonovaTTS
+    ids_list = [np.random.default_rng(5).integers(1, 78, size=n) for n in (40, 23)]
+    B, N = len(ids_list), 40
+    tok = np.zeros((B, N), np.int32)
+    for b, x in enumerate(ids_list):
+        tok[b, :len(x)] = x
+    lens = np.array([len(x) for x in ids_list], np.int32)
+    tok_d, lens_d = torch.from_numpy(tok).to(DEV), torch.from_numpy(lens).to(DEV)
+    # seeded weights: the word stays 0
+    *_, rw = engine("bf16", aw).acoustic(tok_d, lens_d, 12 * N, return_range=True)
+    assert int(rw.item()) == 0
+    k = "encoder.conformer_layers.0.feed_forward_macaron.conv1.weight"
+    aw2 = dict(aw)
+    aw2[k] = aw[k] * 20000.0
+    e = HipEngine(DEV, vocoder_dtype="f16", acoustic_dtype="bf16")
+    e.load_weights(acoustic=aw2, vocoder=make_vocoder_weights(seed=0))
+    *_, rw = e.acoustic(tok_d, lens_d, 12 * N, return_range=True)
+    assert int(rw.item()) == 1
+    with e.encoder_f32():
+        mel, mel_lens, dur, rw = e.acoustic(tok_d, lens_d, 12 * N, return_durations=True, return_range=True)
+    assert int(rw.item()) == 0
+    mel, mel_lens, dur = mel.cpu().numpy(), mel_lens.cpu().numpy(), dur.cpu().numpy()
+    for b, ids in enumerate(ids_list):
+        ref = acoustic_forward(ids, aw2)
+        logd = _oracle_log_durations(ids, aw2)
+        ok = _margin(logd) > 1e-3
+        np.testing.assert_array_equal(dur[b, :len(ids)][ok], ref["durations"][ok])
+        if np.array_equal(dur[b, :len(ids)], ref["durations"]):
+            L = int(mel_lens[b])
+            check(f"acoustic bf16 range-guard fp32 encoder b={b}", mel[b, :L], ref["mel"], kind="ac_bf16")
+    m = GonovaTTS(e, AcousticConfig(), VocoderConfig())
+    with pytest.warns(RuntimeWarning, match="f16 range"):
+        wav, wav_lens = m.synthesize_tokens(tok, lens)
+    assert m.range_fallbacks == 1
+    w = wav.cpu().numpy()
+    assert np.isfinite(w).all() and list(wav_lens) == [int(x) * 256 for x in mel_lens]
+    # the encoder is back on the split path afterwards: the next forward trips the word again
+    *_, rw = e.acoustic(tok_d, lens_d, 12 * N, return_range=True)
+    assert int(rw.item()) == 1
+    e.close()

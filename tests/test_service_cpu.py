@@ -255,7 +255,8 @@ def test_stream_frames_split_sentences_in_order():
     """Opt-in sub-sentence frames: a request with stream_frames gets each
     sentence in pieces, in sentence order, that concatenate to the per-sentence audio; the final
     marker's chunk_id counts the frames; a request without it in the same session keeps the
-    reference's one frame per sentence; a bad stream_frames value is skipped like any bad message."""
+    reference's one frame per sentence; a bad stream_frames value is refused with an error message
+    in the reference's error shape (nothing is queued for it)."""
     model = FakeStreamModel()
     app = create_app(lambda: model)
     text = "Hello world. This is a test! Is it working? yes it is."
@@ -268,6 +269,8 @@ def test_stream_frames_split_sentences_in_order():
             want = np.concatenate([np.full(100 * n, n, np.float32) for n in (12, 15, 25)])
             np.testing.assert_array_equal(np.concatenate(frames), want)
             ws.send_text(json.dumps({"type": "synthesize", "text": "One. Two!", "stream_frames": -3}))
+            err = ws.receive_json()
+            assert err["type"] == "error" and "stream_frames" in err["message"]
             ws.send_text(json.dumps({"type": "synthesize", "text": text}))
             frames, final = recv_until_complete(ws)
             assert [len(f) for f in frames] == [1200, 1500, 2500] and final["chunk_id"] == 3
@@ -286,3 +289,121 @@ def test_stream_frames_service_default():
             ws.send_text(json.dumps({"type": "synthesize", "text": "Per sentence again.", "stream_frames": 0}))
             frames, final = recv_until_complete(ws)
             assert [len(f) for f in frames] == [1900] and final["chunk_id"] == 1
+
+
+def test_stream_frames_floor_and_resampling_refusal():
+    """A tiny stream_frames rounds up to the service floor (one request cannot make the shared
+    batcher run a vocoder window and a host copy per mel frame); a model that resamples cannot cut
+    its output at chunk edges, so the service refuses stream_frames for it with an error message
+    and keeps serving per-sentence frames; the batcher's audio seconds use the model's rate."""
+    model = FakeStreamModel()
+    app = create_app(lambda: model)
+    with TestClient(app) as c:
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            ws.send_text(json.dumps({"type": "synthesize", "text": "Hello world.", "stream_frames": 1}))
+            frames, final = recv_until_complete(ws)
+            assert [len(f) for f in frames] == [320, 320, 320, 240]
+        assert model.stream_calls == [(["Hello world."], 32)]
+
+    class Resampling(FakeStreamModel):
+        sr, native_sr = 24000, 22050
+
+    model = Resampling()
+    app = create_app(lambda: model)
+    with TestClient(app) as c:
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            ws.send_text(json.dumps({"type": "synthesize", "text": "Hello world.", "stream_frames": 64}))
+            err = ws.receive_json()
+            assert err["type"] == "error" and "resamples" in err["message"]
+            ws.send_text(json.dumps({"type": "synthesize", "text": "Hello world."}))
+            frames, final = recv_until_complete(ws)
+            assert [len(f) for f in frames] == [1200] and final["chunk_id"] == 1
+        stats = app.state.service.batcher.stats
+        assert abs(stats["audio_seconds"] - 1200 / 24000) < 1e-9
+        assert model.stream_calls == []
+    with pytest.raises(ValueError, match="native sample rate"):
+        with TestClient(create_app(lambda: Resampling(), stream_frames=64)):
+            pass
+
+
+def test_stream_producer_stops_when_delivery_fails():
+    """If delivering a chunk fails, the streaming producer thread stops at the next chunk and
+    closes the model's generator (releasing its lock) instead of synthesizing the rest of the
+    batch into a queue nobody reads."""
+    import asyncio
+    from gonova_tts_amd.service.batcher import DynamicBatcher
+
+    state = {"yielded": 0, "closed": False}
+
+    def stream(texts, frames):
+        try:
+            for i in range(1000):
+                state["yielded"] += 1
+                time.sleep(0.002)
+                yield [(0, np.zeros(4, np.float32), False)]
+        finally:
+            state["closed"] = True
+
+    b = DynamicBatcher(None, None, synth_stream=stream)
+
+    async def deliver(item):
+        raise OSError("socket gone")
+
+    async def main():
+        with pytest.raises(OSError):
+            await b._stream(asyncio.get_running_loop(), ["x"], 32, {}, deliver)
+
+    asyncio.run(main())
+    assert state["closed"] and state["yielded"] < 50
+
+
+class FakeDeviceModel(FakeModel):
+    """One fake engine per 'device': records which sentences it synthesized."""
+
+    def __init__(self, device, delay=0.0):
+        super().__init__(delay=delay)
+        self.device = device
+
+
+def test_multi_device_fan_out_keeps_order_and_balances():
+    """Opt-in fan-out over the node's GPUs (TTSService(devices=[...])):
+    the factory makes one engine per device, one batcher round deals its sentences across both
+    engines (dist.plan_buckets: longest first to the least-loaded engine), the engines work at
+    the same time, and every request still gets its frames in sentence order followed by the
+    marker -- the same frames a single engine produces."""
+    made = []
+
+    def factory(device):
+        m = FakeDeviceModel(device, delay=0.05)
+        made.append(m)
+        return m
+
+    app = create_app(factory, devices=["cuda:0", "cuda:1"], max_wait=0.05, max_sentences=4)
+    texts = {i: " ".join(f"Sentence {i} number {j} {'x' * (3 * j + i)}." for j in range(5)) for i in range(4)}
+    results = {}
+    with TestClient(app) as c:
+        assert c.get("/health").json()["devices"] == ["cuda:0", "cuda:1"]
+
+        def client(i):
+            with c.websocket_connect("/v1/stream/tts") as ws:
+                ws.send_text(json.dumps({"type": "synthesize", "text": texts[i]}))
+                results[i] = recv_until_complete(ws)
+        ts = [threading.Thread(target=client, args=(i,)) for i in texts]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=30)
+        stats = app.state.service.batcher.stats
+    assert [m.device for m in made] == ["cuda:0", "cuda:1"]
+    from gonova_tts_amd.text import split_into_sentences
+    for i, (frames, final) in results.items():
+        sents = split_into_sentences(texts[i])
+        assert final == {"type": "synthesis_complete", "chunk_id": len(sents)}
+        assert [len(f) for f in frames] == [100 * len(s) for s in sents]
+        for f, s in zip(frames, sents):
+            assert np.all(f == len(s))
+    # both engines got work (warmups excluded), and their loads are within one long sentence
+    work = [sum(len(t) for b in m.batches[3:] for t in b) for m in made]
+    assert all(w > 0 for w in work), work
+    assert abs(work[0] - work[1]) <= max(len(t) for t in texts.values()), work
+    assert sum(stats["engine_sentences"]) == 20 and min(stats["engine_sentences"]) > 0

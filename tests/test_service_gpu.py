@@ -111,9 +111,10 @@ def test_two_concurrent_connections_share_engine_batches(served):
 
 def test_stream_frames_concatenate_to_generate(served):
     """Opt-in sub-sentence frames through the service on the real engine:
-    with "stream_frames": 8 every frame is at most 8 x 256 samples, each sentence comes as
-    ceil(samples / 2048) frames in order, and the frames concatenate to generate() of each
-    sentence (fp32 engine, the same tolerance as the per-sentence test)."""
+    "stream_frames": 8 is below the service's floor (MIN_STREAM_FRAMES = 32) and rounds up to it:
+    every frame is at most 32 x 256 samples, each sentence comes as ceil(samples / 8192) frames
+    in order, and the frames concatenate to generate() of each sentence (fp32 engine, the same
+    tolerance as the per-sentence test)."""
     c, model = served
     text = "Good morning to everyone in the room. The quick brown fox jumps over the lazy dog!"
     with c.websocket_connect("/v1/stream/tts") as ws:
@@ -121,8 +122,8 @@ def test_stream_frames_concatenate_to_generate(served):
         frames, final = recv_until_complete(ws)
     direct = [model.generate(s).squeeze().cpu().numpy() for s in split_into_sentences(text)]
     assert final == {"type": "synthesis_complete", "chunk_id": len(frames)}
-    assert all(0 < len(f) <= 8 * 256 for f in frames)
-    assert len(frames) == sum(-(-len(d) // 2048) for d in direct)
+    assert all(0 < len(f) <= 32 * 256 for f in frames)
+    assert len(frames) == sum(-(-len(d) // 8192) for d in direct)
     got, want = np.concatenate(frames), np.concatenate(direct)
     assert got.shape == want.shape
     np.testing.assert_allclose(got, want, atol=1e-5, rtol=1e-4)

@@ -58,7 +58,7 @@ def build(force: bool = False, verbose: bool = True, variant: str = "", defines=
     objs = [o for o, _ in results]
     rebuilt = any(r for _, r in results)
     if rebuilt or not os.path.exists(lib) or force:
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib] + objs
+        cmd = [HIPCC, "-shared", "-fPIC", "-Wl,-z,defs", f"--offload-arch={ARCH}", "-o", lib] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")

@@ -75,9 +75,25 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int nh = p.nh;
-  const int b = blockIdx.z / nh;
-  const int hd = blockIdx.z - b * nh;
-  const int n0 = blockIdx.x * BN;
+  // (bx, by, bz): row tile, M block, utterance x head -- the grid's own, or decoded from the 1-D
+  // XCD-ordered grid (ConvParams::xres_order)
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  int gx = gridDim.x, gy = gridDim.y;
+  if (p.xres_order) {
+    gx = (p.y_rows + BN - 1) / BN;
+    gy = (p.M + BM - 1) / BM;
+    const int total = gx * gy * p.B * nh;
+    const int per = (total + 7) / 8;
+    const int v = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (v >= total) return;  // padding blocks of the last XCD range (no tile, no counter)
+    by = v % gy;
+    const int r = v / gy;
+    bx = r % gx;
+    bz = r / gx;
+  }
+  const int b = bz / nh;
+  const int hd = bz - b * nh;
+  const int n0 = bx * BN;
   const int ylen = p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows;
   if (n0 >= ylen) return;
   const int xlen = p.x_len ? min(p.x_len[b], p.x_rows) : p.x_rows;
@@ -388,9 +404,25 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int nh = p.nh;
-  const int b = blockIdx.z / nh;
-  const int hd = blockIdx.z - b * nh;
-  const int n0 = blockIdx.x * BN;
+  // (bx, by, bz): row tile, M block, utterance x head -- the grid's own, or decoded from the 1-D
+  // XCD-ordered grid (ConvParams::xres_order)
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  int gx = gridDim.x, gy = gridDim.y;
+  if (p.xres_order) {
+    gx = (p.y_rows + BN - 1) / BN;
+    gy = (p.M + BM - 1) / BM;
+    const int total = gx * gy * p.B * nh;
+    const int per = (total + 7) / 8;
+    const int v = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (v >= total) return;  // padding blocks of the last XCD range (no tile, no counter)
+    by = v % gy;
+    const int r = v / gy;
+    bx = r % gx;
+    bz = r / gx;
+  }
+  const int b = bz / nh;
+  const int hd = bz - b * nh;
+  const int n0 = bx * BN;
   const int ylen = p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows;
   if (n0 >= ylen) return;
   const int xlen = p.x_len ? min(p.x_len[b], p.x_rows) : p.x_rows;
@@ -409,7 +441,7 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
   // packed weights: [MB][taps][Cin/16][64][8]; a wave past M reads the last block (its
   // results are never stored)
   const int KST = p.Cin / 16;
-  const int mb = min((int)blockIdx.y * WM + wm, (p.M + 31) / 32 - 1);
+  const int mb = min(by * WM + wm, (p.M + 31) / 32 - 1);
   // Weight quads stream through a bounds-checked buffer descriptor over this wave's block:
   // a reload past the group's last quad gets an out-of-range offset and fetches nothing, so
   // every ring slot is reloaded unconditionally (a branch around the reloads made the
@@ -622,7 +654,7 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
   const T* R2 = p.r2 ? reinterpret_cast<const T*>(p.r2) + (long long)b * p.srb + (long long)hd * p.srh : nullptr;
   const int tlen = p.up_len ? min(p.up_len[b], (p.y_rows - 1) * p.up_s) : 0;
   const int cl = tid % PPR;                   // 8-channel piece of the block's BM channels
-  const int m8 = blockIdx.y * BM + cl * 8;
+  const int m8 = by * BM + cl * 8;
   const bool mok = m8 < p.M;
   int q = 0, col = m8;
   if (p.up_s) { q = m8 / p.up_cout; col = m8 - q * p.up_cout; }
@@ -643,7 +675,7 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
 #pragma unroll
     for (int g = 0; g < 4; ++g)
       bl[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            brsrc, (blockIdx.y * BM + wm * 32 + 8 * g + 4 * hh) * 4, 0, 0));
+                                            brsrc, (by * BM + wm * 32 + 8 * g + 4 * hh) * 4, 0, 0));
   }
   // first-residual rows in flight before the staging barriers, through a descriptor with no
   // records when there is no residual: the loads are unconditional (a load under `if (R1)`
@@ -716,7 +748,7 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
   }
   if (lnf) {
     // the row tile's last-arriving M block normalises rows [n0, ylen) of it over all M channels
-    if (!ln_tile_last(p.ln_cnt + blockIdx.z * gridDim.x + blockIdx.x, gridDim.y, reinterpret_cast<int*>(smem)))
+    if (!ln_tile_last(p.ln_cnt + bz * gx + bx, gy, reinterpret_cast<int*>(smem)))
       return;
     xres_tile_ln<T, BN>(p, Y, b, n0, ylen, wave, lane);
   }
@@ -918,6 +950,10 @@ static bool xres_ln_ok(const ConvParams& p, int BN) {
   return (long long)((p.y_rows + BN - 1) / BN) * p.B <= p.ln_cnt_n;
 }
 
+#ifndef TTS_XRES_ORDER_DEFAULT
+#define TTS_XRES_ORDER_DEFAULT 2
+#endif
+
 template <typename T, int WM, int NT = 4, int OCC = TTS_XRES_OCC, bool XF = false, int DT = 0>
 static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s, bool* ln_done) {
   constexpr int BM = 32 * WM, BN = 32 * NT * (4 / WM);
@@ -925,6 +961,13 @@ static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s, boo
   const size_t lds = std::max(xt, TTS_XRES_EPI16 ? (size_t)BN * (BM * 2 + 16) : (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
   dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
   ConvParams q = p;
+  // XCD-ordered 1-D grid (TTS_XRES_ORDER=1: the multi-tap DMA launches, the decoder FFN convs and
+  // the stage 0-1 upsamplers; =2, the default: every conv_xres launch; 0: the 3-D grid).  Same-box
+  // A/B (profiles/r04e_ab_xres_order.txt): batch-32 acoustic 5.83 -> 5.67 ms, C5 3.52 -> 3.43 ms,
+  // C2 unchanged; bit-identical (tests/test_acoustic_gpu.py).
+  const int ord = sw(SW_XRES_ORDER) < 0 ? TTS_XRES_ORDER_DEFAULT : sw(SW_XRES_ORDER);
+  q.xres_order = (ord == 2 || (ord == 1 && DT > 1)) ? 1 : 0;
+  if (q.xres_order) grid = dim3(8 * ((grid.x * grid.y * grid.z + 7) / 8), 1, 1);
   if (!xres_ln_ok(q, BN)) q.ln_cnt = nullptr;  // the kernel's LayerNorm switch
   if (ln_done) *ln_done = q.ln_cnt != nullptr;
   hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM, OCC, XF, DT>), grid, dim3(256), lds, s, q, cg);

@@ -482,7 +482,10 @@ struct tts_engine {
               pp.out_act = 1; pp.out_slope = slope;
               s_act = true;
             }
-            auto launch = [&] { return sp ? mrf_pair_sp_launch(dt, ch, pp, s) : mrf_pair_launch(dt, ch, pp, s); };
+            const bool ws = !sp && !pp.post_wpk && mrf_pair_ws_supported(dt, ch, pp);
+            auto launch = [&] {
+              return sp ? mrf_pair_sp_launch(dt, ch, pp, s) : ws ? mrf_pair_ws_launch(dt, ch, pp, s) : mrf_pair_launch(dt, ch, pp, s);
+            };
             if (prof.on) {
               Profiler::Rec r{prof.get(), prof.get(), fl, PK_MRF_PAIR};
               HIP_CHECK(hipEventRecord(r.a, s));

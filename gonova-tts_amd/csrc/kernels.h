@@ -58,6 +58,11 @@ struct ConvParams {
   // the fallback of the exact encoder when its range guard tripped (tts_acoustic_set_precision).
   int* range_flag;
   int no_split;
+  // conv_xres block order (launcher-set): 0 = the 3-D grid as dispatched (row tile fastest);
+  // 1 = a 1-D grid padded to a multiple of 8, block L -> work item (L % 8) * per + L / 8 (each XCD
+  // a contiguous range of items), items ordered M block fastest, so the M blocks of a row tile run
+  // on one XCD together and share its X tile through that L2
+  int xres_order;
 };
 
 inline ConvParams conv_params_default() {
@@ -115,6 +120,10 @@ struct MrfPairParams {
   float out_slope;
 };
 bool mrf_pair_supported(int dtype, int C, int k);
+// warp-specialised persistent pair kernel (mrf_pair_ws.hip): k = 3 at C = 128 / 256, bit-identical
+// to mrf_pair_kernel; TTS_PAIR_WS switches it
+bool mrf_pair_ws_supported(int dtype, int C, const MrfPairParams& p);
+hipError_t mrf_pair_ws_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s);
 bool mrf_pair_outact_supported(int dtype, int C, int k);  // the launch can carry out_act
 
 // Streaming ConvTranspose1d with two taps (k = 2s) for the small upsamplers (upsample.hip):

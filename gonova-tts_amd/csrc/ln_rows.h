@@ -4,15 +4,24 @@
 // reduction everywhere, so a fused LayerNorm is bit-identical to the separate launch.
 //
 // Fused form: the blocks that produce one row tile (its M blocks) each store their part with
-// write-through (sc1) stores, drain them, release at agent scope and add to the tile's counter;
+// write-through (sc1) stores, drain them and add to the tile's counter (Guideline 16 R1, below);
 // the last to arrive acquires at agent scope and normalises the tile's rows (cdna_hip_programming.md Guideline 16,
 // the counter form of the R1 hand-off).  Counters start at 0 (the workspace is zeroed when it is
 // allocated) and the last arriver puts its counter back to 0 for the next launch.
 #pragma once
 #include "common.h"
 
+// The hand-off's publish is the R1 form of cdna_hip_programming.md Guideline 16: every part is
+// stored write-through (sc1, buffer-store aux 16) and drained by its storing wave (vmcnt(0) +
+// the block barrier) before the relaxed agent-scope ticket, so the bytes are past every L2 before
+// the count can complete ("store payload WRITE-THROUGH (sc1), so no release fence"); the last
+// arriver's agent-scope acquire drops its CU's stale lines before its plain loads.  An explicit
+// release fence (TTS_LN_RELEASE=1: buffer_wbl2 sc1 + wait per block) writes back the XCD's whole
+// L2 and cost 0.3 ms of a 6.1 ms batch-32 forward (profiles/r04b_ab_ln_release.txt); the results
+// were bit-identical and run-to-run stable with and without it, the in-launch split-K reduce
+// included (tools/splitk_stability.py, profiles/r04c_splitk_stability.txt).
 #ifndef TTS_LN_RELEASE
-#define TTS_LN_RELEASE 1  // 0: A/B builds -- the sc1 parts + relaxed ticket of round 3, no release fence
+#define TTS_LN_RELEASE 0
 #endif
 #ifndef TTS_LN_FENCE
 #define TTS_LN_FENCE 0  // diagnostic builds: __threadfence() in the last arriver instead of the agent acquire
@@ -191,9 +200,8 @@ __device__ inline bool ln_tile_last(int* cnt, int parts, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
   __syncthreads();
   if (threadIdx.x == 0) {
-    // agent-scope release before the ticket (cdna_hip_programming.md Guideline 16 recipe): the
-    // parts are write-through already, the release makes the hand-off correct under the memory
-    // model and not only under sc1 semantics; the asm wait stays after the fence (Pitfall 12)
+    // (TTS_LN_RELEASE builds: an agent-scope release before the ticket, the asm wait after the
+    // fence -- Guideline 16 Pitfall 12)
 #if TTS_LN_RELEASE
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

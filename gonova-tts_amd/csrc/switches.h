@@ -25,6 +25,8 @@ enum Sw : int {
   SW_XRES_DMA,     // TTS_XRES_DMA=0: FFN convs / upsamplers register-staged with round-2 channel groups; 2: register-staged, same bits
   SW_LN_FUSE,      // TTS_LN_FUSE=0: acoustic post-LNs as their own launches; 7: in every eligible GEMM launch (2-6: bisection)
   SW_SPLIT_NT1,    // TTS_SPLIT_NT1=0: split GEMMs always on 64-row tiles; 1: 32-row tiles wherever eligible (default: small grids)
+  SW_XRES_ORDER,   // TTS_XRES_ORDER=1: multi-tap DMA conv_xres launches on an XCD-ordered grid (M block fastest); 2: every conv_xres launch
+  SW_PAIR_WS,      // TTS_PAIR_WS=0/1: k = 3 pairs at C >= 128 on the warp-specialised persistent kernel off / on
   SW_N
 };
 

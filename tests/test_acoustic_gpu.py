@@ -390,6 +390,29 @@ def test_split_tile_height_bit_identical(aw, dtype, switch):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_xcd_ordered_xres_grid_bit_identical(aw, dtype, switch):
+    """conv_xres launched on a 1-D grid whose blocks are renumbered so that each XCD (blockIdx
+    mod 8) walks a contiguous run of M blocks over the same X rows (TTS_XRES_ORDER=1: the
+    multi-M-block launches; =2: every launch) gives the 3-D grid's bits, fused post-LN counters
+    included, on a ragged batch with predicted durations at both tile heights."""
+    eng = engine(dtype, aw)
+    rng = np.random.default_rng(46)
+    ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70, 127, 129, 9, 33)]
+    outs = {}
+    for order in (0, 1, 2):
+        for nt in (None, 2):
+            switch("TTS_XRES_ORDER", order)
+            switch("TTS_XRES_NT", nt)
+            outs[(order, nt)] = run(eng, ids_list, t_cap=8 * 144)
+    switch("TTS_XRES_NT", None)
+    switch("TTS_XRES_ORDER", None)
+    ref_m, ref_l, ref_d = outs[(0, None)]
+    for k, (m, l, d) in outs.items():
+        assert np.array_equal(d, ref_d) and np.array_equal(l, ref_l), k
+        assert np.array_equal(m, ref_m), k
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_split_whole_slice_staging_bit_identical(aw, dtype, switch):
     """Small split-precision GEMM grids (at most one block per CU: the batch-8 exact encoder and
     predictors) stage every channel group of their K slice at once; the quads and their MFMA order

@@ -220,6 +220,28 @@ def test_pipelined_c32_pairs_bit_identical(vw, dtype, switch):
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_warp_specialised_pairs_bit_identical(vw, dtype, switch):
+    """The warp-specialised persistent k = 3 pair kernel at C = 256 / 128 (mrf_pair_ws.hip:
+    loader waves stage tile k+1 and store tile k-1 while the MFMA waves run tile k) reproduces
+    mrf_pair_kernel bit for bit: ragged, empty and one-frame utterances, and a batch large
+    enough that every block walks several (utterance, tile) items, so the double-buffer
+    hand-off between items -- across utterance boundaries too -- is exercised."""
+    eng = engine_for(dtype, vw)
+    rng = np.random.default_rng(26)
+    lens = [300, 1, 0, 2, 157, 299, 64, 33, 250, 8, 300, 199, 17, 71, 280, 3]
+    mel = torch.from_numpy(rng.standard_normal((16, 300, 80)).astype(np.float32)).to(DEV)
+    ln = torch.tensor(lens, dtype=torch.int32)
+    switch("TTS_PAIR_WS", 1)
+    ws = eng.vocoder(mel, ln).cpu().numpy()
+    switch("TTS_PAIR_WS", 0)
+    ref = eng.vocoder(mel, ln).cpu().numpy()
+    switch("TTS_PAIR_WS", None)
+    for b, L in enumerate(lens):
+        assert np.array_equal(ws[b], ref[b]), (b, float(np.abs(ws[b] - ref[b]).max()))
+        assert np.all(ws[b, L * 256:] == 0)
+
+
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
 def test_fused_conv_post_bit_identical(vw, dtype, switch):
     """conv_post inside the last pair launch (its halo rows computed in the block, the final
     MRF sum never written) reproduces the separate conv_post launch bit for bit: ragged and

@@ -20,8 +20,7 @@ def short(name):
     return "other"
 
 
-def main():
-    d = sys.argv[1]
+def load(d):
     per, kname = defaultdict(dict), {}
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
         i = int(r["Dispatch_Id"])
@@ -31,7 +30,14 @@ def main():
     for r in csv.DictReader(open(f"{d}/run_kernel_trace.csv")):
         dur[int(r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
     ids = sorted(i for i in per if "tts::" in kname[i] or "_ZN3tts" in kname[i])
-    ids = ids[-len(ids) // ITERS:]
+    return per, kname, dur, ids[-len(ids) // ITERS:]  # the last forward
+
+
+def main():
+    """args: <clock/MFMA dir> [<FETCH_SIZE dir> <WRITE_SIZE dir> <instmix dir>] [batch]"""
+    dirs = [a for a in sys.argv[1:] if not a.isdigit()]
+    batch = next((a for a in sys.argv[1:] if a.isdigit()), "32")
+    per, kname, dur, ids = load(dirs[0])
     fam = defaultdict(lambda: [0.0, 0.0, 0.0, 0.0, 0.0, 0])
     for i in ids:
         c, t = per[i], dur.get(i, 0.0)
@@ -42,13 +48,34 @@ def main():
         f[3] += c.get("SQ_WAIT_INST_ANY", 0)
         f[4] += max(c.get("SQ_WAVE_CYCLES", 0), 1)
         f[5] += 1
+    extra = defaultdict(lambda: defaultdict(float))
+    # FETCH_SIZE / WRITE_SIZE in KB; FETCH doubled (MI355X_MICROARCH.md gfx950 correction for 16 B/lane loads)
+    for d, key, mul in ((dirs[1], "FETCH_SIZE", 2.0), (dirs[2], "WRITE_SIZE", 1.0)) if len(dirs) >= 3 else ():
+        p2, k2, _, ids2 = load(d)
+        for i in ids2:
+            extra[short(k2[i])][key] += p2[i].get(key, 0.0) * 1024 * mul
+    if len(dirs) >= 4:
+        p3, k3, _, ids3 = load(dirs[3])
+        for i in ids3:
+            e = extra[short(k3[i])]
+            for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_MFMA", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS",
+                      "SQ_WAVE_CYCLES"):
+                e[k] += p3[i].get(k, 0.0)
     tot = sum(f[0] for f in fam.values())
-    print(f"one acoustic forward (batch 32, bf16, exact encoder): {len(ids)} dispatches, {tot * 1e6:.0f} us under the profiler")
-    print(f"{'family':18s} {'n':>4s} {'us':>8s} {'share':>6s} {'GHz':>5s} {'mfma%':>6s} {'@2.4':>6s}")
+    print(f"one acoustic forward (batch {batch}, bf16, exact encoder): {len(ids)} dispatches, {tot * 1e6:.0f} us under the profiler")
+    print("mfma% = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024) at the measured clock, @2.4 at the nominal one;")
+    print("FETCH (x2 gfx950 correction) / WRITE in MB per forward; valu/mfma, lds/mfma instructions; bankconf = extra LDS cycles per LDS instruction")
+    print(f"{'family':18s} {'n':>4s} {'us':>8s} {'share':>6s} {'GHz':>5s} {'mfma%':>6s} {'@2.4':>6s} {'FETCH':>8s} {'WRITE':>8s} "
+          f"{'valu/mf':>7s} {'lds/mf':>6s} {'bankc':>6s}")
     for k, f in sorted(fam.items(), key=lambda kv: -kv[1][0]):
         ghz = f[1] / max(f[0], 1e-12) / 1e9
+        e = extra[k]
+        mf = max(e.get("SQ_INSTS_MFMA", 0.0), 1.0)
         print(f"{k:18s} {f[5]:4d} {f[0] * 1e6:8.1f} {100 * f[0] / tot:5.1f}% {ghz:5.2f} "
-              f"{100 * f[2] / max(f[1] * 1024, 1):6.1f} {100 * f[2] / (2.4e9 * f[0] * 1024):6.1f}")
+              f"{100 * f[2] / max(f[1] * 1024, 1):6.1f} {100 * f[2] / (2.4e9 * f[0] * 1024):6.1f} "
+              f"{e.get('FETCH_SIZE', 0) / 1e6:8.1f} {e.get('WRITE_SIZE', 0) / 1e6:8.1f} "
+              f"{e.get('SQ_INSTS_VALU', 0) / mf:7.2f} {e.get('SQ_INSTS_LDS', 0) / mf:6.2f} "
+              f"{e.get('SQ_LDS_BANK_CONFLICT', 0) / max(e.get('SQ_INSTS_LDS', 0), 1):6.2f}")
 
 
 if __name__ == "__main__":

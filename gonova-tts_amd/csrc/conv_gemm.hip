@@ -553,6 +553,9 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W1) : "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+#if TTS_XRES_STAMP
+      if (g == 0) st1 = __builtin_amdgcn_s_memtime();
+#endif
       dma(g + NB - 1);
       const char* buf = smem + (g % NB) * BUFB;
 #pragma unroll

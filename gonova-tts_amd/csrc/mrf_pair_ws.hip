@@ -37,16 +37,19 @@
 #define TTS_PAIR_MTO_MIN 64  // (mrf_pair.hip's: M-tile-outer MFMA order from this channel count up)
 #endif
 #ifndef TTS_PAIR_WS_NL
-#define TTS_PAIR_WS_NL 2  // loader waves per block
+#define TTS_PAIR_WS_NL 4  // loader waves per block
+#endif
+#ifndef TTS_PAIR_WS_WN
+#define TTS_PAIR_WS_WN 2  // compute waves along the rows (x 4 along the channels)
 #endif
 #ifndef TTS_PAIR_WS_DEFAULT
 #define TTS_PAIR_WS_DEFAULT 0  // off: slower than mrf_pair_kernel so far (profiles/r04e_ab_pair_ws.txt)
 #endif
 #ifndef TTS_PWS_BN_128
-#define TTS_PWS_BN_128 142  // output rows per tile at C = 128 (pair_bn<128, 3>: conv1's 144 rows in 9 tiles)
+#define TTS_PWS_BN_128 (144 * TTS_PAIR_WS_WN - 2)  // output rows per tile at C = 128: conv1's rows in whole 16-row tiles
 #endif
 #ifndef TTS_PWS_BN_256
-#define TTS_PWS_BN_256 62   // at C = 256: 64 conv1 rows in 4 tiles, two 37 KB buffers per block
+#define TTS_PWS_BN_256 (64 * TTS_PAIR_WS_WN - 2)   // at C = 256
 #endif
 
 #ifndef TTS_PWS_STAMP
@@ -67,6 +70,13 @@ __device__ unsigned long long g_pws_stamp[1 << 20];
 #define TTS_WSTAMP(role_, j_) (void)0
 #endif
 
+// the pair kernel's per-wave tiles (channels x 16-row tiles, weight ring), TTS_PAIR_WS_WN wave rows
+template <int C>
+struct PwsGeom : PairGeom<C> {
+  static_assert(PairGeom<C>::WM == 4 && PairGeom<C>::WN == 1, "4 x 1 pair wave grid");
+  static constexpr int WN = TTS_PAIR_WS_WN;
+};
+
 template <int C>
 constexpr int pws_bn() { return C == 128 ? TTS_PWS_BN_128 : TTS_PWS_BN_256; }
 
@@ -74,7 +84,7 @@ constexpr int pws_bn() { return C == 128 ? TTS_PWS_BN_128 : TTS_PWS_BN_256; }
 // the output staging tile, rounded up to whole 1 KiB DMA pieces
 template <int C, int K>
 static int pws_buf_bytes(int d) {
-  using G = PairGeom<C>;
+  using G = PwsGeom<C>;
   constexpr int BN = pws_bn<C>(), A2 = (K - 1) / 2;
   constexpr int NT1 = (BN + 2 * A2 + 15) / 16, NT2 = (BN + 15) / 16;
   const int g = (16 * NT1 + 2 * A2 * d) * G::RS;
@@ -91,11 +101,12 @@ __device__ inline void pws_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff) 
 }
 
 template <typename T, int C, int K, int NL, bool OUTACT>
-__global__ __launch_bounds__(64 * (4 + NL), 3) void mrf_pair_ws_kernel(MrfPairParams p, int buf_bytes) {
-  using G = PairGeom<C>;
+__global__ __launch_bounds__(64 * (4 * TTS_PAIR_WS_WN + NL), 3) void mrf_pair_ws_kernel(MrfPairParams p, int buf_bytes) {
+  using G = PwsGeom<C>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int BN = pws_bn<C>(), WM = G::WM, WN = G::WN, RS = G::RS, D = G::D, MT = G::MT;
-  static_assert(WM * WN == 4, "four compute waves");
+  constexpr int NCW = WM * WN;  // compute waves
+  static_assert((NCW + NL) % 4 == 0, "whole waves per SIMD: a block's waves spread evenly over the 4 SIMDs");
   constexpr int KS = C / 32, S = K * KS;
   constexpr int A2 = (K - 1) / 2;
   constexpr int BO = BN, RT = BO + 2 * A2;
@@ -145,10 +156,10 @@ __global__ __launch_bounds__(64 * (4 + NL), 3) void mrf_pair_ws_kernel(MrfPairPa
   const size_t utt = (size_t)p.T * C;  // elements per utterance
   const float slope = p.slope;
 
-  if (wave >= 4) {
+  if (wave >= NCW) {
     // =============================== loader waves ===============================
-    const int lt = tid - 256;  // 0 .. NLT-1
-    const int lw = wave - 4;
+    const int lt = tid - 64 * NCW;  // 0 .. NLT-1
+    const int lw = wave - NCW;
     const int NQ = (RG * RS + 1023) / 1024;  // DMA pieces of the G tile
     // DMA of item `it`'s input rows into buffer `buf`: G row r <-> utterance row n0 - a1 - A2 + r
     auto dma = [&](int it, char* buf) __attribute__((always_inline)) {
@@ -173,37 +184,34 @@ __global__ __launch_bounds__(64 * (4 + NL), 3) void mrf_pair_ws_kernel(MrfPairPa
         *q = lrelu_unit<T>(*q, slope);
       }
     };
-    // row pass of item `it` from its output tile in `buf` (mrf_pair_kernel's, piece for piece)
+    // row pass of item `it` from its output tile in `buf` (mrf_pair_kernel's, piece for piece;
+    // never accumulating: the launcher takes only pairs that write the MRF sum fresh): every
+    // input-row load of the lane's P pieces goes out at once (one round trip; the rows are
+    // L2-hot, staged as this tile's G two tiles ago), then LDS read + epilogue + store
+    constexpr int NP = BO * VPR, P = (NP + NLT - 1) / NLT;
     auto row_pass = [&](int it, const char* buf) __attribute__((always_inline)) {
       const int b = it / nx, n0 = (it - b * nx) * BN, len = min(p.len[b], p.T);
       const T* Xb = reinterpret_cast<const T*>(p.x) + (size_t)b * utt;
       T* Yb = reinterpret_cast<T*>(p.y) + (size_t)b * utt;
       const int nb = len * C * (int)sizeof(T);
       const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Xb), 0, nb, 0x00020000);
-      // the MRF sum: no records when the launch does not accumulate (the load fetches nothing)
-      const auto sr = __builtin_amdgcn_make_buffer_rsrc(Yb, 0, p.accum ? nb : 0, 0x00020000);
       const auto yr = __builtin_amdgcn_make_buffer_rsrc(Yb, 0, nb, 0x00020000);  // rows >= len: dropped
-      constexpr int NP = BO * VPR;
-      constexpr int CH = 6;  // pieces per lane in flight
-      for (int i0 = lt; i0 < NP; i0 += CH * NLT) {
-        uint4 h[CH], s[CH];
+      const int base = n0 * C * (int)sizeof(T);
+      uint4 h[P];
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-          const int idx = min(i0 + j * NLT, NP - 1);
-          const int off = ((n0 + idx / VPR) * C + (idx % VPR) * 8) * (int)sizeof(T);
-          h[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
-          s[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(sr, off, 0, 0));
-        }
+      for (int j = 0; j < P; ++j) {
+        const int idx = min(lt + j * NLT, NP - 1);
+        h[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, base + idx * 16, 0, 0));
+      }
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-          const int idx = i0 + j * NLT;
-          if (idx >= NP) break;
+      for (int j = 0; j < P; ++j) {
+        const int idx = lt + j * NLT;
+        if (idx < NP) {
           const int o = idx / VPR, c8 = idx % VPR;
           const uint4 y = *reinterpret_cast<const uint4*>(buf + o * YS16 + c8 * 16);
-          uint4 v = epi_row<T>(y, h[j], p.accum, s[j], p.scale);
+          uint4 v = epi_row<T>(y, h[j], false, uint4{0u, 0u, 0u, 0u}, p.scale);
           if constexpr (OUTACT) v = lrelu_unit<T>(v, p.out_slope);
-          const int off = ((n0 + o) * C + c8 * 8) * (int)sizeof(T);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yr, off, 0, TTS_ROW_STORE);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yr, base + idx * 16, 0, TTS_ROW_STORE);
         }
       }
     };
@@ -351,7 +359,7 @@ __global__ __launch_bounds__(64 * (4 + NL), 3) void mrf_pair_ws_kernel(MrfPairPa
 
 template <int C>
 static bool pws_shape(int dtype, const MrfPairParams& p) {
-  return (dtype == DT_F16 || dtype == DT_BF16) && p.k == 3 && p.d >= 1 && p.d <= 5 && !p.post_wpk &&
+  return (dtype == DT_F16 || dtype == DT_BF16) && p.k == 3 && p.d >= 1 && p.d <= 5 && !p.post_wpk && !p.accum &&
          2 * pws_buf_bytes<C, 3>(p.d) <= 160 * 1024 && p.slope >= 0.f && p.slope <= 1.f;
 }
 
@@ -372,17 +380,20 @@ static hipError_t launch_ws(const MrfPairParams& p, hipStream_t s) {
   }
   const int nx = (p.T + pws_bn<C>() - 1) / pws_bn<C>();
   const long long items = (long long)nx * p.B;
-  // two blocks per CU, a multiple of 8 (every XCD the same number), at most one block per item
-  long long nb = std::min<long long>(2LL * ncu, items);
-  nb = std::max<long long>(8, nb / 8 * 8);
   const int bb = pws_buf_bytes<C, 3>(p.d);
   const size_t lds = 2 * (size_t)bb;
-  constexpr int NL = TTS_PAIR_WS_NL;
+  constexpr int NL = TTS_PAIR_WS_NL, NW = 4 * TTS_PAIR_WS_WN + NL;
+  // blocks per CU: by LDS and by wave slots (3 waves per SIMD at the kernel's register budget);
+  // a multiple of 8 (every XCD the same number), at most one block per item
+  const int bpc = std::max(1, std::min((int)(163840 / lds), 12 / NW));
+  long long nb = std::min<long long>((long long)bpc * ncu, items);
+  nb = std::max<long long>(8, nb / 8 * 8);
+
   if (p.out_act) {
     if (!(p.out_slope >= 0.f && p.out_slope <= 1.f)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((mrf_pair_ws_kernel<T, C, 3, NL, true>), dim3((unsigned)nb), dim3(64 * (4 + NL)), lds, s, p, bb);
+    hipLaunchKernelGGL((mrf_pair_ws_kernel<T, C, 3, NL, true>), dim3((unsigned)nb), dim3(64 * (4 * TTS_PAIR_WS_WN + NL)), lds, s, p, bb);
   } else {
-    hipLaunchKernelGGL((mrf_pair_ws_kernel<T, C, 3, NL, false>), dim3((unsigned)nb), dim3(64 * (4 + NL)), lds, s, p, bb);
+    hipLaunchKernelGGL((mrf_pair_ws_kernel<T, C, 3, NL, false>), dim3((unsigned)nb), dim3(64 * (4 * TTS_PAIR_WS_WN + NL)), lds, s, p, bb);
   }
   return hipGetLastError();
 }

@@ -4,21 +4,22 @@ Each parity test calls `check(name, got, ref, rel_rms_tol=..., max_abs_tol=...)`
 the relative RMS error and the max absolute error against the reference, records both with
 the tolerance (printed, and written as JSON to $PARITY_LOG at the end of the session, see
 conftest.py) and asserts them.  Tolerances sit at about 2x the values measured on MI355X
-(profiles/r02_parity_errors.json), so an error regression of 2x fails."""
+(profiles/r04_parity_errors.json), so an error regression of 2x fails."""
 import numpy as np
 
 RECORDS = []
 
-# (rel_rms, max_abs) bounds per path, ~2x the MI355X-measured errors (profiles/r02_parity_errors.json:
-# fp16 vocoder 1.6e-3 / 4.0e-4, bf16 vocoder 8.9e-3 / 1.9e-3, fp16 acoustic mel 1.5e-3 / 6.7e-3,
-# bf16 acoustic mel 1.1e-2 / 5.2e-2, bf16 tokens -> waveform 1.5e-2 / 3.2e-3; waveform rms ~0.045,
-# mel rms ~1.0).  SURVEY.md §8c's recommended bars were fp16 5e-3 and bf16 2.5e-2 rel-RMS.
+# (rel_rms, max_abs) bounds per path, re-derived each round from the largest errors the GPU suite
+# measured (profiles/r04_parity_errors.json, round 4: fp16 vocoder 1.62e-3 / 4.0e-4, bf16 vocoder
+# 8.9e-3 / 2.0e-3, fp16 acoustic mel 1.26e-3 / 5.9e-3, bf16 acoustic mel 1.02e-2 / 5.0e-2, bf16
+# tokens -> waveform 1.46e-2 / 3.2e-3; waveform rms ~0.045, mel rms ~1.0): about 2x, the
+# end-to-end bf16 bound at 1.7x (SURVEY.md §8c's recommended bars: fp16 5e-3, bf16 2.5e-2 rel-RMS).
 TOL = {
     "voc_f16": (3.2e-3, 8e-4),
     "voc_bf16": (1.8e-2, 4e-3),
-    "ac_f16": (3e-3, 1.5e-2),
-    "ac_bf16": (2.5e-2, 0.1),
-    "e2e_bf16": (3e-2, 6.5e-3),
+    "ac_f16": (2.5e-3, 1.2e-2),
+    "ac_bf16": (2e-2, 0.1),
+    "e2e_bf16": (2.5e-2, 6.5e-3),
 }
 
 

@@ -61,7 +61,7 @@ namespace tts {
 #if TTS_PWS_STAMP
 // The launches whose (C, d) match g_pws_target (the last one of the workload wins): per block 256
 // words -- [0] tiles, [1] entry time, then per tile k < 31 eight s_memtime values: the compute
-// wave 0's arrival at barriers A(k), B(k), C(k), D(k) and the loader wave 4's.  Never in the product.
+// wave 0's arrival at barriers A(k), B(k), C(k), D(k) and the first loader wave's.  Never in the product.
 __device__ int g_pws_target[2];
 __device__ unsigned long long g_pws_stamp[1 << 20];
 #define TTS_WSTAMP(role_, j_)                                                                       \
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(64 * (4 * TTS_PAIR_WS_WN + NL), 3) void mrf_pair_ws
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int d = p.d;
 #if TTS_PWS_STAMP
-  const bool stamp_on = g_pws_target[0] == C && g_pws_target[1] == p.d && (wave == 0 || wave == 4) &&
+  const bool stamp_on = g_pws_target[0] == C && g_pws_target[1] == p.d && (wave == 0 || wave == NCW) &&
                         blockIdx.x < (1u << 12);
   unsigned long long* stamp_rec = g_pws_stamp + blockIdx.x * 256;
   if (stamp_on && wave == 0 && lane == 0) stamp_rec[1] = __builtin_amdgcn_s_memtime();
@@ -162,8 +162,11 @@ __global__ __launch_bounds__(64 * (4 * TTS_PAIR_WS_WN + NL), 3) void mrf_pair_ws
     const int lw = wave - NCW;
     const int NQ = (RG * RS + 1023) / 1024;  // DMA pieces of the G tile
     // DMA of item `it`'s input rows into buffer `buf`: G row r <-> utterance row n0 - a1 - A2 + r
+    // (item, utterance and length made wave-uniform: a descriptor built from a value the compiler
+    // cannot prove uniform becomes a waterfall loop around every buffer instruction)
     auto dma = [&](int it, char* buf) __attribute__((always_inline)) {
-      const int b = it / nx, n0 = (it - b * nx) * BN, len = min(p.len[b], p.T);
+      it = __builtin_amdgcn_readfirstlane(it);
+      const int b = it / nx, n0 = (it - b * nx) * BN, len = __builtin_amdgcn_readfirstlane(min(p.len[b], p.T));
       const T* Xb = reinterpret_cast<const T*>(p.x) + (size_t)b * utt;
       const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Xb), 0, len * C * (int)sizeof(T), 0x00020000);
       const int gs = n0 - a1 - A2;
@@ -177,11 +180,16 @@ __global__ __launch_bounds__(64 * (4 * TTS_PAIR_WS_WN + NL), 3) void mrf_pair_ws
       }
     };
     // LeakyReLU in place over the landed G tile (element-wise: the swizzle does not matter)
+    // (four pieces per lane in flight: one LDS round trip per four, not per piece)
     auto activate = [&](char* buf) __attribute__((always_inline)) {
       const int n16 = NQ * 64;
-      for (int i = lt; i < n16; i += NLT) {
-        uint4* q = reinterpret_cast<uint4*>(buf + 16 * i);
-        *q = lrelu_unit<T>(*q, slope);
+      for (int i0 = lt; i0 < n16; i0 += 4 * NLT) {
+        uint4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const uint4*>(buf + 16 * min(i0 + j * NLT, n16 - 1));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (i0 + j * NLT < n16) *reinterpret_cast<uint4*>(buf + 16 * (i0 + j * NLT)) = lrelu_unit<T>(v[j], slope);
       }
     };
     // row pass of item `it` from its output tile in `buf` (mrf_pair_kernel's, piece for piece;
@@ -190,7 +198,8 @@ __global__ __launch_bounds__(64 * (4 * TTS_PAIR_WS_WN + NL), 3) void mrf_pair_ws
     // L2-hot, staged as this tile's G two tiles ago), then LDS read + epilogue + store
     constexpr int NP = BO * VPR, P = (NP + NLT - 1) / NLT;
     auto row_pass = [&](int it, const char* buf) __attribute__((always_inline)) {
-      const int b = it / nx, n0 = (it - b * nx) * BN, len = min(p.len[b], p.T);
+      it = __builtin_amdgcn_readfirstlane(it);
+      const int b = it / nx, n0 = (it - b * nx) * BN, len = __builtin_amdgcn_readfirstlane(min(p.len[b], p.T));
       const T* Xb = reinterpret_cast<const T*>(p.x) + (size_t)b * utt;
       T* Yb = reinterpret_cast<T*>(p.y) + (size_t)b * utt;
       const int nb = len * C * (int)sizeof(T);

@@ -4,7 +4,7 @@ step (diagnostic build only).
 Build:  python -m gonova_tts_amd.build --variant wstamp -DTTS_PWS_STAMP=1
 Run:    TTS_PAIR_WS=1 TTS_LIB=<repo>/gonova-tts_amd/libtts_hip_wstamp.so python3 tools/pws_stamps.py C d [C d ...]
 
-Per block and tile the library records when compute wave 0 and loader wave 4 arrive at each of
+Per block and tile the library records when compute wave 0 and the first loader wave arrive at each of
 the four barriers A (G ready / output tile written), B (conv1 done / row pass done), C (T written /
 DMA issued), D (conv2 done / G activated).  A barrier opens when the later role arrives, so for
 each barrier this prints how long each role waited for the other, and each role's work per

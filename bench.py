@@ -277,11 +277,12 @@ class Ctx:
         return self.max_over_ranks(el), prof
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, kind="c2"):
     """HBM bytes per launch of one kernel family from the newest committed PMC summary
-    (tools/pmc_traffic.py, profiles/*_pmc_traffic_c2.json), if it covers that family."""
+    (tools/pmc_traffic.py, profiles/*_pmc_traffic_<kind>.json: "c2" the headline step, "c3voc_bf16"
+    the C3 vocoder in bf16 at 864 frames), if it covers that family."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic_c2.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_traffic_{kind}.json")))
     if not files:
         return None
     d = json.load(open(files[-1]))
@@ -431,7 +432,9 @@ def bench_full(ctx, args, steps, warmup):
             "x_realtime_per_gpu": round(value / ctx.world / SR, 2), "dtype": "bf16",
             "config": {"workload": "C3 full pipeline (tokens -> FS2-Conformer -> HiFi-GAN), "
                                    f"batch-{B} x {N} tokens x {dur} frames = {T} frames (10.03 s)"},
-            "roofline": roofline(prof, el, steps, "bf16", None, getattr(ctx, "prof_steps", None))}
+            "roofline": roofline(prof, el, steps, "bf16",
+                                 (lambda k: pmc_traffic(k, "c3voc_bf16")) if (B, N) == (32, 144) else None,
+                                 getattr(ctx, "prof_steps", None))}
 
 
 def bench_c4(ctx, args, steps, warmup):

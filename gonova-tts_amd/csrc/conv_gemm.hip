@@ -381,7 +381,18 @@ __device__ inline void xres_tile_ln(const ConvParams& p, const T* Y, int b, int 
 #endif
 // DMA form geometry: LDS buffers (1-tap: 3, prefetch two groups ahead -- a group is a third of
 // the MFMA work of a 3-tap one) and staged rows per buffer (multi-tap: a 32-row halo)
-template <int DT> constexpr int xdma_nb() { return DT == 1 ? 3 : TTS_XDMA_NB; }
+#ifndef TTS_XDMA_NB2
+#define TTS_XDMA_NB2 2  // ... for the multi-tap 64-row tiles (NT = 2): small grids, one block per CU or less
+#endif
+#ifndef TTS_XDMA_RSL2
+#define TTS_XDMA_RSL2 1  // weight ring depth (groups) of the multi-tap 64-row tiles
+#endif
+// (Build options for the multi-tap 64-row tiles, where the 128-row grid would leave CUs idle: the
+// batch-8 decoder FFN down-projection, 336 blocks of 24 groups.  Prefetching three groups ahead
+// with a two-group weight ring (NB2 = 4, RSL2 = 2; bit-identical) measured 37.5 -> 39 us per
+// launch: the group round trips are not what bounds it.)
+template <int DT, int NT = 4> constexpr int xdma_nb() { return DT == 1 ? 3 : NT == 2 ? TTS_XDMA_NB2 : TTS_XDMA_NB; }
+template <int DT, int NT = 4> constexpr int xdma_rsl() { return DT == 1 ? 2 : NT == 2 ? TTS_XDMA_RSL2 : 1; }
 template <int DT, int BN> constexpr int xdma_rows() { return BN + (DT > 1 ? 32 : 0); }
 // one 16-byte-per-lane buffer load straight into LDS (lane i -> lds + 16 i), no VGPR destination
 __device__ inline void lds_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff) {
@@ -494,10 +505,12 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
     constexpr int RD = xdma_rows<DT, BN>();  // staged rows per group: the tile + a halo of (taps - 1) * dil <= 32
     constexpr int NPW = RD / 32;        // 1 KiB DMA pieces (8 rows) per wave per group
     constexpr int BUFB = RD * 128;      // bytes per LDS buffer
-    constexpr int NB = xdma_nb<DT>();
-    constexpr int RSL = DT == 1 ? 2 : 1;  // weight ring depth in groups (one quad per tap and group)
+    constexpr int NB = xdma_nb<DT, NT>();
+    constexpr int RSL = xdma_rsl<DT, NT>();  // weight ring depth in groups (one quad per tap and group)
+    static_assert(RSL <= NB - 1, "the ring may not run ahead of the staged groups");
     constexpr int Q = 4 * DT;           // weight loads per group
-    static_assert(NB == 2 || NB == 3, "2 or 3 LDS buffers");
+    static_assert(NB >= 2 && NB <= 4, "2 to 4 LDS buffers");
+    static_assert((NB - 2) * (RD / 32) + (NB - 1) * 4 * DT <= 63, "vmcnt wait counts fit the 6-bit field");
     // outstanding memory operations younger than group g's pieces at its wait: the DMAs of groups
     // g + 1 .. g + NB - 2 and the ring loads issued after it -- RSL groups' at g = 0, then
     // min(RSL + g, NB - 1) groups' (the smaller count of the two cases: waiting for more is safe)
@@ -960,7 +973,7 @@ static bool xres_ln_ok(const ConvParams& p, int BN) {
 template <typename T, int WM, int NT = 4, int OCC = TTS_XRES_OCC, bool XF = false, int DT = 0>
 static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s, bool* ln_done) {
   constexpr int BM = 32 * WM, BN = 32 * NT * (4 / WM);
-  const size_t xt = DT ? (size_t)xdma_nb<DT>() * xdma_rows<DT, BN>() * 128 : (size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16);
+  const size_t xt = DT ? (size_t)xdma_nb<DT, NT>() * xdma_rows<DT, BN>() * 128 : (size_t)(BN + (p.taps - 1) * p.dil) * (cg * 2 + 16);
   const size_t lds = std::max(xt, TTS_XRES_EPI16 ? (size_t)BN * (BM * 2 + 16) : (size_t)XRES_HR * (4 / WM) * (BM * 4 + 16));
   dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
   ConvParams q = p;

@@ -77,12 +77,19 @@ constexpr int PAIR_PO = 8;
 // per row drops by the same 18 %).  At C = 64 (two waves along the rows) the height also makes
 // conv1's tile count even, so no wave repeats a tile.  Any height works: a row's arithmetic does
 // not depend on it.  Same-box A/B (profiles/r03i_ab_tile_heights.txt): C = 256 k = 3 / 7 pairs
-// 976 -> 1011 / 1087 -> 1142 TF/s, C = 128 k = 3 996 -> 1039, C = 32 k = 11 963 -> 980.
+// 976 -> 1011 / 1087 -> 1142 TF/s, C = 128 k = 3 996 -> 1039, C = 32 k = 11 963 -> 980.  Round 4
+// (profiles/r04o_ab_c256_tile_heights.txt): at C = 256 the k = 7 / 11 pairs stream 2*k*C*C*2 =
+// 1.8 / 2.9 MB of weights per block from L2, so taller tiles (106 / 86 rows, as tall as the LDS of
+// two blocks per CU and 256 VGPRs allow) cut the weight bytes per row by 30 / 25 %: k = 7 pairs
+// 356 -> 341 us, k = 11 574 -> 558 us (stage-0 pairs -99 us per C2 step), bit-identical.
 #ifndef TTS_PBN_256_3
 #define TTS_PBN_256_3 78
 #endif
 #ifndef TTS_PBN_256_7
-#define TTS_PBN_256_7 74
+#define TTS_PBN_256_7 106  // conv1 7 tiles (112 rows); round 3: 74 (5 tiles)
+#endif
+#ifndef TTS_PBN_256_11
+#define TTS_PBN_256_11 86  // conv1 6 tiles (96 rows); the G tile of d = 5 (146 rows, 75 KB) still fits two blocks per CU
 #endif
 #ifndef TTS_PBN_128_3
 #define TTS_PBN_128_3 142
@@ -103,6 +110,7 @@ template <int C, int K>
 constexpr int pair_bn() {
   if (C == 256 && K == 3) return TTS_PBN_256_3;
   if (C == 256 && K == 7) return TTS_PBN_256_7;
+  if (C == 256 && K == 11) return TTS_PBN_256_11;
   if (C == 128 && K == 3) return TTS_PBN_128_3;
   if (C == 32 && K == 11) return TTS_PBN_32_11;
   if (C == 128 && K == 7) return TTS_PBN_128_7;

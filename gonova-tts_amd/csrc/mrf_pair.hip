@@ -94,6 +94,9 @@ constexpr int PAIR_PO = 8;
 #ifndef TTS_PBN_128_3
 #define TTS_PBN_128_3 142
 #endif
+#ifndef TTS_PBN_128_11
+#define TTS_PBN_128_11 128
+#endif
 #ifndef TTS_PBN_32_11
 #define TTS_PBN_32_11 502
 #endif
@@ -114,6 +117,7 @@ constexpr int pair_bn() {
   if (C == 128 && K == 3) return TTS_PBN_128_3;
   if (C == 32 && K == 11) return TTS_PBN_32_11;
   if (C == 128 && K == 7) return TTS_PBN_128_7;
+  if (C == 128 && K == 11) return TTS_PBN_128_11;
   if (C == 64 && K == 7) return TTS_PBN_64_7;
   if (C == 64 && K == 11) return TTS_PBN_64_11;
   return PairGeom<C>::BN;

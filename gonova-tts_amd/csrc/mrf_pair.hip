@@ -81,9 +81,10 @@ constexpr int PAIR_PO = 8;
 // (profiles/r04o_ab_c256_tile_heights.txt): at C = 256 the k = 7 / 11 pairs stream 2*k*C*C*2 =
 // 1.8 / 2.9 MB of weights per block from L2, so taller tiles (106 / 86 rows, as tall as the LDS of
 // two blocks per CU and 256 VGPRs allow) cut the weight bytes per row by 30 / 25 %: k = 7 pairs
-// 356 -> 341 us, k = 11 574 -> 558 us (stage-0 pairs -99 us per C2 step), bit-identical.
+// 356 -> 341 us, k = 11 574 -> 558 us (stage-0 pairs -99 us per C2 step), bit-identical; k = 3 at
+// 110 rows (profiles/r04q_ab_c256_k3_tile_heights.txt): 169 -> 157 us per pair.
 #ifndef TTS_PBN_256_3
-#define TTS_PBN_256_3 78
+#define TTS_PBN_256_3 110  // conv1 7 tiles (112 rows), 254 VGPRs; round 3: 78 (5 tiles)
 #endif
 #ifndef TTS_PBN_256_7
 #define TTS_PBN_256_7 106  // conv1 7 tiles (112 rows); round 3: 74 (5 tiles)

@@ -124,9 +124,17 @@ constexpr int pair_bn() {
   return PairGeom<C>::BN;
 }
 
+#ifndef TTS_PAIR_SHORT_D256
+#define TTS_PAIR_SHORT_D256 4  // weight-ring depth (k-steps) of the C = 256 short tiles (full height: 2)
+#endif
 template <int C, int DIV, int K = 0, bool POST = false>
 struct PairGeomS : PairGeom<C> {
   static constexpr int BN = DIV == 1 && K > 0 && !POST ? pair_bn<C, K>() : PairGeom<C>::BN / DIV;
+  // short tiles do few MFMAs per k-step (one row tile per wave), so the weight ring's L2 round
+  // trips are exposed unless it runs further ahead; the depth only moves loads earlier (same
+  // k-step order: bit-identical).  C = 256, D 2 -> 4 (profiles/r04t_ab_short_ring.txt): the C5
+  // chunk's stage-0 pairs 337 -> 266 us, C5 3.44 -> 3.36 ms (8: 270 us)
+  static constexpr int D = DIV > 1 && C == 256 ? TTS_PAIR_SHORT_D256 : PairGeom<C>::D;
 };
 
 // LDS bytes of one launch (G tile incl. conv1 overrun rows, T tile; >= output staging tile of

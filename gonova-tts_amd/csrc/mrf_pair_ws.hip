@@ -73,8 +73,8 @@ __device__ unsigned long long g_pws_stamp[1 << 20];
 // the pair kernel's per-wave tiles (channels x 16-row tiles, weight ring), TTS_PAIR_WS_WN wave rows
 template <int C>
 struct PwsGeom : PairGeom<C> {
-  static_assert(PairGeom<C>::WM == 4 && PairGeom<C>::WN == 1, "4 x 1 pair wave grid");
-  static constexpr int WN = TTS_PAIR_WS_WN;
+  // 4 waves along the channels (16 * MT channels each), whatever wave grid mrf_pair_kernel uses
+  static constexpr int WM = 4, WN = TTS_PAIR_WS_WN, MT = C / 64;
 };
 
 template <int C>

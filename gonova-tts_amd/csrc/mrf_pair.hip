@@ -124,6 +124,9 @@ constexpr int pair_bn() {
   return PairGeom<C>::BN;
 }
 
+#ifndef TTS_P32K11_OCC
+#define TTS_P32K11_OCC 3
+#endif
 #ifndef TTS_PAIR_SHORT_D256
 #define TTS_PAIR_SHORT_D256 4  // weight-ring depth (k-steps) of the C = 256 short tiles (full height: 2)
 #endif
@@ -135,6 +138,9 @@ struct PairGeomS : PairGeom<C> {
   // k-step order: bit-identical).  C = 256, D 2 -> 4 (profiles/r04t_ab_short_ring.txt): the C5
   // chunk's stage-0 pairs 337 -> 266 us, C5 3.44 -> 3.36 ms (8: 270 us)
   static constexpr int D = DIV > 1 && C == 256 ? TTS_PAIR_SHORT_D256 : PairGeom<C>::D;
+  // blocks per CU the register budget is sized for (the C = 32 k = 11 pairs without conv_post
+  // may take a fourth: TTS_P32K11_OCC)
+  static constexpr int OCC = C == 32 && K == 11 && !POST && DIV == 1 ? TTS_P32K11_OCC : PairGeom<C>::OCC;
 };
 
 // LDS bytes of one launch (G tile incl. conv1 overrun rows, T tile; >= output staging tile of
@@ -155,7 +161,7 @@ static size_t pair_lds_bytes(int k, int d, bool post) {
 // OUTACT: the stored rows are LeakyReLU(p.out_slope) of the row pass's values (a stage's last
 // pair, whose MRF sum only the next upsampler reads; MrfPairParams::out_act)
 template <typename T, int C, int K, bool POST = false, int DIV = 1, bool OUTACT = false>
-__global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom<C>::OCC)) void mrf_pair_kernel(
+__global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeomS<C, DIV, K, POST>::OCC)) void mrf_pair_kernel(
     MrfPairParams p) {
   using G = PairGeomS<C, DIV, K, POST>;
   typedef typename Mfma<T>::frag Frag;

@@ -25,9 +25,12 @@ struct PairGeom;
 #ifndef TTS_P64_D
 #define TTS_P64_D 4
 #endif
+#ifndef TTS_P32_OCC
+#define TTS_P32_OCC 3
+#endif
 template <>
 struct PairGeom<32> {
-  static constexpr int BN = 512, WM = 1, WN = 4, RS = 64, SW_MUL = 1, SW_S = 1, SW_M = 3, D = TTS_P32_D, MT = 2, OCC = 3;
+  static constexpr int BN = 512, WM = 1, WN = 4, RS = 64, SW_MUL = 1, SW_S = 1, SW_M = 3, D = TTS_P32_D, MT = 2, OCC = TTS_P32_OCC;
 };
 #ifndef TTS_P64_OCC
 #define TTS_P64_OCC 3

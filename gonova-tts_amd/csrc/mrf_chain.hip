@@ -42,7 +42,7 @@ struct ChainGeom;
 #define TTS_CHAIN_BN32_7 320
 #endif
 #ifndef TTS_CHAIN_BN64_3
-#define TTS_CHAIN_BN64_3 128
+#define TTS_CHAIN_BN64_3 160
 #endif
 #ifndef TTS_CHAIN_BN64_7
 #define TTS_CHAIN_BN64_7 128

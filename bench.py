@@ -256,11 +256,11 @@ class Ctx:
         if not self.cpu:
             self.torch.cuda.synchronize()
         # Live kernel timing (hipEvents around every MFMA launch, on its own stream) brackets
-        # the LAST `nprof` timed steps only: two events per launch cost ~0.3 ms per C2 step
-        # (1.6 %), which production runs do not pay.  The per-family averages come from those
-        # steps, inside the timed region.
+        # the LAST timed step only: two events per launch cost ~0.3 ms per C2 step (1.6 %),
+        # which production runs do not pay.  The per-family averages come from that step (27
+        # pair launches in C2), inside the timed region.
         prof_on = eng is not None and not os.environ.get("TTS_BENCH_NOPROF")
-        nprof = max(1, min(steps, 2, steps // 4 or 1))
+        nprof = 1
         self.barrier()
         t0 = time.perf_counter()
         for i in range(steps):

@@ -124,6 +124,9 @@ constexpr int pair_bn() {
   return PairGeom<C>::BN;
 }
 
+#ifndef TTS_P256K11_D
+#define TTS_P256K11_D 2  // weight-ring depth of the full-height C = 256 k = 11 pairs (the others: TTS_P256_D)
+#endif
 #ifndef TTS_P32K11_OCC
 #define TTS_P32K11_OCC 3
 #endif
@@ -137,7 +140,9 @@ struct PairGeomS : PairGeom<C> {
   // trips are exposed unless it runs further ahead; the depth only moves loads earlier (same
   // k-step order: bit-identical).  C = 256, D 2 -> 4 (profiles/r04t_ab_short_ring.txt): the C5
   // chunk's stage-0 pairs 337 -> 266 us, C5 3.44 -> 3.36 ms (8: 270 us)
-  static constexpr int D = DIV > 1 && C == 256 ? TTS_PAIR_SHORT_D256 : PairGeom<C>::D;
+  static constexpr int D = DIV > 1 && C == 256 ? TTS_PAIR_SHORT_D256
+                           : DIV == 1 && C == 256 && K == 11 ? TTS_P256K11_D
+                                                             : PairGeom<C>::D;
   // blocks per CU the register budget is sized for (the C = 32 k = 11 pairs without conv_post
   // may take a fourth: TTS_P32K11_OCC)
   static constexpr int OCC = C == 32 && K == 11 && !POST && DIV == 1 ? TTS_P32K11_OCC : PairGeom<C>::OCC;

@@ -10,8 +10,9 @@
 // the next tile inside the same waves cannot hide that latency: vmcnt retires in issue order, so
 // the weight ring's waits would wait for any older staging load.
 //
-// Block = 4 compute waves (the pair kernel's wave grid, PairGeom<C>) + NL loader waves, two LDS
-// buffers, persistent over a contiguous range of (utterance, row tile) items per XCD:
+// Block = 4 x TTS_PAIR_WS_WN compute waves (16 * MT channels x a share of the rows each) + NL
+// loader waves, two LDS buffers, persistent over a contiguous range of (utterance, row tile) items
+// per XCD:
 //   loader:  DMA (buffer_load ... lds) of tile k+1's input rows h into the other buffer, with the
 //            G tile's chunk swizzle on the source address (rows outside the utterance read 0
 //            through the descriptor's range), then LeakyReLU in place -> G;
@@ -24,8 +25,10 @@
 //   C(k)  T written;                loader's DMA of G_{k+1} issued into the other buffer
 //   D(k)  conv2 done reading T;     G_{k+1} landed and activated
 // The loader waves have their own vmcnt, so the MFMA waves' weight-ring waits never wait on a
-// staging load or a store.  Compute waves: 2 per SIMD (two blocks per CU), as the C = 256 pair
-// kernel runs; loader waves take the third slot.
+// staging load or a store.  Default: 8 compute + 4 loader waves, one block per CU (3 waves per
+// SIMD; a block's waves must spread evenly over the 4 SIMDs, which 6-wave blocks do not).
+// Measured slower than mrf_pair_kernel (profiles/r04i_ab_pair_ws.txt: with one block per CU
+// nothing overlaps the MFMA waves' own epilogues), so TTS_PAIR_WS is off by default.
 #include "common.h"
 #include "kernels.h"
 #include "mrf_tile.h"

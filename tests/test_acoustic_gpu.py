@@ -142,7 +142,7 @@ def test_end_to_end_fp32_matches_golden(aw):
     mel, mel_lens, _ = run(eng, [ids], t_cap=64)
     L = int(mel_lens[0])
     wav = eng.vocoder(torch.from_numpy(mel[:, :L].copy()).to(DEV)).cpu().numpy()[0]
-    np.testing.assert_allclose(wav, G["e2e_wav"], atol=2e-4, rtol=2e-3)
+    np.testing.assert_allclose(wav, G["e2e_wav"], atol=FP32_ATOL, rtol=FP32_RTOL)
 
 
 GS = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_spk.npz"))

@@ -35,7 +35,7 @@ def test_generate_matches_oracle_pipeline(model32):
     ref = vocoder_forward(o["mel"], make_vocoder_weights(0))
     got = model32.generate(text).squeeze().cpu().numpy()
     assert got.shape == ref.shape
-    np.testing.assert_allclose(got, ref, atol=5e-4, rtol=5e-3)
+    np.testing.assert_allclose(got, ref, atol=2e-5, rtol=1e-4)
 
 
 def test_generate_batch_equals_single(model32):

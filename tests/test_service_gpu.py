@@ -73,7 +73,7 @@ def test_service_frames_equal_generate_and_oracle(served):
         assert f.shape == ref.shape
         err = float(np.abs(f - ref).max())
         print(f"service frame {s!r}: {f.size} samples, max|err| vs oracle {err:.2e}")
-        np.testing.assert_allclose(f, ref, atol=2e-4, rtol=2e-3)
+        np.testing.assert_allclose(f, ref, atol=2e-5, rtol=1e-4)
     m = c.get("/metrics").json()
     assert m["chunks_sent"] >= 4 and m["requests_dropped"] == 0
     h = c.get("/health").json()

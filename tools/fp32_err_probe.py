@@ -23,6 +23,7 @@ def main():
     eng.load_weights(acoustic=aw)
 
     def run(ids_list, t_cap):
+        nonlocal eng
         B, N = len(ids_list), max(len(x) for x in ids_list)
         tok = np.zeros((B, N), np.int32)
         for b, x in enumerate(ids_list):
@@ -53,6 +54,18 @@ def main():
         d = np.abs(mel[b, :L] - r)
         print(f"oracle b={b}: max abs {d.max():.3e}, max rel {np.max(d / (np.abs(r) + 1e-3)):.3e}, "
               f"rel-rms {np.sqrt(np.mean(d ** 2)) / np.sqrt(np.mean(r ** 2)):.3e}")
+    eng.close()
+    # end to end (tests/test_acoustic_gpu.py::test_end_to_end_fp32_matches_golden)
+    from gonova_tts_amd.weights import make_vocoder_weights
+    eng = HipEngine("cuda:0", acoustic_dtype="f32", vocoder_dtype="f32")
+    eng.load_weights(acoustic=aw, vocoder=make_vocoder_weights(seed=0))
+    mel, ml, _ = run([G["ac_a_ids"]], 64)
+    L = int(ml[0])
+    wav = eng.vocoder(torch.from_numpy(mel[:, :L].copy()).cuda()).cpu().numpy()[0]
+    ref = G["e2e_wav"]
+    d = np.abs(wav - ref)
+    print(f"e2e wav: max abs {d.max():.3e}, rel-rms {np.sqrt(np.mean(d ** 2)) / np.sqrt(np.mean(ref ** 2)):.3e}, "
+          f"max |d| - 1e-4 |ref| {np.max(d - 1e-4 * np.abs(ref)):.3e}")
     eng.close()
 
 

@@ -35,10 +35,22 @@ namespace tts {
 template <int CIN, int M>
 struct UpGeom;
 // NU: 16-row tiles per item; NW: waves per block (LDS: weights + NW staging slices)
+#ifndef TTS_UP2_NU
+#define TTS_UP2_NU 1
+#endif
+#ifndef TTS_UP2_NW
+#define TTS_UP2_NW 12
+#endif
+#ifndef TTS_UP3_NU
+#define TTS_UP3_NU 2
+#endif
+#ifndef TTS_UP3_NW
+#define TTS_UP3_NW 8
+#endif
 template <>
-struct UpGeom<128, 128> { static constexpr int NU = 1, NW = 12; };  // stage 2: 64 KB weights
+struct UpGeom<128, 128> { static constexpr int NU = TTS_UP2_NU, NW = TTS_UP2_NW; };  // stage 2: 64 KB weights
 template <>
-struct UpGeom<64, 64> { static constexpr int NU = 2, NW = 8; };     // stage 3: 16 KB weights
+struct UpGeom<64, 64> { static constexpr int NU = TTS_UP3_NU, NW = TTS_UP3_NW; };     // stage 3: 16 KB weights
 
 template <int CIN, int M>
 constexpr size_t up_lds_bytes() {

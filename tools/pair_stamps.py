@@ -48,6 +48,9 @@ def run(targets):
 
 
 def analyze(rec, t):
+    if len(rec) == 0:  # e.g. a launch with conv_post fused, which returns before stamping
+        print(f"C={t[0]} k={t[1]} d={t[2]}: no records")
+        return
     st = rec[:, :7].astype(np.float64)
     rt0, rt1 = rec[:, 7].astype(np.float64), rec[:, 8].astype(np.float64)
     n = len(rec)

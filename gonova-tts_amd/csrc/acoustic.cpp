@@ -664,8 +664,18 @@ bool AcousticModel::encoder_f32() const { return impl && impl->enc_f32; }
 
 void AcousticModel::range_flag_to(int32_t* dst, hipStream_t s) {
   if (!impl) throw TtsError(TTS_ERR_STATE, "acoustic model not loaded");
-  HIP_CHECK(hipMemcpyAsync(dst, impl->range_flag, 4, hipMemcpyDefault, s));
-  HIP_CHECK(hipMemsetAsync(impl->range_flag, 0, 4, s));
+  // device (or managed) destination: one small kernel copies and clears the word; host memory:
+  // an async copy and a fill
+  hipPointerAttribute_t at{};
+  const bool dev = hipPointerGetAttributes(&at, dst) == hipSuccess &&
+                   (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged);
+  if (!dev) (void)hipGetLastError();  // (a plain host pointer reports an error: cleared)
+  if (dev) {
+    HIP_CHECK(launch_range_take(impl->range_flag, dst, s));
+  } else {
+    HIP_CHECK(hipMemcpyAsync(dst, impl->range_flag, 4, hipMemcpyDefault, s));
+    HIP_CHECK(hipMemsetAsync(impl->range_flag, 0, 4, s));
+  }
 }
 
 void AcousticModel::free_all() {

@@ -31,6 +31,7 @@ hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, in
 hipError_t launch_spk_bias(int dt, const float* e, int B, int E, const float* We, const float* bias, int D, void* out,
                            hipStream_t s);
 
+hipError_t launch_range_take(int* src, int* dst, hipStream_t s);
 // attention.hip: fused relative-position attention (dk = 192): 16-bit dtypes, fp32 (exact f32
 // MFMA) and, with split set, fp32 in split precision (three f16 MFMAs per product)
 bool rel_attn_supported(int dt, int D, int H);

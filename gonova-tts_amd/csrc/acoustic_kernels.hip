@@ -641,6 +641,20 @@ hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, in
                                       out));
 }
 
+// range word read-out (tts_acoustic_range_flag): copy the word to the caller's device buffer and
+// clear it, one launch instead of a copy and a fill
+__global__ void range_take_kernel(int* __restrict__ src, int* __restrict__ dst) {
+  if (threadIdx.x == 0) {
+    dst[0] = src[0];
+    src[0] = 0;
+  }
+}
+
+hipError_t launch_range_take(int* src, int* dst, hipStream_t s) {
+  hipLaunchKernelGGL(range_take_kernel, dim3(1), dim3(64), 0, s, src, dst);
+  return hipGetLastError();
+}
+
 hipError_t launch_spk_bias(int dt, const float* e, int B, int E, const float* We, const float* bias, int D, void* out,
                            hipStream_t s) {
   TTS_DISPATCH(dt, hipLaunchKernelGGL(spk_bias_kernel<TT>, dim3(B), dim3(256), 0, s, e, E, We, bias, D, (TT*)out));

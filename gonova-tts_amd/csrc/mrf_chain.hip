@@ -98,9 +98,19 @@ struct ChainGeom<128, 3> { static constexpr int BN = TTS_CHAIN_BN128_3, OCC = TT
 
 constexpr int CHAIN_D0 = 1, CHAIN_D1 = 3, CHAIN_D2 = 5;  // HiFi-GAN V1/V2 dilations
 
-template <int C, int K>
+// tile height by dtype: the bf16 C = 64 k = 3 chain keeps 128 rows (at 160 its f32 epilogue
+// arithmetic spills past 168 VGPRs; the f16 form fits: 142)
+#ifndef TTS_CHAIN_BN64_3_BF16
+#define TTS_CHAIN_BN64_3_BF16 128
+#endif
+template <typename T, int C, int K>
+constexpr int chain_bn() {
+  return C == 64 && K == 3 && !__is_same(T, half_t) ? TTS_CHAIN_BN64_3_BF16 : ChainGeom<C, K>::BN;
+}
+
+template <int C, int K, int BNV = ChainGeom<C, K>::BN>
 struct ChainPlan {
-  static constexpr int BN = ChainGeom<C, K>::BN;
+  static constexpr int BN = BNV;
   static constexpr int A = (K - 1) / 2;
   static constexpr int DIL[3] = {CHAIN_D0, CHAIN_D1, CHAIN_D2};
   // first row each pair's output must cover (s[3] = H0)
@@ -119,9 +129,9 @@ struct ChainPlan {
   static constexpr int NRA = cmax(NR, cmax(top(0), cmax(top(1), top(2))));
 };
 
-template <int C, int K>
+template <typename T, int C, int K>
 static size_t chain_lds_bytes() {
-  return (size_t)2 * ChainPlan<C, K>::NRA * PairGeom<C>::RS;
+  return (size_t)2 * ChainPlan<C, K, chain_bn<T, C, K>()>::NRA * PairGeom<C>::RS;
 }
 
 // 4 x T: (y + h), rounded as epi_row does for the intermediate h' (scale 1, no accumulate)
@@ -149,7 +159,7 @@ __device__ inline uint2 lrelu4(uint2 v, float slope) {  // 4 x T, 0 <= slope <= 
 template <typename T, int C, int K>
 __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(MrfChainParams p) {
   using G = PairGeom<C>;
-  using P = ChainPlan<C, K>;
+  using P = ChainPlan<C, K, chain_bn<T, C, K>()>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int BN = P::BN, WM = C / 32, WN = 4 / WM, RS = G::RS, D = G::D, A = P::A;  // 32 channels per wave
   constexpr int NTHR = 256, MT = 2, KS = C / 32, S = K * KS, VPR = C / 8;
@@ -357,9 +367,9 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
 
 template <typename T, int C, int K>
 static hipError_t launch_chain_t(const MrfChainParams& p, hipStream_t s) {
-  constexpr int BN = ChainGeom<C, K>::BN;
-  const size_t lds = chain_lds_bytes<C, K>();
-  static_assert(2 * ChainPlan<C, K>::NRA * PairGeom<C>::RS * ChainGeom<C, K>::OCC <= 160 * 1024, "LDS for OCC blocks per CU");
+  constexpr int BN = chain_bn<T, C, K>();
+  const size_t lds = chain_lds_bytes<T, C, K>();
+  static_assert(2 * ChainPlan<C, K, BN>::NRA * PairGeom<C>::RS * ChainGeom<C, K>::OCC <= 160 * 1024, "LDS for OCC blocks per CU");
   dim3 grid(xcd_grid((p.T + BN - 1) / BN, p.B));
   hipLaunchKernelGGL((mrf_chain_kernel<T, C, K>), grid, dim3(256), lds, s, p);
   return hipGetLastError();

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
   const int ylen = p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows;
   if (n0 >= ylen) return;
   const int xlen = p.x_len ? min(p.x_len[b], p.x_rows) : p.x_rows;
-  const int m_blk = blockIdx.y * BM;
+  const int m_blk = by * BM;  // (the decoded M block on the XCD-ordered grid)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1043,13 +1043,9 @@ static hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-static int wide_mode() { return sw(SW_CONV_WIDE) > 0; }
-
 template <typename T>
 static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
   constexpr int CKW = 64 / (int)sizeof(T);   // 32 x 16-bit / 16 x f32 (64-byte rows)
-  constexpr int CKWW = 128 / (int)sizeof(T); // 64 x 16-bit / 32 x f32 (128-byte rows)
-  const bool wide = wide_mode() && p.Cin % CKWW == 0 && p.Cin >= 2 * CKWW;
   // fp32 head-batched attention products of the exact-duration encoder (M = 144-288 keys /
   // 192 channels, K = 144-192, 144 query rows, batch x heads): when the 128 x 128 grid would
   // fill under half the CUs (batch 8: 64 blocks), 64 x 64 tiles with 128-byte channel chunks,
@@ -1059,17 +1055,14 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
     if (p.nh > 1 && (long long)((p.y_rows + 127) / 128) * ((p.M + 127) / 128) * p.B * p.nh < 128)
       return p.Cin % 32 == 0 ? launch_cfg<T, 1, 1, 2, 2, 32>(p, s) : launch_cfg<T, 1, 1, 2, 2, CKW>(p, s);
   if (p.M <= 32) {
-    if (wide) return launch_cfg<T, 1, 2, 1, 4, CKWW>(p, s);
     return launch_cfg<T, 1, 2, 1, 4, CKW>(p, s);
   }
   if (p.M <= 64) {
-    if (wide) return launch_cfg<T, 1, 2, 2, 2, CKWW>(p, s);
     return launch_cfg<T, 1, 2, 2, 2, CKW>(p, s);
   }
   // M >= 128: 4 waves stacked along M, 32 x 128 per wave.  (A 32 x 256 strip per wave
   // cuts the L2-served weight bytes per MFMA in half but needs 235 VGPRs -> 2 waves/SIMD,
   // and measured 1.8x slower: the kernel is latency/issue-bound, not weight-bandwidth-bound.)
-  if (wide) return launch_cfg<T, 1, 4, 4, 1, CKWW>(p, s);
   return launch_cfg<T, 1, 4, 4, 1, CKW>(p, s);
 }
 

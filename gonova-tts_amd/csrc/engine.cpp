@@ -55,9 +55,6 @@ struct VocoderWeights {
   int hop = 256;
 };
 
-#ifndef TTS_PAIR_SP_DEFAULT
-#define TTS_PAIR_SP_DEFAULT 0  // 1: C = 32 pairs on the software-pipelined kernel (measured slower)
-#endif
 // TTS_MRF_FUSED=0 selects the unfused per-conv path (A/B and parity tests)
 static bool mrf_fused_enabled() { return sw(SW_MRF_FUSED) != 0; }
 // resblock chain kernel for the HBM-bound resblocks (default on; TTS_MRF_CHAIN=0: pairs only)
@@ -474,18 +471,12 @@ struct tts_engine {
               post_done = true;
             }
             const double fl = 2.0 * 2.0 * ch * (double)ch * pp.k * (double)B * Tout;
-            // C = 32 pairs without conv_post: the software-pipelined kernel (bit-identical)
-            const int spsw = sw(SW_PAIR_SP);
-            const bool sp = !pp.post_wpk && (spsw < 0 ? TTS_PAIR_SP_DEFAULT : spsw) != 0 && mrf_pair_sp_supported(dt, ch, pp.k);
             // the stage's final MRF sum feeds only the next upsampler: store it activated
-            if (last && j == nk - 1 && i + 1 < nst && !pp.post_wpk && !sp && mrf_pair_outact_supported(dt, ch, pp.k)) {
+            if (last && j == nk - 1 && i + 1 < nst && !pp.post_wpk && mrf_pair_outact_supported(dt, ch, pp.k)) {
               pp.out_act = 1; pp.out_slope = slope;
               s_act = true;
             }
-            const bool ws = !sp && !pp.post_wpk && mrf_pair_ws_supported(dt, ch, pp);
-            auto launch = [&] {
-              return sp ? mrf_pair_sp_launch(dt, ch, pp, s) : ws ? mrf_pair_ws_launch(dt, ch, pp, s) : mrf_pair_launch(dt, ch, pp, s);
-            };
+            auto launch = [&] { return mrf_pair_launch(dt, ch, pp, s); };
             if (prof.on) {
               Profiler::Rec r{prof.get(), prof.get(), fl, PK_MRF_PAIR};
               HIP_CHECK(hipEventRecord(r.a, s));

@@ -120,10 +120,6 @@ struct MrfPairParams {
   float out_slope;
 };
 bool mrf_pair_supported(int dtype, int C, int k);
-// warp-specialised persistent pair kernel (mrf_pair_ws.hip): k = 3 at C = 128 / 256, bit-identical
-// to mrf_pair_kernel; TTS_PAIR_WS switches it
-bool mrf_pair_ws_supported(int dtype, int C, const MrfPairParams& p);
-hipError_t mrf_pair_ws_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s);
 bool mrf_pair_outact_supported(int dtype, int C, int k);  // the launch can carry out_act
 
 // Streaming ConvTranspose1d with two taps (k = 2s) for the small upsamplers (upsample.hip):
@@ -145,9 +141,6 @@ bool upsample_stream_supported(int dtype, int Cin, int M, int taps);
 hipError_t upsample_stream_launch(int dtype, int Cin, int M, const UpsampleParams& p, hipStream_t s);
 // the pair launch can carry conv_post (C, k and post_k it was compiled for)
 bool mrf_pair_post_supported(int dtype, int C, int post_k);
-// software-pipelined pair for C = 32 (mrf_pair_sp.hip): same arithmetic, bit-identical; no conv_post
-bool mrf_pair_sp_supported(int dtype, int C, int k);
-hipError_t mrf_pair_sp_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s);
 hipError_t mrf_pair_launch(int dtype, int C, const MrfPairParams& p, hipStream_t s);
 
 // Fused resblock (mrf_chain.hip): the three pairs of one resblock (dilations 1, 3, 5) in one

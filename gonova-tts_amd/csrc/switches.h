@@ -15,18 +15,15 @@ enum Sw : int {
   SW_CONV_XRES,    // TTS_CONV_XRES=0: no X-resident conv kernel
   SW_XRES_NARROW,  // TTS_XRES_NARROW=0/1: force conv_xres narrow tiles off / on
   SW_XRES_NT,      // TTS_XRES_NT=2/4: force conv_xres tile height
-  SW_CONV_WIDE,    // TTS_CONV_WIDE=1: 128-byte channel chunks in conv_gemm
   SW_SPLIT_TILE,   // TTS_SPLIT_TILE=1/2: force the per-utterance split GEMM tile
   SW_PAIR_DIV,     // TTS_PAIR_DIV=1: full-height pair tiles; any other value: short tiles
   SW_ATTN_SPLIT,   // TTS_ATTN_SPLIT=0: the exact encoder's fused attention on f32 MFMA, not split
   SW_ATTN_KSPLIT,  // TTS_ATTN_KSPLIT=1: 16-bit attention with two key groups per block (8 waves)
-  SW_PAIR_SP,      // TTS_PAIR_SP=0: C = 32 pairs on mrf_pair_kernel instead of the pipelined mrf_pair_sp_kernel
   SW_SPLIT_WHOLE,  // TTS_SPLIT_WHOLE=0: small split-precision GEMMs stage one channel group at a time
   SW_XRES_DMA,     // TTS_XRES_DMA=0: FFN convs / upsamplers register-staged with round-2 channel groups; 2: register-staged, same bits
   SW_LN_FUSE,      // TTS_LN_FUSE=0: acoustic post-LNs as their own launches; 7: in every eligible GEMM launch (2-6: bisection)
   SW_SPLIT_NT1,    // TTS_SPLIT_NT1=0: split GEMMs always on 64-row tiles; 1: 32-row tiles wherever eligible (default: small grids)
   SW_XRES_ORDER,   // TTS_XRES_ORDER=1: multi-tap DMA conv_xres launches on an XCD-ordered grid (M block fastest); 2: every conv_xres launch
-  SW_PAIR_WS,      // TTS_PAIR_WS=0/1: k = 3 pairs at C >= 128 on the warp-specialised persistent kernel off / on
   SW_N
 };
 

@@ -62,9 +62,12 @@ class ShardedSynthesis:
     """Run one batch of utterances across all ranks of a process group, results on `root`.
 
     synth_fn(tokens int32 [b, N], lens int32 [b]) -> (wav tensor [b, S] float32, wav_lens int64 [b])
-    runs on the calling rank's device (a GonovaTTS.synthesize_tokens, or a fake on CPU).  wav_lens
-    may be a numpy array or a device tensor; with device tensors (synthesize_tokens(...,
-    host_lens=False)) every bucket is queued before the first host sync.  On the root the
+    or (wav, wav_lens, pending) runs on the calling rank's device (a GonovaTTS.synthesize_tokens, or
+    a fake on CPU).  wav_lens may be a numpy array or a device tensor; with device tensors
+    (synthesize_tokens(..., host_lens=False)) every bucket is queued before the first host sync.
+    `pending` (model.PendingRange, or None) carries the bucket's unread range word: it is read in
+    the same device -> host copy as the lengths, and a bucket whose word is set is synthesized
+    again on the fp32 encoder there (pending.resolve) before its audio is packed.  On the root the
     waveforms come back as views into one host buffer per rank (one pinned D2H copy each).
     """
 
@@ -117,11 +120,14 @@ class ShardedSynthesis:
         side = torch.cuda.Stream(device=dev) if overlap else None
         for bk in mine:  # queue every bucket first: no host sync between them
             n_b = int(ln_h[bk].max())
+            pend = None
             if n_b == 0:  # only empty utterances: nothing to synthesize, empty waveforms
                 wav = torch.zeros((len(bk), 0), dtype=torch.float32, device=dev)
                 wav_lens = np.zeros(len(bk), np.int64)
             else:
-                wav, wav_lens = self.synth_fn(tok_h[bk, :n_b], ln_h[bk])
+                res = self.synth_fn(tok_h[bk, :n_b], ln_h[bk])
+                wav, wav_lens = res[0], res[1]
+                pend = res[2] if len(res) > 2 else None
             host = None
             if overlap:
                 ev = torch.cuda.Event()
@@ -131,10 +137,18 @@ class ShardedSynthesis:
                     side.wait_event(ev)
                     host.copy_(wav, non_blocking=True)
                 wav.record_stream(side)
-            done.append((bk, wav, wav_lens, host))
+            done.append((bk, wav, wav_lens, host, pend))
         own = []
-        for bk, wav, wav_lens, host in done:
-            if isinstance(wav_lens, torch.Tensor):
+        for bk, wav, wav_lens, host, pend in done:
+            if pend is not None:  # the lengths and the range word in one read
+                h = torch.cat([torch.as_tensor(wav_lens, device=pend.word.device).to(torch.int64).reshape(-1),
+                               pend.word.to(torch.int64).reshape(-1)]).cpu().numpy()
+                wav2, wav_lens = pend.resolve(wav, h[:-1], int(h[-1]))
+                if wav2 is not wav:  # rerun on the fp32 encoder: its own copy to the host
+                    wav = wav2
+                    if overlap:
+                        host = wav.cpu()
+            elif isinstance(wav_lens, torch.Tensor):
                 wav_lens = wav_lens.cpu().numpy()
             if overlap:
                 own.append((bk, wav_lens, host))

@@ -343,7 +343,10 @@ class HipEngine:
                                                 t_cap, ctypes.c_void_p(dur_out.data_ptr()), _stream_ptr(stream)),
               "tts_acoustic_forward")
         rw = None
-        if self.range_guard:
+        # the word is copied out and cleared only for a caller that reads it: otherwise it keeps
+        # accumulating, so the next caller that asks sees an earlier unread overflow too (a spurious
+        # fp32 rerun at worst, never a lost one)
+        if self.range_guard and return_range:
             rw = torch.empty((1,), dtype=torch.int32, device=tokens.device)
             check(self.lib.tts_acoustic_range_flag(self.handle, ctypes.c_void_p(rw.data_ptr()), _stream_ptr(stream)),
                   "tts_acoustic_range_flag")

@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import os
 import threading
-from contextlib import contextmanager
+from contextlib import contextmanager, nullcontext
 from math import gcd
 from typing import Dict, List, Optional
 
@@ -123,14 +123,15 @@ class GonovaTTS:
     def synthesize_tokens(self, tokens: np.ndarray, lens: np.ndarray, durations: Optional[np.ndarray] = None,
                           stream=None, speaker_embedding: Optional[np.ndarray] = None, host_lens: bool = True):
         """tokens int32 [B, N], lens [B] -> (wav cuda float32 [B, T*256], wav_lens np.int64 [B]).
-        host_lens=False returns wav_lens as a cuda int64 tensor instead: no host sync, so a caller
-        can queue several batches back to back (dist.ShardedSynthesis).
+        host_lens=False makes no host sync, so a caller can queue several batches back to back
+        (dist.ShardedSynthesis), and returns (wav, wav_lens cuda int64 [B], pending): `pending` is
+        None when nothing is left to check, else a PendingRange whose `word` the caller reads with
+        the lengths at its own sync and whose `resolve(...)` reruns the batch when it is set.
 
         Range guard (include/tts_hip.h, ABI 4): with the exact encoder of a 16-bit model the
         acoustic forward's range word travels with the one host read this path makes anyway; when a
         split-precision operand was outside f16's range the batch is synthesized again with the
-        encoder on the exact fp32 MFMA kernels (`range_fallbacks` counts these).  host_lens=False
-        makes no host read, so no word is read there."""
+        encoder on the exact fp32 MFMA kernels (`range_fallbacks` counts these)."""
         import torch
         dev = self.engine.torch_device
         B, N = tokens.shape
@@ -145,9 +146,13 @@ class GonovaTTS:
         # ops below): an executor thread of a multi-GPU service starts on device 0
         with torch.cuda.device(self.engine.device_index):
             wav, wav_lens, tripped = self._synthesize_once(*args)
-            if tripped:
+            if tripped is True:  # read on the host already (predicted durations)
                 with self._range_fallback():
                     wav, wav_lens, _ = self._synthesize_once(*args)
+                tripped = None
+            if not host_lens:  # tripped: the unread range word (device) or None; the caller reads it
+                pend = PendingRange(self, args[:-1] + (True,), tripped) if isinstance(tripped, torch.Tensor) else None
+                return wav, wav_lens, pend
         return wav, wav_lens
 
     @property
@@ -166,7 +171,9 @@ class GonovaTTS:
             yield
 
     def _synthesize_once(self, tok, tl, dd, t_cap, stream, spk, host_lens):
-        """-> (wav, wav_lens, range guard tripped: bool, or None when nothing was read)"""
+        """-> (wav, wav_lens, range guard tripped: bool, or None when nothing was read); with
+        host_lens=False the third item is the forward's range word itself (cuda int32 [1], None
+        without the guard), unread"""
         import torch
         mel, mel_lens, dur, rw = self.engine.acoustic(tok, tl, t_cap, durations=dd, stream=stream,
                                                       return_durations=True, speaker_embedding=spk, return_range=True)
@@ -191,7 +198,7 @@ class GonovaTTS:
                                                  self.native_sr // g, stream=stream)
             out_lens = out_lens.to(torch.int64)
             if not host_lens:
-                return wav, out_lens, None
+                return wav, out_lens, rw if tripped is None else None
             if tripped is None:
                 h, tripped = _read_with_range(out_lens, rw)
                 return wav, h, tripped
@@ -200,7 +207,7 @@ class GonovaTTS:
             return wav, lens_known * self.vocoder_cfg.hop, tripped
         wav_lens = mel_lens.to(torch.int64) * self.vocoder_cfg.hop
         if not host_lens:
-            return wav, wav_lens, None
+            return wav, wav_lens, rw if tripped is None else None
         h, tripped = _read_with_range(wav_lens, rw)
         return wav, h, tripped
 
@@ -256,9 +263,12 @@ class GonovaTTS:
                 need, lens_h, _ = _need_and_lens(dur, mel_lens)
             if need > t_cap:
                 first = None
-                mel, mel_lens, dur, rw = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
-                                                              return_durations=True, speaker_embedding=spk,
-                                                              return_range=True)
+                # after a fallback the second pass stays on the fp32 encoder: its activations do not
+                # depend on the durations, so the split encoder would overflow again
+                with (self.engine.encoder_f32() if fell_back else nullcontext()):
+                    mel, mel_lens, dur, rw = self.engine.acoustic(tok, tl, need, durations=dur, stream=stream,
+                                                                  return_durations=True, speaker_embedding=spk,
+                                                                  return_range=True)
                 need, lens_h, tripped = _need_and_lens(dur, mel_lens, rw)
                 if tripped and not fell_back:
                     with self._range_fallback():
@@ -406,6 +416,25 @@ class GonovaTTS:
 # Alias with the reference's class name so `from gonova_tts_amd.model import ChatterboxTTS`
 # is a one-line swap at synthesizer.py:167.
 ChatterboxTTS = GonovaTTS
+
+
+class PendingRange:
+    """The range word of a batch synthesized with host_lens=False, not yet read (dist.ShardedSynthesis
+    reads it with the wave lengths at the one sync it makes).  resolve(lens_host, word_host) returns
+    the batch's final (wav, wav_lens np.int64) -- the queued result when the word is 0, else the
+    batch synthesized again with the encoder on fp32 MFMA (one RuntimeWarning, range_fallbacks + 1)."""
+
+    def __init__(self, model: "GonovaTTS", args, word):
+        self.model, self.args, self.word = model, args, word
+
+    def resolve(self, wav, lens_host, word_host: int):
+        if not word_host:
+            return wav, lens_host
+        import torch
+        m = self.model
+        with torch.cuda.device(m.engine.device_index), m._range_fallback():
+            wav, wav_lens, _ = m._synthesize_once(*self.args)
+        return wav, np.asarray(wav_lens, np.int64)
 
 
 def _need_and_lens(dur, mel_lens, rw=None):

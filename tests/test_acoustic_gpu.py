@@ -576,4 +576,28 @@ def test_range_guard_falls_back_to_fp32_encoder(aw):
     # the encoder is back on the split path afterwards: the next forward trips the word again
     *_, rw = e.acoustic(tok_d, lens_d, 12 * N, return_range=True)
     assert int(rw.item()) == 1
+    # the sharded path (dist.ShardedSynthesis, one rank, given durations, host_lens=False: no host
+    # read inside synthesize_tokens): the word is read with the lengths at the run's own sync and the
+    # tripped bucket is synthesized again on the fp32 encoder -- finite audio, not inf
+    from gonova_tts_amd.dist import ShardedSynthesis
+
+    def synth(t, l):
+        d = np.where(np.arange(t.shape[1])[None, :] < l[:, None], 6, 0).astype(np.int32)
+        return m.synthesize_tokens(t, l, durations=d, host_lens=False)
+
+    with pytest.warns(RuntimeWarning, match="f16 range"):
+        out = ShardedSynthesis(synth, torch.device(DEV), bucket=4).run(tok, lens)
+    assert m.range_fallbacks == 2
+    for b in range(B):
+        assert out[b].shape == (int(lens[b]) * 6 * 256,) and np.isfinite(out[b]).all(), b
+    # streaming with predicted durations: the first pass trips, the fallback runs on the
+    # fp32 encoder, and with a 64-frame first cap (the durations need 172 / 103 frames) the second,
+    # longer pass must stay on the fp32 encoder too
+    m.FRAMES_PER_TOKEN_CAP = 1
+    with pytest.warns(RuntimeWarning, match="f16 range"):
+        chunks = list(m.stream_tokens(tok, lens, chunk_frames=64))
+    assert m.range_fallbacks == 3
+    assert len(chunks) == 3  # 172 frames in 64-frame chunks: the second pass ran
+    for c0, wav, valid in chunks:
+        assert np.isfinite(wav.cpu().numpy()).all(), c0
     e.close()

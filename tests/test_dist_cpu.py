@@ -125,3 +125,77 @@ def test_all_empty_buckets_yield_empty_waveforms():
     out0 = ShardedSynthesis(synth, torch.device("cpu"), bucket=8).run(np.zeros((3, 4), np.int32),
                                                                       np.zeros(3, np.int32))
     assert all(o.shape == (0,) for o in out0)
+
+
+class FakePending:
+    """Stand-in for model.PendingRange: an unread range word; resolve() reruns the bucket."""
+
+    def __init__(self, tokens, lens, tripped, log):
+        self.word = torch.tensor([1 if tripped else 0], dtype=torch.int32)
+        self.tokens, self.lens, self.log = tokens, lens, log
+
+    def resolve(self, wav, lens_host, word_host):
+        if not word_host:
+            return wav, lens_host
+        self.log.append(len(self.lens))
+        w, wl = fake_synth(self.tokens, self.lens)
+        return w, wl
+
+
+def guarded_synth(log, trip_token=99):
+    """host_lens=False-style engine: device-style lengths plus a pending range word; a bucket
+    holding token `trip_token` "overflows": its queued audio is inf and the word is set."""
+    def synth(t, l):
+        wav, wl = fake_synth(t, l)
+        tripped = bool((t == trip_token).any())
+        if tripped:
+            wav = torch.full_like(wav, float("inf"))
+        return wav, torch.from_numpy(wl), FakePending(t, l, tripped, log)
+    return synth
+
+
+def test_range_word_read_with_lengths_and_tripped_bucket_rerun():
+    """ShardedSynthesis reads a bucket's pending range word with its lengths (one host read) and
+    resolves a set word by synthesizing the bucket again (model.PendingRange.resolve): no inf
+    reaches the caller, the other buckets are untouched."""
+    tok, lens = make_batch(B=40, seed=3)
+    tok[5, 0] = 99
+    log = []
+    out = ShardedSynthesis(guarded_synth(log), torch.device("cpu"), bucket=8).run(tok, lens)
+    assert log == [8]  # exactly the one bucket holding utterance 5 was rerun
+    for o, e in zip(out, expected(tok, lens)):
+        assert np.isfinite(o).all()
+        np.testing.assert_array_equal(o, e)
+
+
+def _guard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tok, lens = make_batch()
+        tok[:, 0] = np.where(np.arange(len(lens)) % 7 == 0, 99, tok[:, 0])
+        log = []
+        out = ShardedSynthesis(guarded_synth(log), torch.device("cpu"), bucket=16).run(
+            tok if rank == 0 else None, lens if rank == 0 else None)
+        q.put(("reran", rank, len(log)))
+        if rank == 0:
+            exp = expected(tok, lens)
+            q.put(("ok", all(o is not None and np.isfinite(o).all() and np.array_equal(o, e) for o, e in zip(out, exp))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_range_guard_rerun_on_every_rank_gloo():
+    """The same on two gloo ranks: each rank resolves its own tripped buckets before the gather."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_guard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    msgs = [q.get(timeout=10) for _ in range(3)]
+    assert ("ok", True) in msgs
+    assert all(m[2] > 0 for m in msgs if m[0] == "reran")  # both ranks had a bucket to rerun

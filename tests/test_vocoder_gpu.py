@@ -195,53 +195,6 @@ def test_resblock_chain_bit_identical_to_pairs(vw, dtype, switch):
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-def test_pipelined_c32_pairs_bit_identical(vw, dtype, switch):
-    """The software-pipelined C = 32 pair kernel (mrf_pair_sp.hip: weights in registers, tile-
-    outer order, epilogues interleaved with the next tile's MFMAs, conv2's epilogue straight to
-    HBM) reproduces mrf_pair_kernel bit for bit: every stage-3 resblock as pair launches (chains
-    and the fused conv_post off, so k = 3, 7 and 11 and every dilation run through it), ragged
-    and empty utterances, an utterance of one frame (256 rows: one 240-row tile and a 16-row
-    one) and one of 15 frames (3,840 rows = 16 whole tiles)."""
-    eng = engine_for(dtype, vw)
-    rng = np.random.default_rng(25)
-    lens = [71, 1, 0, 15, 33, 64]
-    mel = torch.from_numpy(rng.standard_normal((6, 71, 80)).astype(np.float32)).to(DEV)
-    ln = torch.tensor(lens, dtype=torch.int32)
-    switch("TTS_MRF_FUSED", 1)
-    switch("TTS_MRF_CHAIN", 0)
-    switch("TTS_POST_FUSE", 0)
-    switch("TTS_PAIR_SP", 1)
-    sp = eng.vocoder(mel, ln).cpu().numpy()
-    switch("TTS_PAIR_SP", 0)
-    ref = eng.vocoder(mel, ln).cpu().numpy()
-    for b, L in enumerate(lens):
-        assert np.array_equal(sp[b], ref[b]), (b, float(np.abs(sp[b] - ref[b]).max()))
-        assert np.all(sp[b, L * 256:] == 0)
-
-
-@pytest.mark.parametrize("dtype", ["f16", "bf16"])
-def test_warp_specialised_pairs_bit_identical(vw, dtype, switch):
-    """The warp-specialised persistent k = 3 pair kernel at C = 256 / 128 (mrf_pair_ws.hip:
-    loader waves stage tile k+1 and store tile k-1 while the MFMA waves run tile k) reproduces
-    mrf_pair_kernel bit for bit: ragged, empty and one-frame utterances, and a batch large
-    enough that every block walks several (utterance, tile) items, so the double-buffer
-    hand-off between items -- across utterance boundaries too -- is exercised."""
-    eng = engine_for(dtype, vw)
-    rng = np.random.default_rng(26)
-    lens = [300, 1, 0, 2, 157, 299, 64, 33, 250, 8, 300, 199, 17, 71, 280, 3]
-    mel = torch.from_numpy(rng.standard_normal((16, 300, 80)).astype(np.float32)).to(DEV)
-    ln = torch.tensor(lens, dtype=torch.int32)
-    switch("TTS_PAIR_WS", 1)
-    ws = eng.vocoder(mel, ln).cpu().numpy()
-    switch("TTS_PAIR_WS", 0)
-    ref = eng.vocoder(mel, ln).cpu().numpy()
-    switch("TTS_PAIR_WS", None)
-    for b, L in enumerate(lens):
-        assert np.array_equal(ws[b], ref[b]), (b, float(np.abs(ws[b] - ref[b]).max()))
-        assert np.all(ws[b, L * 256:] == 0)
-
-
-@pytest.mark.parametrize("dtype", ["f16", "bf16"])
 def test_fused_conv_post_bit_identical(vw, dtype, switch):
     """conv_post inside the last pair launch (its halo rows computed in the block, the final
     MRF sum never written) reproduces the separate conv_post launch bit for bit: ragged and

@@ -1,6 +1,6 @@
 #!/bin/bash
 # usage (on the GPU box): bash tools/ab_env.sh <tag> <bench flags> "<env settings A>" "<env settings B>" ...
-#   e.g. bash tools/ab_env.sh r04e_ws "--no-full --no-c4 --no-streaming --no-c1" "TTS_PAIR_WS=0" "TTS_PAIR_WS=1"
+#   e.g. bash tools/ab_env.sh r04e_ws "--no-full --no-c4 --no-streaming --no-c1" "TTS_MRF_CHAIN=0" "TTS_MRF_CHAIN=1"
 # Same-box A/B of runtime switches (switches.h): each setting runs bench.py alternately, twice,
 # then one rocprof kernel trace + per-launch breakdown per setting.  Box-to-box clock
 # differences (~5 %) exceed most single-change effects, so compare only within one call.

@@ -45,17 +45,22 @@ def _compile(src, force, build_dir=BUILD, defines=()):
     return obj, True
 
 
-def build(force: bool = False, verbose: bool = True, variant: str = "", defines=()) -> str:
+def build(force: bool = False, verbose: bool = True, variant: str = "", defines=(), only=()) -> str:
     """variant/defines: an A/B build (-D tunables) into build_<variant>/ and
-    libtts_hip_<variant>.so, loaded with TTS_LIB=<path> (tools/ab.sh); the product is LIB."""
+    libtts_hip_<variant>.so, loaded with TTS_LIB=<path> (tools/ab.sh); the product is LIB.
+    only: source basenames the variant recompiles (the defines touch nothing else); every other
+    object comes from the product build."""
     build_dir = BUILD + ("_" + variant if variant else "")
     lib = LIB if not variant else os.path.join(PKG, f"libtts_hip_{variant}.so")
     os.makedirs(build_dir, exist_ok=True)
     srcs = _sources()
-    jobs = min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
+    if only and variant:
+        build(verbose=False)  # the product objects the variant reuses
+    mine = [s for s in srcs if not (only and variant) or os.path.basename(s) in only]
+    jobs = min(len(mine), max(1, min(8, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(jobs) as ex:
-        results = list(ex.map(lambda s: _compile(s, force, build_dir, defines), srcs))
-    objs = [o for o, _ in results]
+        results = list(ex.map(lambda s: _compile(s, force, build_dir, defines), mine))
+    objs = [o for o, _ in results] + [os.path.join(BUILD, os.path.basename(s) + ".o") for s in srcs if s not in mine]
     rebuilt = any(r for _, r in results)
     if rebuilt or not os.path.exists(lib) or force:
         cmd = [HIPCC, "-shared", "-fPIC", "-Wl,-z,defs", f"--offload-arch={ARCH}", "-o", lib] + objs
@@ -70,4 +75,5 @@ def build(force: bool = False, verbose: bool = True, variant: str = "", defines=
 if __name__ == "__main__":
     a = sys.argv[1:]
     var = a[a.index("--variant") + 1] if "--variant" in a else ""
-    build(force="--force" in a or bool(var), variant=var, defines=[x for x in a if x.startswith("-D")])
+    only = tuple(a[a.index("--only") + 1].split(",")) if "--only" in a else ()
+    build(force="--force" in a or bool(var), variant=var, defines=[x for x in a if x.startswith("-D")], only=only)

@@ -1098,6 +1098,7 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why) {
 
 int conv_gemm_kind(int dtype, const ConvParams& p) {
   if (dtype == DT_F32) return conv_split_eligible(p) ? PK_CONV_SPLIT : PK_CONV_GEMM;
+  if (conv_mt_eligible(dtype, p)) return PK_CONV_MT;
   return (dtype != DT_F32 && xres_mode() && xres_group(p, 32 * 4 * (4 / xres_wm(p)))) ? PK_CONV_XRES : PK_CONV_GEMM;
 }
 
@@ -1108,11 +1109,13 @@ static hipError_t conv_gemm_launch_noln(int dtype, const ConvParams& p, hipStrea
       return launch_t<float>(p, s);
     case DT_F16: {
       hipError_t e;
+      if (conv_mt_eligible(dtype, p)) return conv_mt_launch(dtype, p, s, ln_done);
       if (launch_xres<half_t>(p, s, &e, ln_done)) return e;
       return launch_t<half_t>(p, s);
     }
     case DT_BF16: {
       hipError_t e;
+      if (conv_mt_eligible(dtype, p)) return conv_mt_launch(dtype, p, s, ln_done);
       if (launch_xres<bf16_t>(p, s, &e, ln_done)) return e;
       return launch_t<bf16_t>(p, s);
     }

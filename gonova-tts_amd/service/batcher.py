@@ -1,24 +1,25 @@
-"""Cross-request dynamic batcher: the replacement for the reference's serial `_tts_worker`
+"""Cross-request continuous batcher: the replacement for the reference's serial `_tts_worker`
 (`services/tts/server.py:110-186`, strictly one request in flight, one `generate` call per
 sentence).
 
-Each round takes every queued request (up to `max_requests`, waiting at most `max_wait`
-after the first), splits them into sentences with the reference's segmentation
-(`synthesizer.py:48-99`), sorts all sentences by length and synthesizes them in engine
-batches of up to `max_sentences` (one acoustic + one vocoder pass per batch, ragged
-lengths handled on device).  Audio goes back per request in sentence order, one binary
-frame per sentence, then the final marker -- the reference's framing
-(`server.py:150-164`) -- as soon as all earlier sentences of that request are done.
-Requests that ask for sub-sentence frames (`stream_frames` > 0) run through
-`synth_stream` (`GonovaTTS.stream_batch`) in batches of their own: each vocoder chunk's
-pieces go out as soon as they reach the host, still in sentence order per request.
+Admission: requests are taken from the input queue as they arrive (whatever arrived within
+`max_wait` of the first joins it), split into sentences with the reference's segmentation
+(`synthesizer.py:48-99`), and their sentences join one shared work list -- up to
+`max_requests` requests in flight, new ones admitted while engines are busy.
 
-Several GPUs (opt-in, `synth_batches` with one callable per local engine): the per-sentence
-engine batches of a round are dealt across the engines with `dist.plan_buckets` (longest
-sentence first to the least-loaded engine, each engine's share cut into length-sorted batches of
-`max_sentences`), and the engines run at the same time, one executor thread each; frames still
-leave in per-request sentence order.  The reference can only run one server process per GPU
-behind a load balancer (`server.py:397-400,486-488`).  Streamed requests stay on the first engine.
+Engines: each engine (one per local GPU, `synth_batches`; a single engine is the reference's
+one-GPU-per-process shape, `server.py:397-400`) runs a loop of its own: whenever it is free it
+takes the next engine batch from the work list -- the pending sentence earliest in its own request
+(a new request's first sentence goes ahead of an older request's later ones; streamed requests
+first: they are the latency-sensitive ones) together with the pending sentences of the same framing
+whose lengths are closest to it, up to `max_sentences` (one acoustic + one vocoder pass per batch,
+ragged lengths handled on device) -- so no engine idles while work is queued, a fast engine never
+waits for a slow one, and a request that arrives mid-stream starts before the earlier ones end.  Audio goes back per request in sentence order, one binary frame per
+sentence, then the final marker -- the reference's framing (`server.py:150-164`) -- as soon as all
+earlier sentences of that request are done.  Requests that ask for sub-sentence frames
+(`stream_frames` > 0) run through the engine's `synth_streams` entry (`GonovaTTS.stream_batch`) in
+batches of their own, on whichever engine is free: each vocoder chunk's pieces go out as soon as
+they reach the host, still in sentence order per request.
 
 Failure: the reference logs and swallows synthesis errors, so the client never gets a
 final marker (`server.py:173-179`).  That stays the default; `notify_errors=True` sends
@@ -27,6 +28,7 @@ final marker (`server.py:173-179`).  That stays the default; `notify_errors=True
 from __future__ import annotations
 
 import asyncio
+import itertools
 import logging
 import time
 from typing import Callable, List, Optional
@@ -38,161 +40,227 @@ from ..text import split_into_sentences
 logger = logging.getLogger(__name__)
 
 
+class _Request:
+    """One admitted request: its sentences' audio pieces not yet sent, which sentences are done,
+    and how far its frames have gone out."""
+
+    def __init__(self, req, sentences):
+        self.req = req
+        self.sentences = sentences
+        self.pending: List[List[np.ndarray]] = [[] for _ in sentences]
+        self.done = [False] * len(sentences)
+        self.failed = False
+        self.cursor = 0     # the sentence whose pieces go out next
+        self.sent = 0       # frames sent: the chunk_id of the next frame / the final marker
+        self.finished = False
+
+
+class _Item:
+    __slots__ = ("state", "j", "text", "framing", "seq")
+
+    def __init__(self, state, j, text, framing, seq):
+        self.state, self.j, self.text, self.framing, self.seq = state, j, text, framing, seq
+
+
 class DynamicBatcher:
     def __init__(self, queues, synth_batch: Callable[[List[str]], List[np.ndarray]], max_sentences: int = 32,
                  max_requests: int = 64, max_wait: float = 0.004, notify_errors: bool = False,
                  send_error: Optional[Callable] = None, synth_stream: Optional[Callable] = None,
-                 sample_rate: int = 22050, synth_batches: Optional[List[Callable]] = None):
+                 sample_rate: int = 22050, synth_batches: Optional[List[Callable]] = None,
+                 synth_streams: Optional[List[Optional[Callable]]] = None):
         self.queues = queues
         self.sample_rate = float(sample_rate)  # the rate the engine's audio is in (model.sr)
         self.synth_batch = synth_batch
-        # one synth_batch per local engine (GPU); a single engine is the reference-shaped default
+        # one synth_batch (and stream_batch) per local engine (GPU)
         self.synth_batches = list(synth_batches) if synth_batches else [synth_batch]
+        self.synth_stream = synth_stream  # model.stream_batch: sub-sentence frames (opt-in per request)
+        self.synth_streams = list(synth_streams) if synth_streams else [synth_stream] * len(self.synth_batches)
         self.max_sentences = max_sentences
         self.max_requests = max_requests
         self.max_wait = max_wait
         self.notify_errors = notify_errors
         self.send_error = send_error
-        self.synth_stream = synth_stream  # model.stream_batch: sub-sentence frames (opt-in per request)
         self.running = False
+        self._work: List[_Item] = []
+        self._seq = itertools.count()
+        self._inflight = 0
+        self._cond: Optional[asyncio.Condition] = None
+        self._flush_lock: Optional[asyncio.Lock] = None
         self.stats = {"rounds": 0, "engine_batches": 0, "sentences": 0, "requests": 0, "errors": 0,
                       "audio_seconds": 0.0, "busy_seconds": 0.0, "max_batch_seen": 0,
-                      "engine_sentences": [0] * len(self.synth_batches)}
+                      "engine_sentences": [0] * len(self.synth_batches),
+                      "engine_busy_seconds": [0.0] * len(self.synth_batches)}
 
+    # ------------------------------------------------------------------ admission
     async def run(self):
+        """Admission loop plus one worker per engine, until stop() / cancellation."""
         self.running = True
+        self._cond = asyncio.Condition()
+        self._flush_lock = asyncio.Lock()
         loop = asyncio.get_running_loop()
-        while self.running:
-            try:
-                reqs = await self.queues.take_batch(self.max_requests, self.max_wait)
-            except asyncio.CancelledError:
-                break
-            if not reqs:
-                continue
-            t0 = time.perf_counter()
-            try:
-                await self._round(reqs, loop)
-            except asyncio.CancelledError:
-                raise
-            except Exception as e:  # never let the worker die (reference server.py:184-186)
-                logger.error("batcher round failed: %s", e, exc_info=True)
-            finally:
-                self.stats["busy_seconds"] += time.perf_counter() - t0
-                await self.queues.mark_request_done(len(reqs))
+        workers = [asyncio.create_task(self._engine_loop(e, loop)) for e in range(len(self.synth_batches))]
+        try:
+            while self.running:
+                # back-pressure: at most max_requests admitted and unfinished
+                async with self._cond:
+                    await self._cond.wait_for(lambda: self._inflight < self.max_requests or not self.running)
+                    room = self.max_requests - self._inflight
+                if not self.running:
+                    break
+                try:
+                    reqs = await self.queues.take_batch(room, self.max_wait)
+                except asyncio.CancelledError:
+                    break
+                if reqs:
+                    await self._admit(reqs)
+        finally:
+            self.running = False
+            for w in workers:
+                w.cancel()
+            await asyncio.gather(*workers, return_exceptions=True)
 
-    async def _round(self, reqs, loop):
+    async def _admit(self, reqs):
         self.stats["rounds"] += 1
         self.stats["requests"] += len(reqs)
-        sentences = [split_into_sentences(r.text) for r in reqs]
-        work = [(i, j, s) for i, ss in enumerate(sentences) for j, s in enumerate(ss)]
-        # per sentence: audio pieces not yet sent, and whether its last piece has arrived
-        pending: List[List[List[np.ndarray]]] = [[[] for _ in ss] for ss in sentences]
-        done = [[False] * len(ss) for ss in sentences]
-        failed = [False] * len(reqs)
-        cursor = [0] * len(reqs)  # the sentence whose pieces go out next
-        sent = [0] * len(reqs)    # frames sent: the chunk_id of the next frame / the final marker
-        finished = [False] * len(reqs)
-
-        flush_lock = asyncio.Lock()  # engines finishing together must not send a piece twice
-
-        async def flush():
-            async with flush_lock:
-                await flush_locked()
-
-        async def flush_locked():
-            for i, r in enumerate(reqs):
-                if finished[i]:
-                    continue
-                while cursor[i] < len(pending[i]):
-                    j = cursor[i]
-                    for a in pending[i][j]:
-                        await self.queues.enqueue_audio_chunk(r.connection_id, a.astype(np.float32).tobytes(), sent[i])
-                        sent[i] += 1
-                    pending[i][j].clear()
-                    if not done[i][j]:
-                        break
-                    cursor[i] += 1
-                if cursor[i] == len(pending[i]) or failed[i]:
-                    if failed[i] and not self.notify_errors:
-                        finished[i] = True  # reference behaviour: no marker after a failure
-                        continue
-                    await self.queues.enqueue_audio_chunk(r.connection_id, b"", sent[i], is_final=True)
-                    finished[i] = True
-
-        # engine batches: sentences grouped by framing (per sentence, or sub-sentence frames of
-        # one size; the streamed groups first, they are the latency-sensitive ones), each group
-        # sorted by length and cut into batches of max_sentences
-        def framing(i):
-            f = getattr(reqs[i], "stream_frames", 0) or 0
-            return f if self.synth_stream is not None else 0
-        groups = {}
-        for k, (i, _, _) in enumerate(work):
-            groups.setdefault(framing(i), []).append(k)
-        batches = []
-        for f in sorted(groups, key=lambda f: (f == 0, f)):
-            ks = sorted(groups[f], key=lambda k: len(work[k][2]))
-            if f == 0 and len(self.synth_batches) > 1:
-                continue  # dealt across the engines below
-            batches += [(f, ks[b0:b0 + self.max_sentences], 0) for b0 in range(0, len(ks), self.max_sentences)]
-
-        async def one_batch(frames, chunk, eng):
-            texts = [work[k][2] for k in chunk]
-            voices = [getattr(reqs[work[k][0]], "voice", None) for k in chunk]
-            # per-sentence voice (registered embedding) only when one is set
-            kw = {"speaker_embeddings": voices} if any(v is not None for v in voices) else {}
-            synth = self.synth_batches[eng]
+        states = []
+        for r in reqs:
             try:
-                if frames == 0:
-                    audios = await loop.run_in_executor(None, lambda: synth(texts, **kw))
-                    for k, a in zip(chunk, audios):
-                        i, j, _ = work[k]
-                        pending[i][j].append(a)
-                        done[i][j] = True
-                        self.stats["audio_seconds"] += len(a) / self.sample_rate
-                    self.stats["engine_sentences"][eng] += len(chunk)
-                else:
-                    async def deliver(pieces):
-                        for t, a, fin in pieces:
-                            i, j, _ = work[chunk[t]]
-                            if len(a):
-                                pending[i][j].append(a)
-                                self.stats["audio_seconds"] += len(a) / self.sample_rate
-                            done[i][j] = done[i][j] or fin
-                        await flush()
-                    await self._stream(loop, texts, frames, kw, deliver)
-            except Exception as e:
-                self.stats["errors"] += 1
-                logger.error("synthesis_failed: %s", e)
-                for k in chunk:
-                    i = work[k][0]
-                    if not failed[i]:
-                        failed[i] = True
-                        if self.notify_errors and self.send_error is not None:
-                            await self.send_error(reqs[i].connection_id, str(e))
-                await flush()
+                ss = split_into_sentences(r.text)
+            except Exception as e:  # never let the admission die (reference server.py:184-186)
+                logger.error("sentence split failed: %s", e)
+                ss = []
+            states.append(_Request(r, ss))
+        async with self._cond:
+            self._inflight += len(states)
+            for st in states:
+                f = self._framing(st.req)
+                for j, text in enumerate(st.sentences):
+                    self._work.append(_Item(st, j, text, f, next(self._seq)))
+            self._cond.notify_all()
+        for st in states:
+            if not st.sentences:  # empty text: only the marker
+                await self._flush(st)
+
+    def _framing(self, req) -> int:
+        f = getattr(req, "stream_frames", 0) or 0
+        return f if any(s is not None for s in self.synth_streams) else 0
+
+    def _take(self) -> List[_Item]:
+        """The next engine batch (caller holds the condition).  Its head is the pending sentence
+        that is earliest in its own request (a request's first sentence is its time to first audio;
+        later sentences only have to keep pace with playback), streamed requests first, oldest
+        first among equals; the batch is the head plus the pending sentences of its framing closest
+        to it in length, at most max_sentences, in length order."""
+        head = min(self._work, key=lambda it: (it.framing == 0, it.j, it.seq))
+        group = sorted((it for it in self._work if it.framing == head.framing), key=lambda it: (len(it.text), it.seq))
+        n = min(self.max_sentences, len(group))
+        h = group.index(head)
+        best = max(0, h - n + 1)
+        for s0 in range(max(0, h - n + 1), min(h, len(group) - n) + 1):
+            if len(group[s0 + n - 1].text) - len(group[s0].text) < \
+                    len(group[best + n - 1].text) - len(group[best].text):
+                best = s0
+        batch = group[best:best + n]
+        taken = set(id(it) for it in batch)
+        self._work = [it for it in self._work if id(it) not in taken]
+        return batch
+
+    # ------------------------------------------------------------------ engines
+    async def _engine_loop(self, eng: int, loop):
+        while True:
+            async with self._cond:
+                await self._cond.wait_for(lambda: bool(self._work))
+                batch = self._take()
+            t0 = time.perf_counter()
+            try:
+                await self._one_batch(batch, eng, loop)
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # never let a worker die (reference server.py:184-186)
+                logger.error("engine %d batch failed: %s", eng, e, exc_info=True)
+            finally:
+                dt = time.perf_counter() - t0
+                self.stats["busy_seconds"] += dt
+                self.stats["engine_busy_seconds"][eng] += dt
+
+    async def _one_batch(self, batch: List[_Item], eng: int, loop):
+        texts = [it.text for it in batch]
+        voices = [getattr(it.state.req, "voice", None) for it in batch]
+        # per-sentence voice (registered embedding) only when one is set
+        kw = {"speaker_embeddings": voices} if any(v is not None for v in voices) else {}
+        frames = batch[0].framing
+        try:
+            if frames == 0:
+                synth = self.synth_batches[eng]
+                audios = await loop.run_in_executor(None, lambda: synth(texts, **kw))
+                for it, a in zip(batch, audios):
+                    it.state.pending[it.j].append(a)
+                    it.state.done[it.j] = True
+                    self.stats["audio_seconds"] += len(a) / self.sample_rate
+            else:
+                async def deliver(pieces):
+                    touched = {}
+                    for t, a, fin in pieces:
+                        it = batch[t]
+                        if len(a):
+                            it.state.pending[it.j].append(a)
+                            self.stats["audio_seconds"] += len(a) / self.sample_rate
+                        it.state.done[it.j] = it.state.done[it.j] or fin
+                        touched[id(it.state)] = it.state
+                    for st in touched.values():
+                        await self._flush(st)
+                await self._stream(loop, texts, frames, kw, deliver, eng)
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:
+            self.stats["errors"] += 1
+            logger.error("synthesis_failed: %s", e)
+            for it in batch:
+                st = it.state
+                if not st.failed:
+                    st.failed = True
+                    if self.notify_errors and self.send_error is not None:
+                        await self.send_error(st.req.connection_id, str(e))
+            for st in {id(it.state): it.state for it in batch}.values():
+                await self._flush(st)
+            return
+        self.stats["engine_batches"] += 1
+        self.stats["sentences"] += len(batch)
+        self.stats["engine_sentences"][eng] += len(batch)
+        self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(batch))
+        for st in {id(it.state): it.state for it in batch}.values():
+            await self._flush(st)
+
+    async def _flush(self, st: _Request):
+        """Send what request `st` can send in sentence order; its final marker once every sentence
+        is done (or, after a failure, per notify_errors); a finished request frees its slot."""
+        async with self._flush_lock:
+            if st.finished:
                 return
-            self.stats["engine_batches"] += 1
-            self.stats["sentences"] += len(chunk)
-            self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(chunk))
-            await flush()
+            r = st.req
+            while st.cursor < len(st.pending):
+                j = st.cursor
+                for a in st.pending[j]:
+                    await self.queues.enqueue_audio_chunk(r.connection_id, a.astype(np.float32).tobytes(), st.sent)
+                    st.sent += 1
+                st.pending[j].clear()
+                if not st.done[j]:
+                    break
+                st.cursor += 1
+            if st.cursor == len(st.pending) or st.failed:
+                if st.failed:
+                    # drop its queued sentences: nothing more goes to this client
+                    async with self._cond:
+                        self._work = [it for it in self._work if it.state is not st]
+                if not (st.failed and not self.notify_errors):  # reference behaviour: no marker after a failure
+                    await self.queues.enqueue_audio_chunk(r.connection_id, b"", st.sent, is_final=True)
+                st.finished = True
+                await self.queues.mark_request_done(1)
+                async with self._cond:
+                    self._inflight -= 1
+                    self._cond.notify_all()
 
-        for frames, chunk, eng in batches:
-            await one_batch(frames, chunk, eng)
-        if len(self.synth_batches) > 1 and 0 in groups:
-            # per-sentence batches across the engines: longest-first to the least-loaded engine
-            # (load = characters), each engine's share in length-sorted batches, engines concurrent
-            from ..dist import plan_buckets
-            ks = groups[0]
-            plan = plan_buckets([len(work[k][2]) for k in ks], len(self.synth_batches), self.max_sentences)
-
-            async def engine_run(eng, buckets):
-                for bk in buckets:
-                    await one_batch(0, [ks[u] for u in bk], eng)
-
-            await asyncio.gather(*(engine_run(e, bks) for e, bks in enumerate(plan) if bks))
-        await flush()
-
-    async def _stream(self, loop, texts, frames, kw, deliver):
+    async def _stream(self, loop, texts, frames, kw, deliver, eng: int = 0):
         """Run `synth_stream` (a generator of per-chunk pieces) on an executor thread and hand
         each chunk to `deliver` on the event loop as soon as it is on the host, so the first
         frames go out while the vocoder still works on the rest of the batch.
@@ -206,8 +274,10 @@ class DynamicBatcher:
         end = object()
         stop = threading.Event()
 
+        synth_stream = self.synth_streams[eng] if eng < len(self.synth_streams) else self.synth_stream
+
         def produce():
-            gen = self.synth_stream(texts, frames, **kw)
+            gen = synth_stream(texts, frames, **kw)
             try:
                 for item in gen:
                     if stop.is_set():
@@ -236,3 +306,11 @@ class DynamicBatcher:
 
     def stop(self):
         self.running = False
+        if self._cond is not None:
+            async def wake():
+                async with self._cond:
+                    self._cond.notify_all()
+            try:
+                asyncio.get_running_loop().create_task(wake())
+            except RuntimeError:
+                pass

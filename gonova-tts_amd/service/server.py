@@ -73,8 +73,8 @@ class TTSService:
                  device: str = "cuda", device_index: int = 0, stream_frames: int = 0,
                  min_stream_frames: int = MIN_STREAM_FRAMES, devices: Optional[list] = None):
         """devices: opt-in fan-out over the node's GPUs, e.g. ["cuda:0", "cuda:1"]: model_factory is
-        then called once per device (model_factory(device)) and the batcher deals each round's
-        sentences across the engines (batcher.py); default None = one model_factory() model, the
+        then called once per device (model_factory(device)) and each engine pulls its next batch from
+        the batcher's shared work list whenever it is free (batcher.py); default None = one model_factory() model, the
         reference's one-GPU-per-process shape (server.py:397-400)."""
         self.model_factory = model_factory
         self.devices = list(devices) if devices else None
@@ -119,7 +119,8 @@ class TTSService:
                                       max_wait=self.max_wait, notify_errors=self.notify_errors,
                                       send_error=self._send_error,
                                       synth_stream=getattr(self.model, "stream_batch", None), sample_rate=sr,
-                                      synth_batches=[m.generate_batch for m in self.models])
+                                      synth_batches=[m.generate_batch for m in self.models],
+                                      synth_streams=[getattr(m, "stream_batch", None) for m in self.models])
         self._task = asyncio.create_task(self.batcher.run())
         self.is_loaded = True
 

@@ -367,10 +367,9 @@ class FakeDeviceModel(FakeModel):
 
 def test_multi_device_fan_out_keeps_order_and_balances():
     """Opt-in fan-out over the node's GPUs (TTSService(devices=[...])):
-    the factory makes one engine per device, one batcher round deals its sentences across both
-    engines (dist.plan_buckets: longest first to the least-loaded engine), the engines work at
-    the same time, and every request still gets its frames in sentence order followed by the
-    marker -- the same frames a single engine produces."""
+    the factory makes one engine per device, both engines pull batches from the batcher's shared
+    work list at the same time, and every request still gets its frames in sentence order followed
+    by the marker -- the same frames a single engine produces."""
     made = []
 
     def factory(device):
@@ -407,3 +406,85 @@ def test_multi_device_fan_out_keeps_order_and_balances():
     assert all(w > 0 for w in work), work
     assert abs(work[0] - work[1]) <= max(len(t) for t in texts.values()), work
     assert sum(stats["engine_sentences"]) == 20 and min(stats["engine_sentences"]) > 0
+
+
+class TimedModel(FakeModel):
+    """A fake engine that records when each of its batches ran."""
+
+    def __init__(self, device="cuda:0", delay=0.0):
+        super().__init__(delay=delay)
+        self.device = device
+        self.spans = []
+
+    def generate_batch(self, texts):
+        t0 = time.monotonic()
+        out = super().generate_batch(texts)
+        self.spans.append((t0, time.monotonic(), len(texts)))
+        return out
+
+
+def test_continuous_batcher_keeps_unequal_engines_busy():
+    """Continuous batching across engines of unequal speed: each engine pulls
+    its next batch from the shared work list as soon as it is free, so the fast engine is never
+    held for the slow one (no gap between its batches while work is queued) and does most of the
+    work; every request still gets its frames in sentence order, then the marker."""
+    made = {}
+
+    def factory(device):
+        made[device] = TimedModel(device, delay=0.02 if device == "cuda:0" else 0.2)
+        return made[device]
+
+    app = create_app(factory, devices=["cuda:0", "cuda:1"], max_wait=0.05, max_sentences=2)
+    texts = {i: " ".join(f"Sentence {i} number {j} {'y' * (2 * j + i)}." for j in range(6)) for i in range(4)}
+    results = {}
+    with TestClient(app) as c:
+        for m in made.values():
+            m.spans.clear()  # (warmups)
+
+        def client(i):
+            with c.websocket_connect("/v1/stream/tts") as ws:
+                ws.send_text(json.dumps({"type": "synthesize", "text": texts[i]}))
+                results[i] = recv_until_complete(ws)
+        ts = [threading.Thread(target=client, args=(i,)) for i in texts]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=60)
+    from gonova_tts_amd.text import split_into_sentences
+    for i, (frames, final) in results.items():
+        sents = split_into_sentences(texts[i])
+        assert final == {"type": "synthesis_complete", "chunk_id": len(sents)}
+        assert [len(f) for f in frames] == [100 * len(s) for s in sents]
+    fast, slow = made["cuda:0"], made["cuda:1"]
+    n_fast, n_slow = sum(n for *_, n in fast.spans), sum(n for *_, n in slow.spans)
+    assert n_fast + n_slow == 24 and n_fast >= 3 * n_slow > 0, (n_fast, n_slow)
+    # the fast engine's batches follow each other back to back until the list runs dry (a round-
+    # based batcher would park it until the slow engine's batch of the round ends)
+    gaps = [b[0] - a[1] for a, b in zip(fast.spans, fast.spans[1:])]
+    assert max(gaps) < 0.1, gaps
+
+
+def test_request_arriving_mid_stream_starts_before_the_earlier_one_ends():
+    """Admission between engine batches: a request sent while an earlier, long request is being
+    synthesized gets its sentence into the next engine batch (its first sentence goes ahead of the
+    earlier request's later ones) and completes before the earlier request does."""
+    model = TimedModel(delay=0.05)
+    app = create_app(lambda: model, max_wait=0.01, max_sentences=1)
+    long_text = " ".join(f"Long request sentence number {j}." for j in range(8))
+    order = []
+    with TestClient(app) as c:
+        with c.websocket_connect("/v1/stream/tts") as wa, c.websocket_connect("/v1/stream/tts") as wb:
+            wa.send_text(json.dumps({"type": "synthesize", "text": long_text}))
+            first = wa.receive()  # A's first sentence is out: A is mid-stream
+            assert first.get("bytes") is not None
+            wb.send_text(json.dumps({"type": "synthesize", "text": "Short one."}))
+            frames_b, final_b = recv_until_complete(wb)
+            order.append("b")
+            frames_a, final_a = recv_until_complete(wa)
+            order.append("a")
+    assert final_b == {"type": "synthesis_complete", "chunk_id": 1} and len(frames_b) == 1
+    assert final_a == {"type": "synthesis_complete", "chunk_id": 8} and len(frames_a) == 7
+    # B finished while A still had sentences to go: B's batch ran before A's last ones
+    b_batch = next(k for k, b in enumerate(model.batches) if b == ["Short one."])
+    a_last = max(k for k, b in enumerate(model.batches) if b[0].startswith("Long request sentence number 7"))
+    assert b_batch < a_last

@@ -127,3 +127,54 @@ def test_stream_frames_concatenate_to_generate(served):
     got, want = np.concatenate(frames), np.concatenate(direct)
     assert got.shape == want.shape
     np.testing.assert_allclose(got, want, atol=1e-5, rtol=1e-4)
+
+
+def test_two_engines_continuous_batcher_real_engine():
+    """TTSService(devices=["cuda:0", "cuda:0"]): two real GonovaTTS engines (their own workspaces
+    and executor threads) pull engine batches from the continuous batcher's shared work list at the
+    same time.  Three concurrent clients -- one of them streamed (stream_frames,
+    dealt across the engines like the others) -- get every frame in sentence order, equal to
+    generate() of each sentence (fp32 engines, the per-sentence tolerance), and both engines ran
+    batches."""
+    made = []
+
+    def factory(device):
+        made.append(GonovaTTS.from_pretrained(device, vocoder_dtype="f32", acoustic_dtype="f32"))
+        return made[-1]
+
+    app = create_app(factory, devices=["cuda:0", "cuda:0"], max_wait=0.2, max_sentences=2)
+    texts = {0: "Good morning. The quick brown fox jumps. Over the lazy dog!",
+             1: "A second client speaks. Then it stops! And starts again.",
+             2: "Streaming here. In small pieces please."}
+    results = {}
+    with TestClient(app) as c:
+        def client(i):
+            msg = {"type": "synthesize", "text": texts[i]}
+            if i == 2:
+                msg["stream_frames"] = 32
+            with c.websocket_connect("/v1/stream/tts") as ws:
+                ws.send_text(json.dumps(msg))
+                results[i] = recv_until_complete(ws)
+        ts = [threading.Thread(target=client, args=(i,)) for i in texts]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=180)
+        stats = dict(app.state.service.batcher.stats)
+        # (the service closes its engines at shutdown: the reference runs inside the client block)
+        direct_all = {i: [made[0].generate(s).squeeze().cpu().numpy() for s in split_into_sentences(texts[i])]
+                      for i in texts}
+    assert len(results) == 3
+    for i, (frames, final) in results.items():
+        direct = direct_all[i]
+        assert final == {"type": "synthesis_complete", "chunk_id": len(frames)}
+        if i == 2:
+            assert len(frames) == sum(-(-len(d) // 8192) for d in direct)
+            got, want = np.concatenate(frames), np.concatenate(direct)
+        else:
+            assert len(frames) == len(direct)
+            got, want = frames, direct
+        for g, w in zip(got if i != 2 else [got], want if i != 2 else [want]):
+            assert g.shape == w.shape
+            np.testing.assert_allclose(g, w, atol=1e-5, rtol=1e-4)
+    assert min(stats["engine_sentences"]) > 0, stats["engine_sentences"]

@@ -174,35 +174,45 @@ def cpu_baseline(b2: int, b3: int):
     g = torch.Generator().manual_seed(0)
     mel = torch.randn((b2, 862, 80), generator=g)
     voc(mel[:1, :16])  # warm up the thread pool
-    t = time.perf_counter()
-    wav = voc(mel)
-    dt2 = time.perf_counter() - t
     ac = TorchAcoustic(make_acoustic_weights(seed=0, fixed_duration=6))
     ids = torch.randint(1, 78, (b3, 144), generator=g)
     dur = torch.full((b3, 144), 6, dtype=torch.int64)
-    t = time.perf_counter()
-    m, _ = ac(ids, dur)
-    w3 = voc(m)
-    dt3 = time.perf_counter() - t
     # C1: one N = 71 sentence, tokens -> waveform
     from gonova_tts_amd.text import tokenize
     ids1 = torch.from_numpy(np.asarray(tokenize(C1_TEXT), np.int64))[None]
     assert ids1.shape[1] == 71
-    t = time.perf_counter()
-    m1, _ = ac(ids1, torch.full((1, 71), 6, dtype=torch.int64))
-    w1 = voc(m1)
-    dt1 = time.perf_counter() - t
+    # each sample timed REPS times: the rate reported is the median, with the spread beside it
+    # (host load on a shared box moves a single timing by 10-20 %)
+    reps = max(1, int(os.environ.get("TTS_CPU_REPS", "3")))
+    t2, t3, t1 = [], [], []
+    for _ in range(reps):
+        t = time.perf_counter()
+        wav = voc(mel)
+        t2.append(time.perf_counter() - t)
+        t = time.perf_counter()
+        m, _ = ac(ids, dur)
+        w3 = voc(m)
+        t3.append(time.perf_counter() - t)
+        t = time.perf_counter()
+        m1, _ = ac(ids1, torch.full((1, 71), 6, dtype=torch.int64))
+        w1 = voc(m1)
+        t1.append(time.perf_counter() - t)
+    med = lambda v: float(np.median(v))  # noqa: E731
+
+    def spread(n, ts):
+        return {"min": round(n / max(ts), 1), "max": round(n / min(ts), 1), "runs": len(ts)}
+    dt2, dt3, dt1 = med(t2), med(t3), med(t1)
     return {"value": round(wav.numel() / dt2, 1), "unit": "samples/s", "cores": threads, "kind": "port",
-            "cpu_model": _cpu_model(),
-            "sample": f"C2: {b2} utterances x 862 frames ({wav.numel() / SR:.1f} s audio) in {dt2:.1f} s; "
-                      f"torch-CPU fp32 restatement (oracle/torch_cpu.py), {threads} threads",
-            "c3": {"value": round(w3.numel() / dt3, 1), "unit": "samples/s",
-                   "sample": f"C3: {b3} utterances x 144 tokens x 6 frames ({w3.numel() / SR:.1f} s audio) in "
-                             f"{dt3:.1f} s (acoustic + vocoder)"},
+            "cpu_model": _cpu_model(), "statistic": f"median of {reps}", "spread": spread(wav.numel(), t2),
+            "sample": f"C2: {b2} utterances x 862 frames ({wav.numel() / SR:.1f} s audio), median {dt2:.1f} s of "
+                      f"{reps} runs; torch-CPU fp32 restatement (oracle/torch_cpu.py), {threads} threads",
+            "c3": {"value": round(w3.numel() / dt3, 1), "unit": "samples/s", "spread": spread(w3.numel(), t3),
+                   "sample": f"C3: {b3} utterances x 144 tokens x 6 frames ({w3.numel() / SR:.1f} s audio), median "
+                             f"{dt3:.1f} s of {reps} runs (acoustic + vocoder)"},
             "c1": {"value": round(w1.numel() / dt1, 1), "unit": "samples/s", "latency_ms": round(dt1 * 1e3, 1),
-                   "rtf": round(dt1 / (w1.numel() / SR), 4),
-                   "sample": f"C1: 1 utterance x 71 tokens x 6 frames ({w1.numel() / SR:.2f} s audio) in {dt1:.2f} s "
-                             f"(acoustic + vocoder, fp32)"}}
+                   "rtf": round(dt1 / (w1.numel() / SR), 4), "spread": spread(w1.numel(), t1),
+                   "sample": f"C1: 1 utterance x 71 tokens x 6 frames ({w1.numel() / SR:.2f} s audio), median "
+                             f"{dt1:.2f} s of {reps} runs (acoustic + vocoder, fp32)"}}
 
 
 class Ctx:

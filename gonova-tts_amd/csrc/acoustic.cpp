@@ -419,17 +419,18 @@ struct AcousticModel::Impl {
       run(L.qkv, Xb, Tp, lens, QKV, Tp, B, dt, s, prof);
       const bool fused_attn = rel_attn_enabled() && rel_attn_supported(dt, D, H);
       if (!fused_attn) elem(s, [&] { return launch_pos_bias(dt, QKV, rows, D, L.pos_u, L.pos_v, Qu, Qv, s); });
-      elem(s, [&] { return launch_transpose_v(dt, QKV, lens, B, Tp, D, H, Sk, Vt, s); });
       if (fused_attn) {
-        // fused flash-style relative-position attention (attention.hip); Qu / Qv formed in it
+        // fused flash-style relative-position attention (attention.hip); Qu / Qv formed in it,
+        // V read from the QKV rows (transposed in LDS: no Vt launch)
         // fp32 layers of a 16-bit model (the exact-duration encoder) in split precision, like their GEMMs
         const bool split = dt == DT_F32 && this->dt != DT_F32 && sw(SW_ATTN_SPLIT) != 0 && !enc_f32;
-        prof_launch(PK_ATTN, 6.0 * D * (double)B * Tm * Tm, s, [&] { return launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, Vt, L.ptab, lens, B, Tm, Tp, D, H, Sk, rmax, scale,
+        prof_launch(PK_ATTN, 6.0 * D * (double)B * Tm * Tm, s, [&] { return launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, L.ptab, lens, B, Tm, Tp, D, H, rmax, scale,
                                   O, s, range_flag); });
         run_ln(L.out, O, Tp, lens, Y, Tp, B, dt, s, 1.f, Xb, Xb, L.ln_att, nullptr);
         conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
         continue;
       }
+      elem(s, [&] { return launch_transpose_v(dt, QKV, lens, B, Tp, D, H, Sk, Vt, s); });
       const size_t e = dtype_size(dt);
       // AC[b,h][i][j] = Qu[b][i][h] . K[b][j][h]
       attn_gemm(dt, Qu, (long long)Tp * D, dk, D, lens, Tm, (const char*)QKV + (size_t)D * e, (long long)Tp * 3 * D, dk,

@@ -15,9 +15,22 @@
 // softmax statistics, P and O share one lane <-> query map (query = lane & 15):
 //   S^T = K . Qu^T     A = K rows (LDS),       B = Qu^T (registers, whole dk)
 //   G^T = R . Qv^T     A = R window (LDS),     B = Qv^T (registers)
-//   O^T += Vt . P^T    A = Vt rows (LDS),      B = P^T: the lane's own 8 probabilities
+//   O^T += Vt . P^T    A = Vt (LDS, V rows read transposed), B = P^T: the lane's own 8 probabilities
 // P^T's k index is permuted (keys 4g..4g+3, 16+4g..16+4g+3 for lane group g) and the Vt
 // fragment is read with the same permutation, so no cross-lane move is needed.
+//
+// V is staged as it lies in QKV, [32 keys][dk] rows like K, and the A fragment of O^T is taken
+// with two ds_read_b64_tr_b16 per 16-row tile: lane group g reads the 4 x 16 block (keys 4g..4g+3
+// or 16+4g..16+4g+3, channels 16t..16t+15) and lane q receives channel 16t + q of those 4 keys --
+// exactly the Vt row piece the lane needs.  (Round 4 wrote Vt with a transpose launch per layer.)
+// LDS images (MI355X_MICROARCH.md §LDS bank model), all conflict-free:
+//   * K / V / R rows at a stride of dk*2 + 32 bytes (dk/8 + 2 16-byte slots, = 2 mod 4): the
+//     ds_read_b128 fragment reads (16 rows x 2 lane groups per 16-lane bank group) take 16
+//     distinct slots; the odd-slot stride of round 4 (dk*2 + 16) was 2-way there;
+//   * the transposed V reads: 8 keys x 4 column pieces per 32-lane half on 64 distinct banks;
+//   * the per-wave G scratch (48 slots x 16 queries, f32): slot s is stored at row
+//     s ^ ((s >> 2) & 1), so the two lane groups of a 32-lane half (slots 4 apart) land in
+//     opposite bank halves for the writes and for the diagonal gather.
 //
 // Three forms share that schedule: rel_attn_kernel (16-bit stacks: the decoder, and the whole
 // model with encoder_precision "fast"), rel_attn_split_kernel (fp32 stacks of a 16-bit model:
@@ -55,6 +68,22 @@ __device__ inline float at_xor32_sum(float x) {
 // 2^x on v_exp_f32 (arguments <= 0 here; -inf -> 0), without exp2f's denormal-range fixup
 __device__ inline float at_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// K / V / R row stride in LDS (bytes): dk/8 + 2 16-byte slots for 16-bit rows (see the header),
+// dk + 4 dwords for fp32 rows (the f32 kernel's scalar V reads: lane groups 16 dwords apart)
+template <typename T>
+constexpr int at_kr(int dk) { return sizeof(T) == 2 ? dk * 2 + 32 : dk * 4 + 16; }
+// G scratch row of slot s (see the header)
+__device__ inline int at_gslot(int s) { return s ^ ((s >> 2) & 1); }
+// byte offset, within the V rows, of lane (g, q)'s transposed read of tile 0's keys 4g .. 4g + 3:
+// lane 4a + c of the 16-lane group supplies key 4g + a, channels 4c .. 4c + 3
+__device__ inline int at_tr_addr(int kr, int g, int q) { return (4 * g + (q >> 2)) * kr + (q & 3) * 8; }
+// ds_read_b64_tr_b16 (all 64 lanes active: the loop has no divergence)
+__device__ inline uint2 at_tr16(const char* p) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)const_cast<char*>(p));
+  return __builtin_bit_cast(uint2, v);
+}
+
 constexpr int AT_BQ = 64;   // queries per block
 constexpr int AT_BK = 32;   // keys per step
 constexpr int AT_RW = AT_BQ + AT_BK;  // R window rows per block (95 used)
@@ -65,22 +94,21 @@ constexpr int AT_RW = AT_BQ + AT_BK;  // R window rows per block (95 used)
 // on the utterance's length, so a row's result does not depend on the batch.
 template <typename T, int DK, int KH>
 __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(const float* __restrict__ pu, const float* __restrict__ pv,
-                                                         const T* __restrict__ qkv, const T* __restrict__ vt,
+                                                         const T* __restrict__ qkv,
                                                          const T* __restrict__ ptab, const int* __restrict__ lens,
-                                                         int Tp, int D, int H, int Sk, int rmax, float scale,
+                                                         int Tp, int D, int H, int rmax, float scale,
                                                          T* __restrict__ out, int nqb, int nbatch) {
   using MF = Mfma16<T>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int KS = DK / 32;         // k-steps over dk
   constexpr int DT = DK / 16;         // 16-row tiles of dk (O^T)
-  constexpr int KR = DK * 2 + 16;     // K / R row stride in LDS (bytes; odd 16-byte slots)
-  constexpr int VR = AT_BK * 2 + 16;  // Vt row stride (80 B)
-  constexpr int HALF = AT_BK * KR + DK * VR + AT_RW * KR;  // one key group's staging bytes
+  constexpr int KR = at_kr<T>(DK);    // K / V / R row stride in LDS (bytes)
+  constexpr int HALF = 2 * AT_BK * KR + AT_RW * KR;  // one key group's staging bytes
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int kh = KH > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) : 0;  // key group
   char* Ks = smem + kh * HALF;                      // [32 keys][DK]
-  char* Vs = Ks + AT_BK * KR;                       // [DK][32 keys]
-  char* Rs = Vs + DK * VR;                          // [96 slots][DK]
+  char* Vs = Ks + AT_BK * KR;                       // [32 keys][DK]
+  char* Rs = Vs + AT_BK * KR;                       // [96 slots][DK]
   float* Gs = reinterpret_cast<float*>(smem + KH * HALF);  // [KH][4 waves][48 slots][16 q]
 
   // 1-D grid, XCD-grouped: the query blocks of one (utterance, head) -- which all stream the
@@ -134,41 +162,37 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
   // at the end of the (utterance, head) Vt block, and at the position table's last row; each
   // thread's byte offsets, LDS destinations and ring slots are fixed or stepped by one unsigned
   // min, so the staging costs no index arithmetic per step (it was ~40 % of the loop's VALU).
-  constexpr int KP = AT_BK * (DK / 8) / 256;   // 16-byte pieces per thread: K, Vt, new R rows
-  static_assert(AT_BK * (DK / 8) % 256 == 0 && DK * (AT_BK / 8) % 256 == 0, "staging split");
+  constexpr int KP = AT_BK * (DK / 8) / 256;   // 16-byte pieces per thread: K, V, new R rows
+  static_assert(AT_BK * (DK / 8) % 256 == 0, "staging split");
   constexpr unsigned RING = AT_RW * KR;        // R ring bytes
   auto rslot = [](int m) { const int r = m % AT_RW; return r < 0 ? r + AT_RW : r; };
   auto rrow = [&](int m) { return min(max(rmax - 1 - m, 0), 2 * rmax - 1); };
   // next ring slot, 32 rows back (mod 96), of a byte address slot * KR + col (col < KR)
   auto ring_back = [](unsigned a) { return min(a - AT_BK * KR, a + (AT_RW - AT_BK) * KR); };
   const int rowB = 3 * D * (int)sizeof(T);     // QKV row bytes
-  int kofs[KP], vofs[KP], rofs[KP];
-  unsigned kdst[KP], vdst[KP], rdst[KP];
+  int kofs[KP], rofs[KP];
+  unsigned kdst[KP], rdst[KP];
 #pragma unroll
   for (int i = 0; i < KP; ++i) {
     const int p = tid + 256 * i;
     const int r = p / (DK / 8), c = p - r * (DK / 8);
-    kofs[i] = r * rowB + c * 16;
+    kofs[i] = r * rowB + c * 16;  // K and V rows: the same pieces of the row's two slices
     kdst[i] = r * KR + c * 16;
     // position-table row row0 + r <-> m = i0 - j0 - r; the first prefetch is for j0 = kbeg + 32
     rofs[i] = r * D * (int)sizeof(T) + c * 16;
     rdst[i] = rslot(i0 - kbeg - AT_BK - r) * KR + c * 16;
-    const int d = p / (AT_BK / 8), cv = p - d * (AT_BK / 8);
-    vofs[i] = d * Sk * (int)sizeof(T) + cv * 16;
-    vdst[i] = d * VR + cv * 16;
   }
   u32x4 pkv[KP], pvt[KP], prr[KP];
   auto load_kv = [&](int j0) __attribute__((always_inline)) {
-    // Vt is zero past len (transpose_v); columns past Sk read the next row's (finite) values or,
-    // past the block, 0 -- those keys are masked out of the softmax
-    const auto kr = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(qkv + ((long long)b * Tp + j0) * 3 * rowD + D + h * DK),
-                                                      0, max(len - j0, 0) * rowB, 0x00020000);
-    const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(vt + ((long long)b * H + h) * DK * Sk + j0), 0,
-                                                      max(DK * Sk - j0, 0) * (int)sizeof(T), 0x00020000);
+    // K and V rows >= len read 0 (the descriptors' range ends at the utterance's last key):
+    // those keys are masked out of the softmax, and V = 0 keeps 0 * V finite
+    const T* krow = qkv + ((long long)b * Tp + j0) * 3 * rowD + D + h * DK;
+    const auto kr = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(krow), 0, max(len - j0, 0) * rowB, 0x00020000);
+    const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(krow + D), 0, max(len - j0, 0) * rowB, 0x00020000);
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
       pkv[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(kr, kofs[i], 0, 0));
-      pvt[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vr, vofs[i], 0, 0));
+      pvt[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vr, kofs[i], 0, 0));
     }
   };
   auto load_r = [&](int j0) __attribute__((always_inline)) {
@@ -185,7 +209,7 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
       *reinterpret_cast<u32x4*>(Ks + kdst[i]) = pkv[i];
-      *reinterpret_cast<u32x4*>(Vs + vdst[i]) = pvt[i];
+      *reinterpret_cast<u32x4*>(Vs + kdst[i]) = pvt[i];
     }
   };
   auto write_r = [&]() __attribute__((always_inline)) {
@@ -207,6 +231,7 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
   __syncthreads();
   // this lane's R fragment rows: slot of m = i0w - j0 - 31 + q (+ 16 t per tile), plus its column
   unsigned ra = rslot(i0w - kbeg - (AT_BK - 1) + q) * KR + 16 * g;
+  const int vta = at_tr_addr(KR, g, q);  // this lane's transposed-read address in the V rows (tile 0)
 
   for (int j0 = kbeg; j0 < kbeg + khalf; j0 += AT_BK) {
     load_kv(j0 + AT_BK);  // in flight during this step's MFMAs (the last step's are written, unused)
@@ -239,7 +264,7 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) gw[(16 * t + 4 * g + e) * 16 + q] = gacc[t][e];
+      for (int e = 0; e < 4; ++e) gw[at_gslot(16 * t + 4 * g + e) * 16 + q] = gacc[t][e];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's scratch writes landed
     __builtin_amdgcn_wave_barrier();
     float sv[8];
@@ -248,7 +273,7 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int kk = 16 * kt + 4 * g + e;
-        const float bd = gw[(q - kk + AT_BK - 1) * 16 + q];
+        const float bd = gw[at_gslot(q - kk + AT_BK - 1) * 16 + q];
         sv[4 * kt + e] = (sacc[kt][e] + bd) * sl2;
       }
     __builtin_amdgcn_wave_barrier();
@@ -284,12 +309,11 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
     l_run = l_run * alpha + lsum;
     m_run = m_new;
     const Frag bp = __builtin_bit_cast(Frag, pack8<T>(pe0, pe1));
-    // O^T += Vt . P^T with the permuted key order of bp
+    // O^T += Vt . P^T with the permuted key order of bp: the Vt fragment by transposed reads
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
-      const char* vr = Vs + (16 * t + q) * VR + 8 * g;
-      const uint2 lo = *reinterpret_cast<const uint2*>(vr);
-      const uint2 hi = *reinterpret_cast<const uint2*>(vr + 32);
+      const uint2 lo = at_tr16(Vs + vta + t * 32);
+      const uint2 hi = at_tr16(Vs + vta + 16 * KR + t * 32);
       const uint4 av = uint4{lo.x, lo.y, hi.x, hi.y};
       oacc[t] = MF::mma(*reinterpret_cast<const Frag*>(&av), bp, oacc[t] * alpha);
     }
@@ -345,17 +369,16 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
 // K / Vt / R (140 KB): one block per CU.
 template <int DK>
 __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __restrict__ pu, const float* __restrict__ pv,
-                                                             const float* __restrict__ qkv, const float* __restrict__ vt,
+                                                             const float* __restrict__ qkv,
                                                              const float* __restrict__ ptab, const int* __restrict__ lens,
-                                                             int Tp, int D, int H, int Sk, int rmax, float scale,
+                                                             int Tp, int D, int H, int rmax, float scale,
                                                              float* __restrict__ out, int nqb, int nbatch) {
   constexpr int KU = DK / 16;         // 16-wide dk chunks (4 k-steps each); also O^T tiles
-  constexpr int KR = DK * 4 + 16;     // K / R row stride in LDS (bytes; odd 16-byte slots)
-  constexpr int VR = AT_BK * 4 + 16;  // Vt row stride (144 B)
+  constexpr int KR = at_kr<float>(DK);  // K / V / R row stride in LDS (bytes; odd 16-byte slots)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;                                  // [32 keys][DK]
-  char* Vs = Ks + AT_BK * KR;                       // [DK][32 keys]
-  char* Rs = Vs + DK * VR;                          // [96 slots][DK]
+  char* Vs = Ks + AT_BK * KR;                       // [32 keys][DK]
+  char* Rs = Vs + AT_BK * KR;                       // [96 slots][DK]
   float* Gs = reinterpret_cast<float*>(Rs + AT_RW * KR);  // [4 waves][48 slots][16 q]
 
   int bh, qb;
@@ -388,8 +411,8 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
 
   // staging as the 16-bit kernel: loads for step s+1 in flight during step s, written after
   // the barrier that ends it (every step), masks applied at the write
-  constexpr int KP = AT_BK * (DK / 4) / 256;  // 16-byte pieces per thread: K, Vt, new R rows
-  static_assert(AT_BK * (DK / 4) % 256 == 0 && DK * (AT_BK / 4) % 256 == 0, "staging split");
+  constexpr int KP = AT_BK * (DK / 4) / 256;  // 16-byte pieces per thread: K, V, new R rows
+  static_assert(AT_BK * (DK / 4) % 256 == 0, "staging split");
   auto rslot = [](int m) { const int r = m % AT_RW; return r < 0 ? r + AT_RW : r; };
   auto rrow = [&](int m) { return min(max(rmax - 1 - m, 0), 2 * rmax - 1); };
   f32x4 pkv[KP], pvt[KP], prr[KP];
@@ -398,9 +421,9 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
     for (int i = 0; i < KP; ++i) {
       const int p = tid + 256 * i;
       const int r = p / (DK / 4), c = p - r * (DK / 4);
-      pkv[i] = *reinterpret_cast<const f32x4*>(qkv + ((long long)b * Tp + min(j0 + r, Tp - 1)) * 3 * rowD + D + h * DK + c * 4);
-      const int d = p / (AT_BK / 4), cv = p - d * (AT_BK / 4);
-      pvt[i] = *reinterpret_cast<const f32x4*>(vt + (((long long)b * H + h) * DK + d) * Sk + min(j0 + cv * 4, Sk - 4));
+      const float* kv = qkv + ((long long)b * Tp + min(j0 + r, Tp - 1)) * 3 * rowD + D + h * DK + c * 4;
+      pkv[i] = *reinterpret_cast<const f32x4*>(kv);
+      pvt[i] = *reinterpret_cast<const f32x4*>(kv + D);
     }
   };
   auto load_r = [&](int j0) __attribute__((always_inline)) {
@@ -417,8 +440,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
       const int p = tid + 256 * i;
       const int r = p / (DK / 4), c = p - r * (DK / 4);
       *reinterpret_cast<f32x4*>(Ks + r * KR + c * 16) = j0 + r < len ? pkv[i] : f32x4{};
-      const int d = p / (AT_BK / 4), cv = p - d * (AT_BK / 4);
-      *reinterpret_cast<f32x4*>(Vs + d * VR + cv * 16) = j0 + cv * 4 < Sk ? pvt[i] : f32x4{};
+      *reinterpret_cast<f32x4*>(Vs + r * KR + c * 16) = j0 + r < len ? pvt[i] : f32x4{};  // 0 * V finite
     }
   };
   auto write_r = [&](int j0) __attribute__((always_inline)) {
@@ -467,7 +489,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) gw[(16 * t + 4 * g + e) * 16 + q] = gacc[t][e];
+      for (int e = 0; e < 4; ++e) gw[at_gslot(16 * t + 4 * g + e) * 16 + q] = gacc[t][e];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's scratch writes landed
     __builtin_amdgcn_wave_barrier();
     float sv[8];
@@ -477,7 +499,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int kk = 16 * kt + 4 * g + e;
-        const float bd = gw[(q - kk + AT_BK - 1) * 16 + q];
+        const float bd = gw[at_gslot(q - kk + AT_BK - 1) * 16 + q];
         float sc = (sacc[kt][e] + bd) * sl2;
         if (j0 + kk >= len) sc = -INFINITY;
         sv[4 * kt + e] = sc;
@@ -504,9 +526,11 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
       f32x4 o = oacc[t] * alpha;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(Vs + (16 * t + q) * VR + (16 * kt + 4 * g) * 4);
+        // Vt[16t + q][16kt + 4g + e] = V[16kt + 4g + e][16t + q]: four dword reads down the V rows
+        // (the two lane groups of a 32-lane half are 4 rows = 16 banks apart: conflict-free)
+        const float* vc = reinterpret_cast<const float*>(Vs + (16 * kt + 4 * g) * KR) + 16 * t + q;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], pe[kt][e], o, 0, 0, 0);
+        for (int e = 0; e < 4; ++e) o = __builtin_amdgcn_mfma_f32_16x16x4f32(vc[e * (KR / 4)], pe[kt][e], o, 0, 0, 0);
       }
       oacc[t] = o;
     }
@@ -551,22 +575,21 @@ __device__ inline void at_split8(f32x4 a, f32x4 b, half8& hi, half8& lo) {
 
 template <int DK>
 __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __restrict__ pu, const float* __restrict__ pv,
-                                                               const float* __restrict__ qkv, const float* __restrict__ vt,
+                                                               const float* __restrict__ qkv,
                                                                const float* __restrict__ ptab, const int* __restrict__ lens,
-                                                               int Tp, int D, int H, int Sk, int rmax, float scale,
+                                                               int Tp, int D, int H, int rmax, float scale,
                                                                float* __restrict__ out, int nqb, int nbatch,
                                                                int* __restrict__ range_flag) {
   using MF = Mfma16<half_t>;
   typedef half8 Frag;
   constexpr int KS = DK / 32;         // k-steps over dk
   constexpr int DT = DK / 16;         // 16-row tiles of dk (O^T)
-  constexpr int KR = DK * 2 + 16;     // K / R plane row stride (bytes; odd 16-byte slots)
-  constexpr int VR = AT_BK * 2 + 16;  // Vt plane row stride (80 B)
-  constexpr int KPL = AT_BK * KR, VPL = DK * VR, RPL = AT_RW * KR;  // plane sizes (lo = hi + size)
+  constexpr int KR = at_kr<half_t>(DK);  // K / V / R plane row stride (bytes)
+  constexpr int KPL = AT_BK * KR, RPL = AT_RW * KR;  // plane sizes (lo = hi + size)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;                                        // 2 x [32 keys][DK]
-  char* Vs = Ks + 2 * KPL;                                // 2 x [DK][32 keys]
-  char* Rs = Vs + 2 * VPL;                                // 2 x [96 slots][DK]
+  char* Vs = Ks + 2 * KPL;                                // 2 x [32 keys][DK]
+  char* Rs = Vs + 2 * KPL;                                // 2 x [96 slots][DK]
   float* Gs = reinterpret_cast<float*>(Rs + 2 * RPL);     // [4 waves][48 slots][16 q]
 
   int bh, qb;
@@ -607,11 +630,11 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
 
   // staging: fp32 pieces loaded for step s+1 during step s, split into the two planes after
   // the barrier that ends it (every step).  As in rel_attn_kernel: buffer descriptors stepped by
-  // scalar base arithmetic (K rows >= len and Vt columns past the block read 0, table rows past
-  // the last read 0 -- only masked keys use them), per-thread offsets and LDS destinations fixed,
-  // ring slots stepped by one unsigned min, masks only on the last key step
+  // scalar base arithmetic (K and V rows >= len read 0, table rows past the last read 0 -- only
+  // masked keys use them), per-thread offsets and LDS destinations fixed, ring slots stepped by
+  // one unsigned min, masks only on the last key step
   constexpr int KP = AT_BK * (DK / 4) / 256;
-  static_assert(AT_BK * (DK / 4) % 256 == 0 && DK * (AT_BK / 4) % 256 == 0, "staging split");
+  static_assert(AT_BK * (DK / 4) % 256 == 0, "staging split");
   constexpr unsigned RING = AT_RW * KR;
   auto rslot = [](int m) { const int r = m % AT_RW; return r < 0 ? r + AT_RW : r; };
   auto rrow = [&](int m) { return min(max(rmax - 1 - m, 0), 2 * rmax - 1); };
@@ -624,30 +647,26 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
     *reinterpret_cast<uint2*>(plane_hi + plane + off) = lo;
   };
   const int rowB = 3 * D * 4;  // QKV row bytes
-  int kofs[KP], vofs[KP], rofs[KP];
-  unsigned kdst[KP], vdst[KP], rdst[KP];
+  int kofs[KP], rofs[KP];
+  unsigned kdst[KP], rdst[KP];
 #pragma unroll
   for (int i = 0; i < KP; ++i) {
     const int p = tid + 256 * i;
     const int r = p / (DK / 4), c = p - r * (DK / 4);
-    kofs[i] = r * rowB + c * 16;
+    kofs[i] = r * rowB + c * 16;                         // K and V rows
     kdst[i] = r * KR + c * 8;
     rofs[i] = r * D * 4 + c * 16;                        // table row row0 + r <-> m = i0 - j0 - r
     rdst[i] = rslot(i0 - AT_BK - r) * KR + c * 8;        // slot for the first prefetch (j0 = 32)
-    const int d = p / (AT_BK / 4), cv = p - d * (AT_BK / 4);
-    vofs[i] = d * Sk * 4 + cv * 16;
-    vdst[i] = d * VR + cv * 8;
   }
   f32x4 pkv[KP], pvt[KP], prr[KP];
   auto load_kv = [&](int j0) __attribute__((always_inline)) {
-    const auto kr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(qkv + ((long long)b * Tp + j0) * 3 * rowD + D + h * DK),
-                                                      0, max(len - j0, 0) * rowB, 0x00020000);
-    const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vt + ((long long)b * H + h) * DK * Sk + j0), 0,
-                                                      max(DK * Sk - j0, 0) * 4, 0x00020000);
+    const float* krow = qkv + ((long long)b * Tp + j0) * 3 * rowD + D + h * DK;
+    const auto kr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(krow), 0, max(len - j0, 0) * rowB, 0x00020000);
+    const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(krow + D), 0, max(len - j0, 0) * rowB, 0x00020000);
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
       pkv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(kr, kofs[i], 0, 0));
-      pvt[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(vr, vofs[i], 0, 0));
+      pvt[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(vr, kofs[i], 0, 0));
     }
   };
   auto load_r = [&](int j0) __attribute__((always_inline)) {
@@ -662,7 +681,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
       put(Ks, KPL, kdst[i], pkv[i]);
-      put(Vs, VPL, vdst[i], pvt[i]);
+      put(Vs, KPL, kdst[i], pvt[i]);
     }
   };
   auto write_r = [&]() __attribute__((always_inline)) {
@@ -681,6 +700,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
   write_kv();
   __syncthreads();
   unsigned ra = rslot(i0w - (AT_BK - 1) + q) * KR + 16 * g;  // this lane's R rows (slot of m + 16 t) and column
+  const int vta = at_tr_addr(KR, g, q);  // this lane's transposed-read address in the V planes (tile 0)
 
   for (int j0 = 0; j0 < len; j0 += AT_BK) {
     load_kv(j0 + AT_BK);
@@ -719,7 +739,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
     for (int t = 0; t < 3; ++t) {
       const f32x4 gv = gacc[t] + gaccx[t] * (1.f / AT_SPLIT);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) gw[(16 * t + 4 * g + e) * 16 + q] = gv[e];
+      for (int e = 0; e < 4; ++e) gw[at_gslot(16 * t + 4 * g + e) * 16 + q] = gv[e];
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's scratch writes landed
     __builtin_amdgcn_wave_barrier();
@@ -730,7 +750,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int kk = 16 * kt + 4 * g + e;
-        const float bd = gw[(q - kk + AT_BK - 1) * 16 + q];
+        const float bd = gw[at_gslot(q - kk + AT_BK - 1) * 16 + q];
         sv[4 * kt + e] = (s4[e] + bd) * sl2;
       }
     }
@@ -766,9 +786,9 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
     at_split8(pe0, pe1, bp, bpl);
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
-      const char* vr = Vs + (16 * t + q) * VR + 8 * g;
-      const uint2 h0 = *reinterpret_cast<const uint2*>(vr), h1 = *reinterpret_cast<const uint2*>(vr + 32);
-      const uint2 l0 = *reinterpret_cast<const uint2*>(vr + VPL), l1 = *reinterpret_cast<const uint2*>(vr + VPL + 32);
+      const char* vr = Vs + vta + t * 32;
+      const uint2 h0 = at_tr16(vr), h1 = at_tr16(vr + 16 * KR);
+      const uint2 l0 = at_tr16(vr + KPL), l1 = at_tr16(vr + KPL + 16 * KR);
       const Frag ah = __builtin_bit_cast(Frag, uint4{h0.x, h0.y, h1.x, h1.y});
       const Frag al = __builtin_bit_cast(Frag, uint4{l0.x, l0.y, l1.x, l1.y});
       oacc[t] = MF::mma(ah, bp, oacc[t] * alpha);
@@ -793,20 +813,20 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
 
 template <int DK>
 size_t rel_attn_split_lds() {
-  return (size_t)2 * (AT_BK * (DK * 2 + 16) + DK * (AT_BK * 2 + 16) + AT_RW * (DK * 2 + 16)) + (size_t)4 * 48 * 16 * 4;
+  return (size_t)2 * (2 * AT_BK + AT_RW) * at_kr<half_t>(DK) + (size_t)4 * 48 * 16 * 4;
 }
 
 template <int DK>
 size_t rel_attn_f32_lds() {
-  return (size_t)AT_BK * (DK * 4 + 16) + (size_t)DK * (AT_BK * 4 + 16) + (size_t)AT_RW * (DK * 4 + 16) +
-         (size_t)4 * 48 * 16 * 4;
+  return (size_t)(2 * AT_BK + AT_RW) * at_kr<float>(DK) + (size_t)4 * 48 * 16 * 4;
 }
 
 template <int DK>
 size_t rel_attn_lds(int kh) {
-  return (size_t)kh * (AT_BK * (DK * 2 + 16) + (size_t)DK * (AT_BK * 2 + 16) + (size_t)AT_RW * (DK * 2 + 16) +
-                       (size_t)4 * 48 * 16 * 4);
+  return (size_t)kh * ((2 * AT_BK + AT_RW) * at_kr<half_t>(DK) + (size_t)4 * 48 * 16 * 4);
 }
+// two 16-bit blocks per CU (rel_attn_kernel's launch bounds)
+static_assert((2 * AT_BK + AT_RW) * at_kr<half_t>(192) + 4 * 48 * 16 * 4 <= 160 * 1024 / 2, "LDS");
 
 }  // namespace
 
@@ -814,21 +834,21 @@ bool rel_attn_supported(int dt, int D, int H) {
   return (dt == DT_F16 || dt == DT_BF16 || dt == DT_F32) && H > 0 && D % H == 0 && D / H == 192;
 }
 
-hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* pos_v, const void* qkv, const void* vt,
-                           const void* ptab, const int* lens, int B, int Tm, int Tp, int D, int H, int Sk, int rmax,
+hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* pos_v, const void* qkv,
+                           const void* ptab, const int* lens, int B, int Tm, int Tp, int D, int H, int rmax,
                            float scale, void* out, hipStream_t s, int* range_flag) {
-  if (!rel_attn_supported(dt, D, H) || Tm > rmax || Sk % 8) return hipErrorInvalidValue;
+  if (!rel_attn_supported(dt, D, H) || Tm > rmax) return hipErrorInvalidValue;
   const int nqb = (Tm + AT_BQ - 1) / AT_BQ;
   dim3 grid(xcd_grid(nqb, H * B));
   if (dt == DT_F32 && split) {
     hipLaunchKernelGGL((rel_attn_split_kernel<192>), grid, dim3(256), rel_attn_split_lds<192>(), s, pos_u, pos_v,
-                       (const float*)qkv, (const float*)vt, (const float*)ptab, lens, Tp, D, H, Sk, rmax, scale,
+                       (const float*)qkv, (const float*)ptab, lens, Tp, D, H, rmax, scale,
                        (float*)out, nqb, B, range_flag);
     return hipGetLastError();
   }
   if (dt == DT_F32) {
     hipLaunchKernelGGL((rel_attn_f32_kernel<192>), grid, dim3(256), rel_attn_f32_lds<192>(), s, pos_u, pos_v,
-                       (const float*)qkv, (const float*)vt, (const float*)ptab, lens, Tp, D, H, Sk, rmax, scale,
+                       (const float*)qkv, (const float*)ptab, lens, Tp, D, H, rmax, scale,
                        (float*)out, nqb, B);
     return hipGetLastError();
   }
@@ -839,7 +859,7 @@ hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* 
   const size_t lds = rel_attn_lds<192>(kh);
 #define TTS_ATTN_LAUNCH(TT_, KH_)                                                                  \
   hipLaunchKernelGGL((rel_attn_kernel<TT_, 192, KH_>), grid, dim3(256 * KH_), lds, s, pos_u, pos_v, \
-                     (const TT_*)qkv, (const TT_*)vt, (const TT_*)ptab, lens, Tp, D, H, Sk, rmax, scale, \
+                     (const TT_*)qkv, (const TT_*)ptab, lens, Tp, D, H, rmax, scale,                     \
                      (TT_*)out, nqb, B)
   if (dt == DT_F16) {
     if (kh == 2) TTS_ATTN_LAUNCH(half_t, 2); else TTS_ATTN_LAUNCH(half_t, 1);

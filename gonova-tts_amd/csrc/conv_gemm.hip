@@ -293,6 +293,12 @@ __device__ unsigned long long g_xres_stamp[1 << 20];
 // rows in flight per wave; arithmetic of layernorm8_kernel / ln_linear1_kernel (ln_rows.h).
 template <typename T, int BN>
 __device__ inline void xres_tile_ln(const ConvParams& p, const T* Y, int b, int n0, int ylen, int wave, int lane) {
+  if constexpr (BN > 128) {
+    // 128-row pieces: at 256 rows the tail's loop below is not fully unrolled, and its
+    // double buffer u[it & 1] went to scratch (144 B/lane)
+    for (int h = 0; h < BN && n0 + h < ylen; h += 128) xres_tile_ln<T, 128>(p, Y, b, n0 + h, ylen, wave, lane);
+    return;
+  }
   const int nrow = min(BN, ylen - n0);
   const int C = p.M;
   constexpr int RB = TTS_LN_RB;  // rows per wave in flight and normalised together
@@ -1005,7 +1011,7 @@ static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err, boo
   const bool big = TTS_XRES_BIGCG_MIN > 0 && wm == 4 && p.Cin >= TTS_XRES_BIGCG_MIN;
   const int cg = xres_group(p, 32 * 4 * (4 / wm), big ? XRES_LDS_BIG : XRES_LDS_MAX);
   if (!cg) return false;
-  if (wm == 2)
+  if (wm == 2)  // (the postnet's 80-channel output conv)
     *err = launch_xres_wm<T, 2>(p, cg, s, ln_done);
   else if (big)
     *err = xres_narrow(p, nt) ? launch_xres_wm<T, 2, 1, 1>(p, cg, s, ln_done)

@@ -164,6 +164,9 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
   constexpr int BN = P::BN, WM = C / 32, WN = 4 / WM, RS = G::RS, D = G::D, A = P::A;  // 32 channels per wave
   constexpr int NTHR = 256, MT = 2, KS = C / 32, S = K * KS, VPR = C / 8;
   constexpr int H0 = P::H0, NR = P::NR, NRA = P::NRA;
+  // bf16 (f32 epilogue arithmetic) on the tall C = 64 tile: the MRF-sum rows are loaded after
+  // the last epilogue instead of during it (held across it they push the kernel past 168 VGPRs)
+  constexpr bool SIN_LATE = !__is_same(T, half_t) && C == 64 && BN > 128;
   static_assert(WM * WN * 64 == NTHR && WM * 32 == C, "wave grid");
   static_assert(BN % 16 == 0 && (NR - 2 * P::lo2(2)) == BN, "last conv covers exactly the output rows");
   auto swz = [](int r) { return ((r * G::SW_MUL) >> G::SW_S) & G::SW_M; };
@@ -244,6 +247,16 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
   T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
   constexpr int NIT = (BN * VPR + NTHR - 1) / NTHR;  // row-pass pieces per thread (the last may be partial)
   uint4 sin[NIT];
+  // the MRF-sum rows the row pass adds (no records when not accumulating)
+  auto load_sin = [&]() __attribute__((always_inline)) {
+    const auto yrsrc = __builtin_amdgcn_make_buffer_rsrc(Y, 0, p.accum ? len * C * (int)sizeof(T) : 0, 0x00020000);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NTHR;
+      const int e = min(n0 + idx / VPR, len - 1) * C + (idx % VPR) * 8;
+      sin[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrsrc, e * (int)sizeof(T), 0, 0));
+    }
+  };
   auto pair = [&](auto PI) __attribute__((always_inline)) {
     constexpr int Q = decltype(PI)::value;
     constexpr int DQ = P::DIL[Q];
@@ -307,14 +320,8 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) bias[mt] = *reinterpret_cast<const f32x4*>(p.b1[Q + 1] + ch0 + 16 * mt);
         preload(p.w1[Q + 1]);
-      } else {  // MRF-sum rows in flight during the last epilogue (no records: not accumulating)
-        const auto yrsrc = __builtin_amdgcn_make_buffer_rsrc(Y, 0, p.accum ? len * C * (int)sizeof(T) : 0, 0x00020000);
-#pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-          const int idx = tid + it * NTHR;
-          const int e = min(n0 + idx / VPR, len - 1) * C + (idx % VPR) * 8;
-          sin[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrsrc, e * (int)sizeof(T), 0, 0));
-        }
+      } else if constexpr (!SIN_LATE) {  // MRF-sum rows in flight during the last epilogue
+        load_sin();
       }
       __builtin_amdgcn_sched_barrier(0);
       __syncthreads();  // T no longer read
@@ -348,6 +355,7 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
   pair(std::integral_constant<int, 0>{});
   pair(std::integral_constant<int, 1>{});
   pair(std::integral_constant<int, 2>{});
+  if constexpr (SIN_LATE) load_sin();
 
   // ---- row pass: y = ((accum ? S : 0) + (y2 + h2)) * scale over rows [n0, n0 + BN) ----
 #pragma unroll

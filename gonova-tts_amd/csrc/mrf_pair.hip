@@ -144,8 +144,10 @@ struct PairGeomS : PairGeom<C> {
                            : DIV == 1 && C == 256 && K == 11 ? TTS_P256K11_D
                                                              : PairGeom<C>::D;
   // blocks per CU the register budget is sized for (the C = 32 k = 11 pairs without conv_post
-  // may take a fourth: TTS_P32K11_OCC)
-  static constexpr int OCC = C == 32 && K == 11 && !POST && DIV == 1 ? TTS_P32K11_OCC : PairGeom<C>::OCC;
+  // may take a fourth: TTS_P32K11_OCC; the HiFi-GAN V3 C = 64 k = 5 pair spills at three)
+  static constexpr int OCC = C == 32 && K == 11 && !POST && DIV == 1 ? TTS_P32K11_OCC
+                             : C == 64 && K == 5                    ? 2
+                                                                    : PairGeom<C>::OCC;
 };
 
 // LDS bytes of one launch (G tile incl. conv1 overrun rows, T tile; >= output staging tile of

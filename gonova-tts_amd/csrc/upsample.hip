@@ -19,6 +19,7 @@
 //   * the output tile goes through a per-wave LDS slice into 16-byte row pieces: the item's
 //     outputs are one contiguous span (rows s*u0 - p ...), written with non-temporal stores.
 #include <algorithm>
+#include <atomic>
 
 #include "common.h"
 #include "kernels.h"
@@ -32,7 +33,7 @@
 
 namespace tts {
 
-template <int CIN, int M>
+template <typename T, int CIN, int M>
 struct UpGeom;
 // NU: 16-row tiles per item; NW: waves per block (LDS: weights + NW staging slices)
 #ifndef TTS_UP2_NU
@@ -41,20 +42,25 @@ struct UpGeom;
 #ifndef TTS_UP2_NW
 #define TTS_UP2_NW 12
 #endif
+#ifndef TTS_UP2_NW_BF16
+#define TTS_UP2_NW_BF16 8  // bf16: its LeakyReLU goes through f32, and at 12 waves (168 VGPRs) it spilled
+#endif
 #ifndef TTS_UP3_NU
 #define TTS_UP3_NU 2
 #endif
 #ifndef TTS_UP3_NW
 #define TTS_UP3_NW 8
 #endif
-template <>
-struct UpGeom<128, 128> { static constexpr int NU = TTS_UP2_NU, NW = TTS_UP2_NW; };  // stage 2: 64 KB weights
-template <>
-struct UpGeom<64, 64> { static constexpr int NU = TTS_UP3_NU, NW = TTS_UP3_NW; };     // stage 3: 16 KB weights
+template <typename T>
+struct UpGeom<T, 128, 128> {  // stage 2: 64 KB weights
+  static constexpr int NU = TTS_UP2_NU, NW = __is_same(T, bf16_t) ? TTS_UP2_NW_BF16 : TTS_UP2_NW;
+};
+template <typename T>
+struct UpGeom<T, 64, 64> { static constexpr int NU = TTS_UP3_NU, NW = TTS_UP3_NW; };  // stage 3: 16 KB weights
 
-template <int CIN, int M>
+template <typename T, int CIN, int M>
 constexpr size_t up_lds_bytes() {
-  using G = UpGeom<CIN, M>;
+  using G = UpGeom<T, CIN, M>;
   return (size_t)M * 2 * CIN * 2 + (size_t)M * 4 + (size_t)G::NW * 16 * G::NU * (M * 2 + 16);
 }
 
@@ -72,8 +78,8 @@ __device__ inline uint4 up_lrelu(uint4 u, float slope) {
 }
 
 template <typename T, int CIN, int M>
-__global__ __launch_bounds__((64 * UpGeom<CIN, M>::NW)) void upsample_stream_kernel(UpsampleParams p) {
-  using G = UpGeom<CIN, M>;
+__global__ __launch_bounds__((64 * UpGeom<T, CIN, M>::NW)) void upsample_stream_kernel(UpsampleParams p) {
+  using G = UpGeom<T, CIN, M>;
   using MF = Mfma16<T>;
   typedef typename Mfma<T>::frag Frag;
   constexpr int NU = G::NU, NW = G::NW, K = 2 * CIN, KS = K / 32, MT = M / 16;
@@ -206,17 +212,21 @@ bool upsample_stream_supported(int dtype, int Cin, int M, int taps) {
 
 template <typename T, int CIN, int M>
 static hipError_t launch_up_t(const UpsampleParams& p, hipStream_t s) {
-  using G = UpGeom<CIN, M>;
-  constexpr size_t lds = up_lds_bytes<CIN, M>();
+  using G = UpGeom<T, CIN, M>;
+  constexpr size_t lds = up_lds_bytes<T, CIN, M>();
   static_assert(lds <= 160 * 1024, "LDS");
-  static int grid = 0;
+  // blocks that fit at once, per device (engines on several GPUs launch from their own threads)
+  static std::atomic<int> grid_of[64];
+  int dev = 0;
+  HIP_RETURN_IF(hipGetDevice(&dev));
+  int grid = dev >= 0 && dev < 64 ? grid_of[dev].load(std::memory_order_relaxed) : 0;
   if (!grid) {
-    int per_cu = 0, dev = 0, cus = 0;
+    int per_cu = 0, cus = 0;
     HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upsample_stream_kernel<T, CIN, M>,
                                                                64 * G::NW, lds));
-    HIP_RETURN_IF(hipGetDevice(&dev));
     HIP_RETURN_IF(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     grid = std::max(1, per_cu) * cus;
+    if (dev >= 0 && dev < 64) grid_of[dev].store(grid, std::memory_order_relaxed);
   }
   const int ipu = (p.T + 1 + 16 * G::NU - 1) / (16 * G::NU);
   const int blocks = std::min(grid, (ipu * p.B + G::NW - 1) / G::NW);

@@ -401,10 +401,11 @@ def test_multi_device_fan_out_keeps_order_and_balances():
         assert [len(f) for f in frames] == [100 * len(s) for s in sents]
         for f, s in zip(frames, sents):
             assert np.all(f == len(s))
-    # both engines got work (warmups excluded), and their loads are within one long sentence
+    # both engines got work (warmups excluded) and neither carried most of it: engines pull
+    # batches when they come free, so the split follows timing, not a fixed deal
     work = [sum(len(t) for b in m.batches[3:] for t in b) for m in made]
     assert all(w > 0 for w in work), work
-    assert abs(work[0] - work[1]) <= max(len(t) for t in texts.values()), work
+    assert min(work) >= 0.25 * sum(work), work
     assert sum(stats["engine_sentences"]) == 20 and min(stats["engine_sentences"]) > 0
 
 

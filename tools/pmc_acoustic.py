@@ -13,7 +13,7 @@ ITERS = 4  # tools/acoustic_prof.py
 
 
 def short(name):
-    for k in ("conv_xres", "conv_splitp", "conv_split_kernel", "split_reduce", "conv_gemm", "rel_attn_split",
+    for k in ("conv_mt", "conv_xres", "conv_splitp", "conv_split_kernel", "split_reduce", "conv_gemm", "rel_attn_split",
               "rel_attn_kernel", "layernorm8", "layernorm_kernel", "glu_dwconv", "transpose_v", "ln_linear1"):
         if k in name:
             return k
@@ -38,12 +38,15 @@ def main():
     dirs = [a for a in sys.argv[1:] if not a.isdigit()]
     batch = next((a for a in sys.argv[1:] if a.isdigit()), "32")
     per, kname, dur, ids = load(dirs[0])
-    fam = defaultdict(lambda: [0.0, 0.0, 0.0, 0.0, 0.0, 0])
+    # per family: time, GRBM cycles and time of the long dispatches, MFMA busy, waits, wave cycles, count
+    fam = defaultdict(lambda: [0.0, 0.0, 0.0, 0.0, 0.0, 0, 0.0])
     for i in ids:
         c, t = per[i], dur.get(i, 0.0)
         f = fam[short(kname[i])]
         f[0] += t
-        f[1] += c.get("GRBM_GUI_ACTIVE", 0) / 8
+        if t >= 20e-6:
+            f[1] += c.get("GRBM_GUI_ACTIVE", 0) / 8
+            f[6] += t
         f[2] += c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0)
         f[3] += c.get("SQ_WAIT_INST_ANY", 0)
         f[4] += max(c.get("SQ_WAVE_CYCLES", 0), 1)
@@ -63,19 +66,27 @@ def main():
                 e[k] += p3[i].get(k, 0.0)
     tot = sum(f[0] for f in fam.values())
     print(f"one acoustic forward (batch {batch}, bf16, exact encoder): {len(ids)} dispatches, {tot * 1e6:.0f} us under the profiler")
-    print("mfma% = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024) at the measured clock, @2.4 at the nominal one;")
+    print("mfma% = SQ_VALU_MFMA_BUSY_CYCLES / (clock x duration x 1024 SIMDs): GHz = GRBM_GUI_ACTIVE/8 / duration over the")
+    print("family's dispatches of >= 20 us (a short dispatch's counter window outlasts its trace duration, which")
+    print("overstated the clock); '-' where none is that long, mfma% then only at the nominal 2.4 GHz (@2.4);")
     print("FETCH (x2 gfx950 correction) / WRITE in MB per forward; valu/mfma, lds/mfma instructions; bankconf = extra LDS cycles per LDS instruction")
     print(f"{'family':18s} {'n':>4s} {'us':>8s} {'share':>6s} {'GHz':>5s} {'mfma%':>6s} {'@2.4':>6s} {'FETCH':>8s} {'WRITE':>8s} "
           f"{'valu/mf':>7s} {'lds/mf':>6s} {'bankc':>6s}")
     for k, f in sorted(fam.items(), key=lambda kv: -kv[1][0]):
-        ghz = f[1] / max(f[0], 1e-12) / 1e9
         e = extra[k]
-        mf = max(e.get("SQ_INSTS_MFMA", 0.0), 1.0)
-        print(f"{k:18s} {f[5]:4d} {f[0] * 1e6:8.1f} {100 * f[0] / tot:5.1f}% {ghz:5.2f} "
-              f"{100 * f[2] / max(f[1] * 1024, 1):6.1f} {100 * f[2] / (2.4e9 * f[0] * 1024):6.1f} "
-              f"{e.get('FETCH_SIZE', 0) / 1e6:8.1f} {e.get('WRITE_SIZE', 0) / 1e6:8.1f} "
-              f"{e.get('SQ_INSTS_VALU', 0) / mf:7.2f} {e.get('SQ_INSTS_LDS', 0) / mf:6.2f} "
-              f"{e.get('SQ_LDS_BANK_CONFLICT', 0) / max(e.get('SQ_INSTS_LDS', 0), 1):6.2f}")
+        if f[6] > 0:
+            ghz = min(f[1] / f[6] / 1e9, 2.4)  # (bounded by the chip's peak clock)
+            g_s, m_s = f"{ghz:5.2f}", f"{100 * f[2] / (ghz * 1e9 * f[0] * 1024):6.1f}"
+        else:
+            g_s, m_s = f"{'-':>5s}", f"{'-':>6s}"
+        mf = e.get("SQ_INSTS_MFMA", 0.0)
+        lds = e.get("SQ_INSTS_LDS", 0.0)
+        r_valu = f"{e.get('SQ_INSTS_VALU', 0) / mf:7.2f}" if mf else f"{'-':>7s}"
+        r_lds = f"{lds / mf:6.2f}" if mf else f"{'-':>6s}"
+        r_bank = f"{e.get('SQ_LDS_BANK_CONFLICT', 0) / lds:6.2f}" if lds else f"{'-':>6s}"
+        print(f"{k:18s} {f[5]:4d} {f[0] * 1e6:8.1f} {100 * f[0] / tot:5.1f}% {g_s} {m_s} "
+              f"{100 * f[2] / (2.4e9 * f[0] * 1024):6.1f} "
+              f"{e.get('FETCH_SIZE', 0) / 1e6:8.1f} {e.get('WRITE_SIZE', 0) / 1e6:8.1f} {r_valu} {r_lds} {r_bank}")
 
 
 if __name__ == "__main__":

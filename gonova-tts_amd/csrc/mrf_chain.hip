@@ -103,6 +103,9 @@ constexpr int CHAIN_D0 = 1, CHAIN_D1 = 3, CHAIN_D2 = 5;  // HiFi-GAN V1/V2 dilat
 #ifndef TTS_CHAIN_BN64_3_BF16
 #define TTS_CHAIN_BN64_3_BF16 128
 #endif
+#ifndef TTS_CHAIN_D64_BF16
+#define TTS_CHAIN_D64_BF16 3
+#endif
 template <typename T, int C, int K>
 constexpr int chain_bn() {
   return C == 64 && K == 3 && !__is_same(T, half_t) ? TTS_CHAIN_BN64_3_BF16 : ChainGeom<C, K>::BN;
@@ -161,7 +164,10 @@ __global__ __launch_bounds__(256, (ChainGeom<C, K>::OCC)) void mrf_chain_kernel(
   using G = PairGeom<C>;
   using P = ChainPlan<C, K, chain_bn<T, C, K>()>;
   typedef typename Mfma<T>::frag Frag;
-  constexpr int BN = P::BN, WM = C / 32, WN = 4 / WM, RS = G::RS, D = G::D, A = P::A;  // 32 channels per wave
+  constexpr int BN = P::BN, WM = C / 32, WN = 4 / WM, RS = G::RS, A = P::A;  // 32 channels per wave
+  // weight ring depth (k-steps ahead): one shallower for the tall bf16 C = 64 tile, whose f32
+  // epilogue arithmetic otherwise pushes it past 168 VGPRs (same k-step order: bit-identical)
+  constexpr int D = !__is_same(T, half_t) && C == 64 && BN > 128 ? TTS_CHAIN_D64_BF16 : G::D;
   constexpr int NTHR = 256, MT = 2, KS = C / 32, S = K * KS, VPR = C / 8;
   constexpr int H0 = P::H0, NR = P::NR, NRA = P::NRA;
   // bf16 (f32 epilogue arithmetic) on the tall C = 64 tile: the MRF-sum rows are loaded after

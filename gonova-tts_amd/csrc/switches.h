@@ -24,8 +24,8 @@ enum Sw : int {
   SW_LN_FUSE,      // TTS_LN_FUSE=0: acoustic post-LNs as their own launches; 7: in every eligible GEMM launch (2-6: bisection)
   SW_SPLIT_NT1,    // TTS_SPLIT_NT1=0: split GEMMs always on 64-row tiles; 1: 32-row tiles wherever eligible (default: small grids)
   SW_XRES_ORDER,   // TTS_XRES_ORDER=1: multi-tap DMA conv_xres launches on an XCD-ordered grid (M block fastest); 2: every conv_xres launch
-  SW_CONV_MT,      // TTS_CONV_MT=0: the acoustic 16-bit GEMMs on conv_xres instead of the macro-tiled conv_mt kernel
-  SW_MT_TILE,      // TTS_MT_TILE=0..3: force a conv_mt tile configuration (tests; default: chosen per launch)
+  SW_CONV_MT,      // TTS_CONV_MT=1: the acoustic 16-bit GEMMs on conv_mt (k = 3 layers on conv_tap_kernel; 2: on conv_mt_kernel) instead of conv_xres (default 0)
+  SW_MT_TILE,      // TTS_MT_TILE=0..3: force a conv_mt_kernel tile configuration, 4..10 a conv_tap_kernel one (tests; default: chosen per launch)
   SW_N
 };
 

@@ -291,7 +291,7 @@ def test_short_row_tiles_bit_identical(aw, dtype, switch):
     rng = np.random.default_rng(12)
     ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70)]
     durs = [np.full(len(x), 3) for x in ids_list]
-    switch("TTS_CONV_MT", 0)       # conv_xres runs the acoustic GEMMs (the decoder's default is conv_mt)
+    switch("TTS_CONV_MT", 0)       # conv_xres runs the acoustic GEMMs (the default; conv_mt is opt-in)
     switch("TTS_XRES_NARROW", 0)   # 128-channel tiles: the tile-height pair
     switch("TTS_XRES_NT", 4)
     big, lb, _ = run(eng, ids_list, t_cap=432, durations=durs)
@@ -422,9 +422,11 @@ def test_xcd_ordered_xres_grid_bit_identical(aw, dtype, switch):
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_macro_tile_gemm_configs_bit_identical(aw, dtype, switch):
-    """conv_mt (csrc/conv_mt.hip: 8-wave blocks, both operands through LDS by LDS-DMA) runs the
-    16-bit acoustic GEMMs.  Its tile configurations (256 x 224, 192 x 224, 384 x 112 with the
-    post-LN in the launch, 128 x 128; TTS_MT_TILE forces one wherever the layer's channels divide)
+    """conv_mt (csrc/conv_mt.hip: 8-wave blocks, both operands through LDS by LDS-DMA; opt-in,
+    TTS_CONV_MT=1) runs the 16-bit acoustic GEMMs, the k = 3 FFN convs on its multi-tap form (one
+    X tile shared by the taps).  Its tile configurations (256 x 224, 192 x 224, 384 x 112 with the post-LN in the
+    launch, 128 x 128; multi-tap 128 x 448, 192 x 224, 256 x 224, 128 x 224, 128 x 128;
+    TTS_MT_TILE forces one wherever the layer's channels divide)
     share one K order, so predicted durations, frame counts and mel agree bit for bit with the
     automatic choice, with the post-LN fused or as its own launch (TTS_LN_FUSE=0), on a ragged
     batch whose lengths cross 112-, 128- and 224-row edges; batch 1 equals its row of the batch;
@@ -433,7 +435,8 @@ def test_macro_tile_gemm_configs_bit_identical(aw, dtype, switch):
     rng = np.random.default_rng(47)
     ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70, 127, 129, 9, 33)]
     outs = {}
-    for tile in (None, 0, 1, 2, 3):
+    switch("TTS_CONV_MT", 1)  # (opt-in: conv_xres is the default)
+    for tile in (None, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10):  # 4..10: the multi-tap (k = 3) configurations
         switch("TTS_MT_TILE", tile)
         outs[tile] = run(eng, ids_list, t_cap=8 * 144)
     switch("TTS_MT_TILE", None)
@@ -451,7 +454,7 @@ def test_macro_tile_gemm_configs_bit_identical(aw, dtype, switch):
     forced, fl, _ = run(eng, ids_list, t_cap=8 * 144, durations=durs)
     switch("TTS_CONV_MT", 0)
     xres, xl, _ = run(eng, ids_list, t_cap=8 * 144, durations=durs)
-    switch("TTS_CONV_MT", None)
+    switch("TTS_CONV_MT", 1)
     for b in (0, 2, 4, 5):
         L = int(fl[b])
         assert int(xl[b]) == L

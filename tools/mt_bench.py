@@ -2,7 +2,8 @@
 conv_xres / conv_gemm, whichever the library picks for the shape), at the C3 decoder's shapes.
 
 usage (GPU box): python3 tools/mt_bench.py [layer ...]    (default: every layer below)
-env: MT_B (utterances, 32), MT_T (rows per utterance, 864), MT_ITERS (50), TTS_MT_TILE / TTS_LIB as usual.
+env: MT_B (utterances, 32), MT_T (rows per utterance, 864), MT_ITERS (50), TTS_MT_TILE / TTS_LIB as usual;
+TTS_CONV_MT defaults to 1 here (the kernels under test; conv_xres needs the engine's packed weights).
 Prints per layer: launches' mean time (hipEvents around MT_ITERS back-to-back launches), algorithmic
 TFLOP/s, and the max relative error against a torch fp32 reference of the same conv on one utterance.
 """
@@ -25,6 +26,7 @@ LAYERS = {
 
 
 def main():
+    os.environ.setdefault("TTS_CONV_MT", "1")  # conv_mt / conv_tap (opt-in in the product)
     import torch
     from gonova_tts_amd.engine import TtsConvDesc, conv1d_op, load_library
     load_library()

@@ -461,6 +461,7 @@ struct tts_engine {
             pp.b1 = blk[q][0].bias; pp.b2 = blk[q][1].bias;
             pp.T = Tout; pp.B = B; pp.k = blk[q][0].taps; pp.d = blk[q][0].dil;
             pp.slope = slope;
+            pp.tbuf = T1;  // (free in the pair path: the channel-split form's t rows)
             pp.accum = (last && j > 0) ? 1 : 0;
             pp.scale = (last && j == nk - 1) ? 1.0f / (float)nk : 1.f;
             if (last && j == nk - 1 && i == nst - 1 && v.post_wh && post_fuse_enabled() &&

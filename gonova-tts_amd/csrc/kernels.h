@@ -123,6 +123,9 @@ struct MrfPairParams {
   // activation the next upsampler would apply on load, so a stage's last pair hands it lrelu(S)
   int out_act;
   float out_slope;
+  // optional [B][T][C] scratch (compute dtype): with it, launches whose full-height grid is small
+  // (the streamed vocoder's first chunk) run the channel-split form (mrf_pair.hip), bit-identical
+  void* tbuf;
 };
 bool mrf_pair_supported(int dtype, int C, int k);
 bool mrf_pair_outact_supported(int dtype, int C, int k);  // the launch can carry out_act

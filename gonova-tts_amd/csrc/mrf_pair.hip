@@ -52,6 +52,12 @@
 
 namespace tts {
 
+#define HIP_RETURN_IF_ERR(expr)         \
+  do {                                  \
+    const hipError_t e_ = (expr);       \
+    if (e_ != hipSuccess) return e_;    \
+  } while (0)
+
 #if TTS_PAIR_STAMP
 // Phase timestamps of the pair launches whose (C, k, d) match g_pair_stamp_target (the last such
 // launch of the workload wins), one record of 16 words per block: s_memtime at entry / input tile
@@ -468,6 +474,180 @@ static int pair_div(int C, const MrfPairParams& p, bool post) {
   return (long long)((p.T + bn - 1) / bn) * p.B < TTS_PAIR_SHORT ? TTS_PAIR_SHORT_DIV : 1;
 }
 
+
+// ---------------------------------------------------------------- channel-split form (small grids)
+// A pair launch whose full-height grid leaves most CUs idle (the streamed vocoder's first chunk:
+// batch 8 x 48 frames, stage 0 at 36 blocks, stage 1 at 192) is bound by the weight stream: every
+// block of mrf_pair_kernel reads the pair's 2 k C^2 weights from L2 (2.9 MB for k = 11 at C = 256,
+// ~41 us at the per-CU L2 rate of ~70 GB/s: the C5 trace's 42 us per launch,
+// profiles/r05j_c5_trace.txt).  Here the two convs are two launches over (row tile, channel slice)
+// blocks: each block stages the tile's input rows for every input channel and computes one 64-channel
+// slice, reading a quarter (C = 256) or half (C = 128) of a conv's weights; conv1's t rows go
+// through an HBM scratch (the engine's free T1 buffer).  Every output element is the same
+// k-step sequence (pair_conv: bias-initialised accumulators, taps x 32-channel k-steps in order),
+// the same roundings (epi_conv1 -> T, epi_conv2 -> T, epi_row) and the same zeros outside the
+// utterance as mrf_pair_kernel, so the result is bit-identical (tests/test_vocoder_gpu.py).
+#ifndef TTS_PSPLIT_WM
+#define TTS_PSPLIT_WM 4  // waves per block, one 16-channel M tile each (4: a 64-channel slice)
+#endif
+#ifndef TTS_PSPLIT_NU
+#define TTS_PSPLIT_NU 2  // 16-row tiles per wave: 32 rows per block (C5 chunk A/B: 4 -> 2 rows tiles 0.745 -> 0.719 ms, profiles/r05l_ab_pair_split.txt)
+#endif
+constexpr int PSPLIT_WM = TTS_PSPLIT_WM;
+constexpr int PSPLIT_NU = TTS_PSPLIT_NU;
+constexpr int PSPLIT_D = 4;   // weight ring depth (k-steps)
+
+template <typename T, int C, int K, bool CONV2, bool OUTACT>
+__global__ __launch_bounds__(64 * PSPLIT_WM) void mrf_pair_split_kernel(MrfPairParams p) {
+  using G = PairGeom<C>;
+  typedef typename Mfma<T>::frag Frag;
+  constexpr int WM = PSPLIT_WM, NU = PSPLIT_NU, D = PSPLIT_D, BN = 16 * NU, NTHR = 64 * WM;
+  constexpr int RS = G::RS, KS = C / 32, S = K * KS, A2 = (K - 1) / 2, VPR = C / 8;
+  constexpr int NSL = C / (16 * WM);   // channel slices
+  constexpr int SL = 16 * WM;          // channels per slice
+  constexpr int OS = SL * 2 + 16;      // conv2 output staging row stride (bytes)
+  static_assert(C % SL == 0 && NTHR % VPR == 0, "geometry");
+  auto swz = [](int r) { return ((r * G::SW_MUL) >> G::SW_S) & G::SW_M; };
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int ntile = (p.T + BN - 1) / BN;
+  int v = blockIdx.x;
+  const int slice = v % NSL;
+  v /= NSL;
+  const int tile = v % ntile, b = v / ntile;
+  if (b >= p.B) return;
+  const int n0 = tile * BN;
+  const int len = min(p.len[b], p.T);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, lq = lane >> 4;
+  const int mtile = slice * WM + wave;  // this wave's 16-channel M tile
+  const int ch0 = 16 * mtile + 4 * lq;  // the lane's 4 output channels
+  T* Tb = reinterpret_cast<T*>(p.tbuf) + (long long)b * p.T * C;
+  if (!CONV2 && n0 >= len) {
+    // t rows past the utterance are zero (conv2 reads them as padding)
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int row = n0 + 16 * u + l15;
+      if (row < p.T) *reinterpret_cast<uint2*>(Tb + (long long)row * C + ch0) = uint2{0u, 0u};
+    }
+    return;
+  }
+  if (CONV2 && n0 >= len) return;
+  const int d = CONV2 ? 1 : p.d;
+  const int a = A2 * d;               // input rows needed past each side of the tile
+  const int RG = BN + 2 * a;
+  const int gs = n0 - a;              // utterance row of LDS row 0
+  const char* wsrc = reinterpret_cast<const char*>(CONV2 ? p.w2 : p.w1) + (long long)mtile * S * 1024 + lane * 16;
+  const f32x4 bias = *reinterpret_cast<const f32x4*>((CONV2 ? p.b2 : p.b1) + ch0);
+  Frag ring[D][1];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (i < S) ring[i][0] = *reinterpret_cast<const Frag*>(wsrc + (long long)i * 1024);
+
+  // ---- stage the input rows: conv1 g = lrelu(h), conv2 t (zero outside the utterance) ----
+  {
+    const T* src = CONV2 ? Tb : reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
+    const int cc = tid % VPR, r0 = tid / VPR;
+    constexpr int rstep = NTHR / VPR;
+    for (int rb = r0; rb < RG; rb += PAIR_SU * rstep) {
+      uint4 vv[PAIR_SU];
+#pragma unroll
+      for (int i = 0; i < PAIR_SU; ++i) {
+        const int gr = min(max(gs + min(rb + i * rstep, RG - 1), 0), len - 1);
+        vv[i] = *reinterpret_cast<const uint4*>(src + (long long)gr * C + cc * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < PAIR_SU; ++i) {
+        const int r = rb + i * rstep;
+        const int gr = gs + r;
+        const uint4 g = CONV2 ? vv[i] : lrelu_unit<T>(vv[i], p.slope);
+        if (r < RG)
+          *reinterpret_cast<uint4*>(smem + r * RS + (cc ^ swz(r)) * 16) = (gr >= 0 && gr < len) ? g : uint4{0u, 0u, 0u, 0u};
+      }
+    }
+  }
+  __syncthreads();
+
+  f32x4 acc[NU][1];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) acc[u][0] = acc_init(bias);
+  pair_conv<T, C, S, NU, D, 1, false, 16 * RS>(acc, ring, wsrc, smem + l15 * RS, d * RS, d, l15, lq, (NU - 1) * 16 * RS);
+  __builtin_amdgcn_sched_barrier(0);
+
+  if constexpr (!CONV2) {
+    // t = epi_conv1 -> the scratch (zero past the utterance), as mrf_pair_kernel writes T
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int row = n0 + 16 * u + l15;
+      uint2 pk = epi_conv1<T>(acc[u][0], bias, p.slope);
+      if (row >= len) pk = uint2{0u, 0u};
+      if (row < p.T) *reinterpret_cast<uint2*>(Tb + (long long)row * C + ch0) = pk;
+    }
+    return;
+  } else {
+    // conv2 -> T in LDS [BN rows][SL channels], then the row pass of mrf_pair_kernel
+    __syncthreads();  // staged rows no longer read
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+      *reinterpret_cast<uint2*>(smem + (16 * u + l15) * OS + (16 * wave + 4 * lq) * 2) = epi_conv2<T>(acc[u][0], bias);
+    __syncthreads();
+    constexpr int PPR = SL / 8;                         // 16-byte pieces per row of the slice
+    constexpr int NIT = (BN * PPR + NTHR - 1) / NTHR;
+    const T* X = reinterpret_cast<const T*>(p.x) + (long long)b * p.T * C;
+    T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
+    const auto yrsrc = __builtin_amdgcn_make_buffer_rsrc(Y, 0, p.accum ? len * C * (int)sizeof(T) : 0, 0x00020000);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NTHR;
+      const int o = idx / PPR, c8 = idx % PPR;
+      const int gr = n0 + o;
+      if ((BN * PPR % NTHR != 0 && idx >= BN * PPR) || gr >= len) continue;
+      const int e = gr * C + SL * slice + c8 * 8;
+      const uint4 xin = *reinterpret_cast<const uint4*>(X + e);
+      const uint4 sin = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrsrc, e * (int)sizeof(T), 0, 0));
+      const uint4 y = *reinterpret_cast<const uint4*>(smem + o * OS + c8 * 16);
+      uint4 vo = epi_row<T>(y, xin, p.accum, sin, p.scale);
+      if constexpr (OUTACT) vo = lrelu_unit<T>(vo, p.out_slope);
+      store16<TTS_ROW_STORE>(Y, e * (int)sizeof(T), vo);
+    }
+  }
+}
+
+template <typename T, int C, int K>
+static hipError_t launch_pair_split(const MrfPairParams& p, hipStream_t s) {
+  constexpr int BN = 16 * PSPLIT_NU, NSL = C / (16 * PSPLIT_WM);
+  const int blocks = (p.T + BN - 1) / BN * p.B * NSL;
+  const int a1 = (K - 1) / 2 * p.d;
+  const size_t lds1 = (size_t)(BN + 2 * a1) * PairGeom<C>::RS;
+  const size_t lds2 = std::max((size_t)(BN + K - 1) * PairGeom<C>::RS, (size_t)BN * (16 * PSPLIT_WM * 2 + 16));
+  if (lds1 > 160 * 1024 || blocks <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((mrf_pair_split_kernel<T, C, K, false, false>), dim3(blocks), dim3(64 * PSPLIT_WM), lds1, s, p);
+  HIP_RETURN_IF_ERR(hipGetLastError());
+  if (p.out_act)
+    hipLaunchKernelGGL((mrf_pair_split_kernel<T, C, K, true, true>), dim3(blocks), dim3(64 * PSPLIT_WM), lds2, s, p);
+  else
+    hipLaunchKernelGGL((mrf_pair_split_kernel<T, C, K, true, false>), dim3(blocks), dim3(64 * PSPLIT_WM), lds2, s, p);
+  return hipGetLastError();
+}
+
+#ifndef TTS_PAIR_SPLIT_MAXBLK
+#define TTS_PAIR_SPLIT_MAXBLK 256  // full-height blocks below which C >= 128 pairs run channel-split (0: never)
+#endif
+// whether a launch runs the channel-split form: C = 128 / 256 (the weight-heavy stages), a scratch
+// given, and a full-height grid under TTS_PAIR_SPLIT_MAXBLK blocks (TTS_PAIR_SPLIT=0/1 forces it
+// off / on wherever possible: tests)
+#ifndef TTS_PAIR_SPLIT_CMIN
+#define TTS_PAIR_SPLIT_CMIN 256  // C = 128 measured slower split (C5 trace: k = 3 / 7 / 11 pairs 12 / 18 / 24 -> 17 / 22 / 27 us)
+#endif
+static bool pair_split(int C, const MrfPairParams& p) {
+  if (C < 128 || C < TTS_PAIR_SPLIT_CMIN || !p.tbuf || p.post_wpk) return false;
+  const int force = sw(SW_PAIR_SPLIT);
+  if (force >= 0) return force != 0;
+  const int bn = C == 128 ? PairGeom<128>::BN : PairGeom<256>::BN;
+  return (long long)((p.T + bn - 1) / bn) * p.B < TTS_PAIR_SPLIT_MAXBLK;
+}
+
 // output activation compiled for the stage-final pairs of HiFi-GAN V1 (k = 11 at C = 64 .. 256)
 template <int C, int K>
 constexpr bool pair_outact_compiled() { return K == 11 && (C == 64 || C == 128 || C == 256); }
@@ -491,6 +671,8 @@ static hipError_t launch_pair_g(const MrfPairParams& p, hipStream_t s) {
 
 template <typename T, int C, int K, bool POST = false>
 static hipError_t launch_pair_t(const MrfPairParams& p, hipStream_t s) {
+  if constexpr (!POST && C >= 128)
+    if (pair_split(C, p)) return launch_pair_split<T, C, K>(p, s);
   if constexpr (!POST)
     if (pair_div(C, p, POST) != 1) return launch_pair_g<T, C, K, POST, TTS_PAIR_SHORT_DIV>(p, s);
   return launch_pair_g<T, C, K, POST, 1>(p, s);

@@ -225,6 +225,7 @@ def test_short_pair_tiles_bit_identical(vw, dtype, switch):
     mel = torch.from_numpy(rng.standard_normal((5, 71, 80)).astype(np.float32)).to(DEV)
     ln = torch.tensor(lens, dtype=torch.int32)
     switch("TTS_MRF_CHAIN", 0)     # every resblock as pair launches
+    switch("TTS_PAIR_SPLIT", 0)    # (the channel-split form has its own test below)
     switch("TTS_PAIR_DIV", 0)
     short = eng.vocoder(mel, ln).cpu().numpy()
     switch("TTS_PAIR_DIV", 1)
@@ -237,6 +238,37 @@ def test_short_pair_tiles_bit_identical(vw, dtype, switch):
         assert np.array_equal(short[b], full[b]), (b, float(np.abs(short[b] - full[b]).max()))
         assert np.array_equal(auto[b], default_full[b]), b
         assert np.all(short[b, L * 256:] == 0)
+
+
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_channel_split_pairs_bit_identical(vw, dtype, switch):
+    """The channel-split pair form (two launches per pair over (row tile, 64-channel slice)
+    blocks, t rows through the T1 scratch; picked for small C >= 128 grids such as the streamed
+    vocoder's first chunk) reproduces mrf_pair_kernel bit for bit: forced on and off, ragged and
+    empty utterances, tile edges, the stage-final pairs with the stored LeakyReLU included; the
+    automatic choice agrees, and the zero tail past each utterance stays zero."""
+    eng = engine_for(dtype, vw)
+    rng = np.random.default_rng(25)
+    lens = [71, 1, 0, 33, 64, 8]
+    mel = torch.from_numpy(rng.standard_normal((6, 71, 80)).astype(np.float32)).to(DEV)
+    ln = torch.tensor(lens, dtype=torch.int32)
+    switch("TTS_MRF_CHAIN", 0)     # every resblock as pair launches
+    outs = {}
+    for sp, div in ((0, 1), (1, 1), (None, 1), (0, None), (1, None), (None, None)):
+        switch("TTS_PAIR_SPLIT", sp)
+        switch("TTS_PAIR_DIV", div)
+        outs[(sp, div)] = eng.vocoder(mel, ln).cpu().numpy()
+    switch("TTS_MRF_CHAIN", None)
+    switch("TTS_PAIR_SPLIT", 1)
+    chain_split = eng.vocoder(mel, ln).cpu().numpy()
+    switch("TTS_PAIR_SPLIT", 0)
+    chain_full = eng.vocoder(mel, ln).cpu().numpy()
+    ref = outs[(0, 1)]
+    for k, o in outs.items():
+        for b, L in enumerate(lens):
+            assert np.array_equal(o[b], ref[b]), (k, b, float(np.abs(o[b] - ref[b]).max()))
+            assert np.all(o[b, L * 256:] == 0), (k, b)
+    assert np.array_equal(chain_split, chain_full)
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])

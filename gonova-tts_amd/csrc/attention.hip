@@ -36,8 +36,11 @@
 // model with encoder_precision "fast"), rel_attn_split_kernel (fp32 stacks of a 16-bit model:
 // the exact-duration encoder, each product as three f16 MFMAs) and rel_attn_f32_kernel (fp32
 // models, v_mfma_f32_16x16x4_f32).
+#include <type_traits>
+
 #include "acoustic_kernels.h"
 #include "common.h"
+#include "ln_rows.h"
 #include "mrf_tile.h"
 #include "switches.h"
 
@@ -233,7 +236,8 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
   unsigned ra = rslot(i0w - kbeg - (AT_BK - 1) + q) * KR + 16 * g;
   const int vta = at_tr_addr(KR, g, q);  // this lane's transposed-read address in the V rows (tile 0)
 
-  for (int j0 = kbeg; j0 < kbeg + khalf; j0 += AT_BK) {
+  // one 32-key step; MASK: a step with keys past the group's end
+  auto key_step = [&](const int j0, auto MASK) __attribute__((always_inline)) {
     load_kv(j0 + AT_BK);  // in flight during this step's MFMAs (the last step's are written, unused)
     load_r(j0 + AT_BK);
     __builtin_amdgcn_sched_barrier(0);
@@ -277,7 +281,7 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
         sv[4 * kt + e] = (sacc[kt][e] + bd) * sl2;
       }
     __builtin_amdgcn_wave_barrier();
-    if (j0 + AT_BK > kend) {  // wave-uniform: only a group's last step has keys past its end
+    if constexpr (decltype(MASK)::value) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -300,15 +304,21 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
       pe0[e] = at_exp2(sv[e] - m_ref);
       pe1[e] = at_exp2(sv[4 + e] - m_ref);
     }
-    // normalise with the rounded probabilities P.V uses (keys in the order e = 0 .. 7)
+    // normalise with the rounded probabilities P.V uses (keys in the order e = 0 .. 7), read back
+    // from the packed P fragment (the same round-to-nearest conversion, done once)
+    uint4 pk = pack8<T>(pe0, pe1);
+    // (keeps the unpack below on these bits: else the compiler converts each value again)
+    asm volatile("" : "+v"(pk.x), "+v"(pk.y), "+v"(pk.z), "+v"(pk.w));
+    const Frag bp = __builtin_bit_cast(Frag, pk);
+    {
+      float pr[8];
+      ln_unpack8<T>(pk, pr);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) lsum += (float)(T)pe0[e];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) lsum += (float)(T)pe1[e];
+      for (int e = 0; e < 8; ++e) lsum += pr[e];
+    }
     lsum = at_xor32_sum(at_xor16_sum(lsum));
     l_run = l_run * alpha + lsum;
     m_run = m_new;
-    const Frag bp = __builtin_bit_cast(Frag, pack8<T>(pe0, pe1));
     // O^T += Vt . P^T with the permuted key order of bp: the Vt fragment by transposed reads
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
@@ -321,7 +331,14 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
     write_kv();
     write_r();
     __syncthreads();
-  }
+  };
+  // steps whose 32 keys all lie before the group's end run without the per-key compares; the
+  // rest (KH = 1: at most the last; KH = 2: the second group of a short utterance may have several
+  // past its end) with them
+  const int nsteps = (khalf + AT_BK - 1) / AT_BK;  // (KH = 1: khalf = len)
+  const int nfull = min(nsteps, max(0, (kend - kbeg) / AT_BK));
+  for (int st = 0; st < nfull; ++st) key_step(kbeg + st * AT_BK, std::false_type{});
+  for (int st = nfull; st < nsteps; ++st) key_step(kbeg + st * AT_BK, std::true_type{});
   if constexpr (KH > 1) {
     // merge the two key groups: group 1 leaves (m, l, O^T) in LDS, group 0 rescales both
     constexpr int MS = 2 + 4 * DT + 2;  // floats per lane (padded)
@@ -702,6 +719,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
   unsigned ra = rslot(i0w - (AT_BK - 1) + q) * KR + 16 * g;  // this lane's R rows (slot of m + 16 t) and column
   const int vta = at_tr_addr(KR, g, q);  // this lane's transposed-read address in the V planes (tile 0)
 
+  // (the last-step peel of rel_attn_kernel pushed this kernel past 256 VGPRs: kept as one loop)
   for (int j0 = 0; j0 < len; j0 += AT_BK) {
     load_kv(j0 + AT_BK);
     load_r(j0 + AT_BK);

@@ -90,6 +90,16 @@ __device__ inline uint2 at_tr16(const char* p) {
 constexpr int AT_BQ = 64;   // queries per block
 constexpr int AT_BK = 32;   // keys per step
 constexpr int AT_RW = AT_BQ + AT_BK;  // R window rows per block (95 used)
+// Lazy online-softmax rescale (16-bit kernel): a row's reference max moves only when a step's
+// max exceeds it by more than AT_LAZY (log2 units), so P = 2^(s - m) stays <= 2^AT_LAZY (f16 /
+// bf16 hold it exactly as well as any P <= 1: same relative precision) and the O^T rescale of
+// DT tiles is skipped on every step where no row of the wave moved -- after the first steps,
+// nearly all.  0: eager (a row moves whenever its max grows; the skipped multiplies are by
+// exactly 1, so the result equals the eager form's bits).
+#ifndef TTS_ATTN_LAZY
+#define TTS_ATTN_LAZY 8
+#endif
+constexpr float AT_LAZY = TTS_ATTN_LAZY;
 
 // KH = 2: 8 waves, the block's keys split into two groups of whole 32-key steps, one per 4
 // waves (each group with its own K / Vt / R staging), merged through LDS at the end -- twice
@@ -292,11 +302,16 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
 #pragma unroll
     for (int e = 0; e < 8; ++e) mloc = fmaxf(mloc, sv[e]);
     mloc = at_xor32_max(at_xor16_max(mloc));
-    const float m_new = fmaxf(m_run, mloc);
+    // (m_run = -inf: -inf + AT_LAZY = -inf, so the first step with a key moves the row)
+    const bool grow = mloc > m_run + AT_LAZY;
+    const float m_new = grow ? mloc : m_run;
     // a step with every key masked (the second key group of a short utterance) keeps m = -inf:
     // exponents are then taken against 0, so alpha and P stay 0 instead of NaN
     const float m_ref = KH > 1 && m_new == -INFINITY ? 0.f : m_new;
     const float alpha = at_exp2(m_run - m_ref);  // m_run = -inf on the first step: alpha = 0
+    // alpha is exactly 1 for a row that did not move (or 0 with O^T and l still 0): the rescale
+    // runs only when some row of the wave moved
+    const bool rescale = __builtin_amdgcn_ballot_w64(grow) != 0;
     float lsum = 0.f;
     f32x4 pe0, pe1;
 #pragma unroll
@@ -319,13 +334,17 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
     lsum = at_xor32_sum(at_xor16_sum(lsum));
     l_run = l_run * alpha + lsum;
     m_run = m_new;
+    if (rescale) {
+#pragma unroll
+      for (int t = 0; t < DT; ++t) oacc[t] *= alpha;
+    }
     // O^T += Vt . P^T with the permuted key order of bp: the Vt fragment by transposed reads
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
       const uint2 lo = at_tr16(Vs + vta + t * 32);
       const uint2 hi = at_tr16(Vs + vta + 16 * KR + t * 32);
       const uint4 av = uint4{lo.x, lo.y, hi.x, hi.y};
-      oacc[t] = MF::mma(*reinterpret_cast<const Frag*>(&av), bp, oacc[t] * alpha);
+      oacc[t] = MF::mma(*reinterpret_cast<const Frag*>(&av), bp, oacc[t]);
     }
     __syncthreads();  // every wave is done with this step's K / Vt and the leaving R rows
     write_kv();
@@ -784,8 +803,17 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
 #pragma unroll
     for (int e = 0; e < 8; ++e) mloc = fmaxf(mloc, sv[e]);
     mloc = at_xor32_max(at_xor16_max(mloc));
-    const float m_new = fmaxf(m_run, mloc);
+    // lazy rescale as in rel_attn_kernel (P <= 2^AT_LAZY: its hi / lo planes keep their range)
+    const bool grow = mloc > m_run + AT_LAZY;
+    const float m_new = grow ? mloc : m_run;
     const float alpha = at_exp2(m_run - m_new);
+    if (__builtin_amdgcn_ballot_w64(grow) != 0) {
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        oacc[t] *= alpha;
+        oaccx[t] *= alpha;
+      }
+    }
     f32x4 pe0, pe1;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -809,8 +837,8 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
       const uint2 l0 = at_tr16(vr + KPL), l1 = at_tr16(vr + KPL + 16 * KR);
       const Frag ah = __builtin_bit_cast(Frag, uint4{h0.x, h0.y, h1.x, h1.y});
       const Frag al = __builtin_bit_cast(Frag, uint4{l0.x, l0.y, l1.x, l1.y});
-      oacc[t] = MF::mma(ah, bp, oacc[t] * alpha);
-      f32x4 ox = MF::mma(ah, bpl, oaccx[t] * alpha);
+      oacc[t] = MF::mma(ah, bp, oacc[t]);
+      f32x4 ox = MF::mma(ah, bpl, oaccx[t]);
       oaccx[t] = MF::mma(al, bp, ox);
     }
     __syncthreads();

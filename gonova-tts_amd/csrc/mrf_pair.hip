@@ -139,8 +139,17 @@ constexpr int pair_bn() {
 #ifndef TTS_PAIR_SHORT_D256
 #define TTS_PAIR_SHORT_D256 4  // weight-ring depth (k-steps) of the C = 256 short tiles (full height: 2)
 #endif
+// A/B builds only: the row pass's residual rows loaded into registers right after the input tile
+// is staged (L2-hot then) and held through both convs, instead of re-read at the end (where they
+// have left the 4 MB L2: the 1.48x FETCH of profiles/r05z_pmc_traffic_c2.json).  The registers
+// cost the third block per CU (OCC 2); C = 256 (already two blocks, 254 VGPRs) and conv_post
+// keep the re-read.  Measured in profiles/r05o_ab_resreg.txt.
+#ifndef TTS_PAIR_RESREG
+#define TTS_PAIR_RESREG 0
+#endif
 template <int C, int DIV, int K = 0, bool POST = false>
 struct PairGeomS : PairGeom<C> {
+  static constexpr bool RESREG = TTS_PAIR_RESREG && C <= 128 && !POST;
   static constexpr int BN = DIV == 1 && K > 0 && !POST ? pair_bn<C, K>() : PairGeom<C>::BN / DIV;
   // short tiles do few MFMAs per k-step (one row tile per wave), so the weight ring's L2 round
   // trips are exposed unless it runs further ahead; the depth only moves loads earlier (same
@@ -151,7 +160,8 @@ struct PairGeomS : PairGeom<C> {
                                                              : PairGeom<C>::D;
   // blocks per CU the register budget is sized for (the C = 32 k = 11 pairs without conv_post
   // may take a fourth: TTS_P32K11_OCC; the HiFi-GAN V3 C = 64 k = 5 pair spills at three)
-  static constexpr int OCC = C == 32 && K == 11 && !POST && DIV == 1 ? TTS_P32K11_OCC
+  static constexpr int OCC = RESREG                                  ? 2
+                             : C == 32 && K == 11 && !POST && DIV == 1 ? TTS_P32K11_OCC
                              : C == 64 && K == 5                    ? 2
                                                                     : PairGeom<C>::OCC;
 };
@@ -289,6 +299,16 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   __syncthreads();
   TTS_PSTAMP(1);
 
+  constexpr int NIT = (BO * VPR + NTHR - 1) / NTHR;  // 16-byte row pieces per thread in the row pass
+  uint4 xin[NIT];  // the row pass's residual pieces (load_rows)
+  if constexpr (G::RESREG) {  // L2-hot: the block just staged these rows
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NTHR;
+      xin[it] = *reinterpret_cast<const uint4*>(X + min(max(n0 - PO + idx / VPR, 0), len - 1) * C + (idx % VPR) * 8);
+    }
+  }
+
   // ---- conv1 over T rows [0, 16*NT1): T row t <-> global row n0 - PO - a2 + t ----
   // Tiles are dealt round-robin to the WN waves of an M slice; a wave whose share is one
   // short repeats the block's last tile (straight-line loop, result not stored).
@@ -336,8 +356,6 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   __syncthreads();
   TTS_PSTAMP(3);
 
-  constexpr int NIT = (BO * VPR + NTHR - 1) / NTHR;  // 16-byte row pieces per thread in the row pass
-
   // ---- conv2 over the BN output rows: output row o reads T rows o .. o + 2*a2 ----
   f32x4 acc2[NU2][MT];
 #pragma unroll
@@ -354,7 +372,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   // pass) and fetches nothing.
   T* Y = reinterpret_cast<T*>(p.y) + (long long)b * p.T * C;
   const auto yrsrc = __builtin_amdgcn_make_buffer_rsrc(Y, 0, p.accum ? len * C * (int)sizeof(T) : 0, 0x00020000);
-  uint4 xin[NIT], sin[NIT];
+  uint4 sin[NIT];
   auto load_rows = [&](bool lx, bool ls) __attribute__((always_inline)) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
@@ -366,7 +384,7 @@ __global__ __launch_bounds__((64 * PairGeom<C>::WM * PairGeom<C>::WN), (PairGeom
   };
   // with conv_post fused the residual rows wait until the accumulators are staged (registers)
   const f32x4 (&bias)[MT] = bias2;
-  load_rows(!POST, true);
+  load_rows(!POST && !G::RESREG, true);
   __builtin_amdgcn_sched_barrier(0);
   __syncthreads();  // T no longer read
   {

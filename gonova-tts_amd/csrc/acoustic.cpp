@@ -423,7 +423,7 @@ struct AcousticModel::Impl {
         // fused flash-style relative-position attention (attention.hip); Qu / Qv formed in it,
         // V read from the QKV rows (transposed in LDS: no Vt launch)
         // fp32 layers of a 16-bit model (the exact-duration encoder) in split precision, like their GEMMs
-        const bool split = dt == DT_F32 && this->dt != DT_F32 && sw(SW_ATTN_SPLIT) != 0 && !enc_f32;
+        const bool split = dt == DT_F32 && this->dt != DT_F32 && !enc_f32;
         prof_launch(PK_ATTN, 6.0 * D * (double)B * Tm * Tm, s, [&] { return launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, L.ptab, lens, B, Tm, Tp, D, H, rmax, scale,
                                   O, s, range_flag); });
         run_ln(L.out, O, Tp, lens, Y, Tp, B, dt, s, 1.f, Xb, Xb, L.ln_att, nullptr);

@@ -904,7 +904,6 @@ static int xres_group(const ConvParams& p, int BN, int lds_max = XRES_LDS_MAX) {
   return 0;
 }
 
-static int xres_mode() { return sw(SW_CONV_XRES) != 0; }  // TTS_CONV_XRES=0 disables the X-resident kernel
 
 // 128-channel blocks (4 x 1 waves, BN = 128) for M >= 128; 64-channel blocks (2 x 2 waves,
 // BN = 256) for M = 64 (the last upsampler)
@@ -998,7 +997,6 @@ static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s, boo
 
 template <typename T>
 static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err, bool* ln_done) {
-  if (!xres_mode()) return false;
   const int wm = xres_wm(p);
   const int nt = xres_nt(p, wm);
   // channel group sized for 128-row tiles whatever the tile height: the group fixes the K
@@ -1105,7 +1103,7 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why) {
 int conv_gemm_kind(int dtype, const ConvParams& p) {
   if (dtype == DT_F32) return conv_split_eligible(p) ? PK_CONV_SPLIT : PK_CONV_GEMM;
   if (conv_mt_eligible(dtype, p)) return PK_CONV_MT;
-  return (dtype != DT_F32 && xres_mode() && xres_group(p, 32 * 4 * (4 / xres_wm(p)))) ? PK_CONV_XRES : PK_CONV_GEMM;
+  return (dtype != DT_F32 && xres_group(p, 32 * 4 * (4 / xres_wm(p)))) ? PK_CONV_XRES : PK_CONV_GEMM;
 }
 
 static hipError_t conv_gemm_launch_noln(int dtype, const ConvParams& p, hipStream_t s, bool* ln_done) {

@@ -890,10 +890,8 @@ bool conv_split_eligible(const ConvParams& p) {
 
 // Per-utterance form (callers without the packed-row promise): 128 channels x 64 rows of one
 // utterance (NT = 2) when that grid fills the chip 4x over, else 32 rows (more blocks, a 160-row
-// cover of 144 rows instead of 192).  TTS_SPLIT_TILE=1/2 forces one; the K order is the same.
+// cover of 144 rows instead of 192); the K order is the same.
 static int split_tile(const ConvParams& p) {
-  const int force = sw(SW_SPLIT_TILE);
-  if (force == 1 || force == 2) return force;
   const long long blocks2 = (long long)((p.y_rows + 63) / 64) * ((p.M + 127) / 128) * p.B;
   return blocks2 >= 4 * 256 ? 2 : 1;
 }

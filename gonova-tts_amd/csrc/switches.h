@@ -12,12 +12,9 @@ enum Sw : int {
   SW_MRF_CHAIN,    // TTS_MRF_CHAIN=0/1: resblock chain kernel off / on
   SW_POST_FUSE,    // TTS_POST_FUSE=0: conv_post as its own launch
   SW_UP_STREAM,    // TTS_UP_STREAM=0: stages 2-3 upsamplers on conv_xres
-  SW_CONV_XRES,    // TTS_CONV_XRES=0: no X-resident conv kernel
   SW_XRES_NARROW,  // TTS_XRES_NARROW=0/1: force conv_xres narrow tiles off / on
   SW_XRES_NT,      // TTS_XRES_NT=2/4: force conv_xres tile height
-  SW_SPLIT_TILE,   // TTS_SPLIT_TILE=1/2: force the per-utterance split GEMM tile
   SW_PAIR_DIV,     // TTS_PAIR_DIV=1: full-height pair tiles; any other value: short tiles
-  SW_ATTN_SPLIT,   // TTS_ATTN_SPLIT=0: the exact encoder's fused attention on f32 MFMA, not split
   SW_ATTN_KSPLIT,  // TTS_ATTN_KSPLIT=1: 16-bit attention with two key groups per block (8 waves)
   SW_SPLIT_WHOLE,  // TTS_SPLIT_WHOLE=0: small split-precision GEMMs stage one channel group at a time
   SW_XRES_DMA,     // TTS_XRES_DMA=0: FFN convs / upsamplers register-staged with round-2 channel groups; 2: register-staged, same bits

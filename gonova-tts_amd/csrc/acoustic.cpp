@@ -24,6 +24,10 @@
 #include "runtime.h"
 #include "switches.h"
 
+#ifndef TTS_DEC_TRIM_RATIO
+#define TTS_DEC_TRIM_RATIO 8  // frames per token above which a predicted-duration forward trims the decoder extent
+#endif
+
 namespace tts {
 
 namespace {
@@ -489,7 +493,7 @@ struct AcousticModel::Impl {
     }
     if (Tm > rmax) build_ptabs(rup(Tm, 256), s);
     const float xscale = std::sqrt((float)D);
-    const int Np = enc_rows(N), Tp = rup(Tcap, 32);
+    const int Np = enc_rows(N);
     // encoder
     elem(s, [&] { return launch_embed(dte, tokens, tok_lens, B, N, Np, embed, V, D, xscale, ENC, s); });
     cur_rpad = Np - N;  // encoder side: packed-row split GEMMs
@@ -520,36 +524,47 @@ struct AcousticModel::Impl {
     int* dur = durations ? durations : i_dur;
     elem(s, [&] { return launch_durations_strided(s, B, N, Np, tok_lens, dur_override, Tcap, dur, mel_lens); });
     elem(s, [&] { return launch_var_embed_add(dte, ENC, B * Np, D, f_energy, ee_w, ee_b, f_pitch, pe_w, pe_b, s); });
-    // decoder rows are laid out with stride Tp; regulate writes [B][Tcap] rows
-    void* Xd = X;
-    if (Tp == Tcap) {
-      elem(s, [&] { return launch_regulate(dte, dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, X, s); });
-    } else {
-      elem(s, [&] { return launch_regulate(dte, dt, ENC, B, Np, D, i_tokmap, Tcap, xscale, Y, s); });
-      HIP_CHECK(hipMemcpy2DAsync(X, (size_t)Tp * D * dtype_size(dt), Y, (size_t)Tcap * D * dtype_size(dt),
-                                 (size_t)Tcap * D * dtype_size(dt), B, hipMemcpyDeviceToDevice, s));
+    // Decoder extent.  With predicted durations the caller's Tcap is a frame budget (model.py: 12
+    // frames per token, retried exactly if exceeded), typically twice the frames the durations
+    // give; the decoder then runs at the longest utterance's frame count, read back here (one
+    // stream sync, after the variance adaptor is enqueued).  Run at Tcap, every grid doubled with
+    // blocks that exit at once: the tile-height and LayerNorm-placement rules saw twice the rows,
+    // and a launch whose blocks all fit at once (attention) put two real blocks on some CUs and
+    // none on others -- batch-8 acoustic pass 2,061 us at 6 N vs 2,155 us at 12 N
+    // (profiles/r05q_tcap_trace.txt).  The read costs ~20-40 us of idle device, so it is made
+    // only for a loose budget (Tcap > TTS_DEC_TRIM_RATIO frames per token; a caller passing the
+    // frames it expects gets no sync).  A row's result does not depend on the extent
+    // (tests/test_acoustic_gpu.py).  TTS_DEC_TRIM=0: never; 1: whatever the budget (tests).
+    int Td = Tcap;
+    const int trim = sw(SW_DEC_TRIM);
+    if (!dur_override && B > 0 && (trim == 1 || (trim < 0 && Tcap > TTS_DEC_TRIM_RATIO * N))) {
+      std::vector<int> lens_h((size_t)B);
+      HIP_CHECK(hipMemcpyAsync(lens_h.data(), mel_lens, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      int mx = 1;
+      for (int v : lens_h) mx = std::max(mx, v);
+      Td = std::min(Tcap, mx);
     }
-    stack(dec, Xd, mel_lens, B, Tcap, Tp, s);
+    const int Tpd = rup(Td, 32);  // decoder row stride
+    // regulate writes the Td frames of each utterance at row stride Tpd (frames past an
+    // utterance's length are zero rows)
+    void* Xd = X;
+    elem(s, [&] { return launch_regulate(dte, dt, ENC, B, Np, D, i_tokmap, Tcap, Td, Tpd, xscale, X, s); });
+    stack(dec, Xd, mel_lens, B, Td, Tpd, s);
     // postnet (HF:238-244), BatchNorm folded
-    run(feat_out, Xd, Tp, mel_lens, BEF, Tp, B, dt, s, prof);
+    run(feat_out, Xd, Tpd, mel_lens, BEF, Tpd, B, dt, s, prof);
     const void* h = BEF;
     void* bufs[2] = {PN1, PN2};
     const int n = (int)postnet.size();
     for (int i = 0; i < n; ++i) {
       const bool last = i == n - 1;
       void* o = last ? MELT : bufs[i & 1];
-      run(postnet[i], h, Tp, mel_lens, o, Tp, B, dt, s, prof, 1.f, last ? ACT_NONE : ACT_TANH, 1.f,
+      run(postnet[i], h, Tpd, mel_lens, o, Tpd, B, dt, s, prof, 1.f, last ? ACT_NONE : ACT_TANH, 1.f,
                 last ? BEF : nullptr);
       h = o;
     }
-    // MELT rows have stride Tp; output [B][Tcap][80] float32
-    if (Tp == Tcap) {
-      elem(s, [&] { return launch_mel_out(dt, MELT, mel_lens, B, Tcap, NMEL, mel, s); });
-    } else {
-      HIP_CHECK(hipMemcpy2DAsync(BEF, (size_t)Tcap * NMEL * dtype_size(dt), MELT, (size_t)Tp * NMEL * dtype_size(dt),
-                                 (size_t)Tcap * NMEL * dtype_size(dt), B, hipMemcpyDeviceToDevice, s));
-      elem(s, [&] { return launch_mel_out(dt, BEF, mel_lens, B, Tcap, NMEL, mel, s); });
-    }
+    // MELT rows have stride Tpd; output [B][Tcap][80] float32 (rows past mel_len zero)
+    elem(s, [&] { return launch_mel_out(dt, MELT, mel_lens, B, Tpd, Tcap, NMEL, mel, s); });
   }
 
   hipError_t launch_durations_strided(hipStream_t s, int B, int N, int Np, const int* tok_lens, const int* ovr,

@@ -22,10 +22,12 @@ hipError_t launch_durations(const float* logd, const int* lens, int B, int N, co
                             int Tcap, int* dur, int* mel_lens, int* tokmap, hipStream_t s);
 hipError_t launch_var_embed_add(int dt, void* x, int rows, int D, const float* e, const float* we, const float* be,
                                 const float* p, const float* wp, const float* bp, hipStream_t s);
-// enc in dt_in (dt or fp32), out in dt
+// enc in dt_in (dt or fp32), out in dt: frames <= Tcap rows per utterance (tokmap row stride Tcap)
+// written at row stride Tout
 hipError_t launch_regulate(int dt_in, int dt, const void* enc, int B, int N, int D, const int* tokmap, int Tcap,
-                           float scale, void* out, hipStream_t s);
-hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, int Tcap, int C, float* out,
+                           int frames, int Tout, float scale, void* out, hipStream_t s);
+// in: row stride Tin; out: float32 [B][Tcap][C]
+hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, int Tin, int Tcap, int C, float* out,
                           hipStream_t s);
 
 hipError_t launch_spk_bias(int dt, const float* e, int B, int E, const float* We, const float* bias, int D, void* out,

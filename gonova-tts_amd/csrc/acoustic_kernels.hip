@@ -429,11 +429,11 @@ __global__ void var_embed_add_kernel(T* __restrict__ x, int rows, int D, const f
 // side may be fp32 (TTS_ENCODER_EXACT) while the decoder runs 16-bit: one rounding, after the scale
 template <typename T, typename TI = T>
 __global__ void regulate_kernel(const TI* __restrict__ enc, int N, int D, const int* __restrict__ tokmap, int Tcap,
-                                float scale, T* __restrict__ out) {
+                                int Tout, float scale, T* __restrict__ out) {
   const int b = blockIdx.y;
   const int f = blockIdx.x;
   const int tok = tokmap[(long long)b * Tcap + f];
-  T* o = out + ((long long)b * Tcap + f) * D;
+  T* o = out + ((long long)b * Tout + f) * D;
   if (tok < 0) {
     for (int c = threadIdx.x; c < D; c += blockDim.x) o[c] = from_f32<T>(0.f);
     return;
@@ -442,16 +442,16 @@ __global__ void regulate_kernel(const TI* __restrict__ enc, int N, int D, const 
   for (int c = threadIdx.x; c < D; c += blockDim.x) o[c] = from_f32<T>(to_f32(s[c]) * scale);
 }
 
-// mel [B][Tcap][C] (T) -> float32 [B][Tcap][C], rows >= mel_len zeroed
+// mel [B][Tin][C] (T, row stride Tin >= mel_len) -> float32 [B][Tcap][C], rows >= mel_len zeroed
 template <typename T>
-__global__ void mel_out_kernel(const T* __restrict__ in, const int* __restrict__ mel_lens, int Tcap, int C,
+__global__ void mel_out_kernel(const T* __restrict__ in, const int* __restrict__ mel_lens, int Tin, int Tcap, int C,
                                float* __restrict__ out) {
   const int b = blockIdx.y;
   const long long n = (long long)Tcap * C;
   const int L = mel_lens[b];
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const int t = (int)(i / C);
-    out[(long long)b * n + i] = t < L ? to_f32(in[(long long)b * n + i]) : 0.f;
+    out[(long long)b * n + i] = t < L ? to_f32(in[(long long)b * Tin * C + i]) : 0.f;
   }
 }
 
@@ -624,21 +624,22 @@ hipError_t launch_var_embed_add(int dt, void* x, int rows, int D, const float* e
 }
 
 hipError_t launch_regulate(int dt_in, int dt, const void* enc, int B, int N, int D, const int* tokmap, int Tcap,
-                           float scale, void* out, hipStream_t s) {
+                           int frames, int Tout, float scale, void* out, hipStream_t s) {
+  if (frames > Tcap || frames > Tout) return hipErrorInvalidValue;
   if (dt_in == DT_F32 && dt != DT_F32) {
-    TTS_DISPATCH(dt, hipLaunchKernelGGL((regulate_kernel<TT, float>), dim3(Tcap, B), dim3(128), 0, s,
-                                        (const float*)enc, N, D, tokmap, Tcap, scale, (TT*)out));
+    TTS_DISPATCH(dt, hipLaunchKernelGGL((regulate_kernel<TT, float>), dim3(frames, B), dim3(128), 0, s,
+                                        (const float*)enc, N, D, tokmap, Tcap, Tout, scale, (TT*)out));
   }
   if (dt_in != dt) return hipErrorInvalidValue;
-  TTS_DISPATCH(dt, hipLaunchKernelGGL(regulate_kernel<TT>, dim3(Tcap, B), dim3(128), 0, s, (const TT*)enc, N, D,
-                                      tokmap, Tcap, scale, (TT*)out));
+  TTS_DISPATCH(dt, hipLaunchKernelGGL(regulate_kernel<TT>, dim3(frames, B), dim3(128), 0, s, (const TT*)enc, N, D,
+                                      tokmap, Tcap, Tout, scale, (TT*)out));
 }
 
-hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, int Tcap, int C, float* out,
+hipError_t launch_mel_out(int dt, const void* in, const int* mel_lens, int B, int Tin, int Tcap, int C, float* out,
                           hipStream_t s) {
   dim3 grid(grid1((long long)Tcap * C), B);
-  TTS_DISPATCH(dt, hipLaunchKernelGGL(mel_out_kernel<TT>, grid, dim3(256), 0, s, (const TT*)in, mel_lens, Tcap, C,
-                                      out));
+  TTS_DISPATCH(dt, hipLaunchKernelGGL(mel_out_kernel<TT>, grid, dim3(256), 0, s, (const TT*)in, mel_lens, Tin, Tcap,
+                                      C, out));
 }
 
 // range word read-out (tts_acoustic_range_flag): copy the word to the caller's device buffer and

@@ -135,7 +135,11 @@ int tts_vocoder_forward_chunk(tts_engine* eng, const float* d_mel, const int32_t
  *                  the duration predictor is not run and d_durations returns these counts)
  *   d_mel         [B][Tcap][80] float32 output, d_mel_lens [B] int32 output
  *   d_durations   optional [B][N] int32 output of the durations actually used
- * Frames past Tcap are dropped (d_mel_lens is clamped to Tcap). */
+ * Frames past Tcap are dropped (d_mel_lens is clamped to Tcap).  With predicted durations and a
+ * loose budget (Tcap > 8 N) the call reads the frame counts back once after the variance adaptor
+ * (the calling thread waits for the encoder on `stream`) and runs the decoder at the longest
+ * utterance's count instead of Tcap; the output is the same (TTS_DEC_TRIM=0: never, 1: at any
+ * budget).  Otherwise, and with d_dur_override, the call stays fully asynchronous. */
 int tts_acoustic_forward(tts_engine* eng, const int32_t* d_tokens, const int32_t* d_tok_lens,
                          int B, int N, const int32_t* d_dur_override, float* d_mel,
                          int32_t* d_mel_lens, int Tcap, int32_t* d_durations, void* stream);
@@ -176,7 +180,7 @@ int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, doubl
 /* Process-wide switch selecting an alternative kernel path (A/B runs, the parity tests'
  * reference paths): TTS_REL_ATTN, TTS_MRF_FUSED, TTS_MRF_CHAIN, TTS_POST_FUSE, TTS_UP_STREAM,
  * TTS_XRES_NARROW, TTS_XRES_NT, TTS_PAIR_DIV, TTS_ATTN_KSPLIT, TTS_SPLIT_WHOLE, TTS_XRES_DMA,
- * TTS_LN_FUSE, TTS_SPLIT_NT1, TTS_XRES_ORDER, TTS_CONV_MT, TTS_MT_TILE, TTS_PAIR_SPLIT.  Each
+ * TTS_LN_FUSE, TTS_SPLIT_NT1, TTS_XRES_ORDER, TTS_CONV_MT, TTS_MT_TILE, TTS_PAIR_SPLIT, TTS_DEC_TRIM.  Each
  * starts from its environment variable, read once; value -1 restores the built-in default.
  * Applies to launches enqueued after the call (use from one thread while no forward runs). */
 int tts_set_switch(const char* name, int value);

@@ -557,6 +557,29 @@ def test_predicted_durations_bf16_mel_matches_oracle(aw):
         assert np.all(mel[b, L:] == 0)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_decoder_extent_trim_bit_identical(aw, dtype, switch):
+    """With predicted durations the decoder runs at the longest utterance's frame count, read back
+    after the variance adaptor, not at the caller's budget t_cap (acoustic.cpp forward,
+    TTS_DEC_TRIM): the same mel, lengths and durations bit for bit as the decoder at t_cap, for
+    a ragged batch at three budgets (12, 7 frames per token, and one that cuts the longest
+    utterance short), with the output zero past each length."""
+    eng = engine(dtype, aw)
+    rng = np.random.default_rng(41)
+    ids_list = [rng.integers(1, 78, size=n) for n in (60, 1, 33, 47, 12)]
+    for t_cap in (12 * 60, 7 * 60, 200):
+        switch("TTS_DEC_TRIM", 0)
+        m0, l0, d0 = run(eng, ids_list, t_cap=t_cap)
+        switch("TTS_DEC_TRIM", 1)
+        m1, l1, d1 = run(eng, ids_list, t_cap=t_cap)
+        assert m1.shape == m0.shape == (len(ids_list), t_cap, 80)
+        assert np.array_equal(l1, l0) and np.array_equal(d1, d0), t_cap
+        assert np.array_equal(m1, m0), t_cap
+        for b in range(len(ids_list)):
+            assert np.all(m1[b, int(l1[b]):] == 0)
+        assert int(l1.max()) <= t_cap
+
+
 def test_fast_encoder_precision_bounded():
     """encoder_precision="fast" (the whole acoustic model in bf16) stays available: its durations
     may round differently near .5 (measured 131 of 4,608 C3 tokens, all within 0.1 of a boundary);

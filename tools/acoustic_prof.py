@@ -20,13 +20,14 @@ def run():
     from gonova_tts_amd.engine import HipEngine
     from gonova_tts_amd.weights import make_acoustic_weights
     B, N, dur = int(os.environ.get("ACOUSTIC_PROF_B", "32")), 144, 6
-    eng = HipEngine("cuda:0", acoustic_dtype="bf16", max_batch=B, max_frames=N * dur, max_tokens=N)
+    t_cap = int(os.environ.get("ACOUSTIC_PROF_TCAP", str(N * dur)))  # padded frame extent (predicted durations)
+    eng = HipEngine("cuda:0", acoustic_dtype="bf16", max_batch=B, max_frames=t_cap, max_tokens=N)
     eng.load_weights(acoustic=make_acoustic_weights(seed=0, fixed_duration=dur))
     g = torch.Generator(device="cpu").manual_seed(2000)
     tok = torch.randint(1, 78, (B, N), generator=g, dtype=torch.int32).cuda()
     tl = torch.full((B,), N, dtype=torch.int32, device="cuda")
     for _ in range(ITERS):
-        eng.acoustic(tok, tl, N * dur)
+        eng.acoustic(tok, tl, t_cap)
         torch.cuda.synchronize()
     eng.close()
 

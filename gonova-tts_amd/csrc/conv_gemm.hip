@@ -744,7 +744,9 @@ __global__ __launch_bounds__(256, OCC) void conv_xres_kernel(ConvParams p, int C
   }
   __syncthreads();
   const bool plain = !R1 && !R2 && p.out_scale == 1.0f;
-  const bool lnf = p.ln_cnt != nullptr;  // LayerNorm in this launch (the launcher checked the shape)
+  // LayerNorm in this launch (the launcher checked the shape; never the 96-row tiles, small grids
+  // only, where the separate launch is faster -- and their non-inlined tail put p in scratch)
+  const bool lnf = NT != 3 && p.ln_cnt != nullptr;
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int rl = tid / PPR + it * (NTHR / PPR);
@@ -936,13 +938,37 @@ static bool xres_narrow(const ConvParams& p, int nt) {
 #ifndef TTS_XRES_NT2_MAXBLK
 #define TTS_XRES_NT2_MAXBLK 400        // 0 disables the small-grid 64-row rule below
 #endif
+#ifndef TTS_XRES_NT3
+#define TTS_XRES_NT3 1                 // 96-row tiles where they balance a small grid better (below)
+#endif
 // 64-row tiles (NT = 2) where 128-row tiles would leave much of the last tile of every
 // utterance empty (the encoder's 144 rows: 3 x 64 = 192 rows of work instead of 2 x 128)
-static int xres_nt(const ConvParams& p, int wm) {
-  const int force = sw(SW_XRES_NT);  // 2 / 4 force a tile height (tests), else automatic
+static int xres_nt_auto(const ConvParams& p);
+// nt3: the launch has a 96-row (NT = 3) instance (the DMA forms of 1 and 3 taps)
+static int xres_nt(const ConvParams& p, int wm, bool nt3 = false) {
+  const int force = sw(SW_XRES_NT);  // 2 / 3 / 4 force a tile height (tests), else automatic
   if (wm != 4) return 4;
   if (force == 2 || force == 4) return force;
+  if (force == 3 && nt3) return 3;
   if (!TTS_XRES_SMALL_TILES) return 4;
+  const int nt = xres_nt_auto(p);
+  // 96-row tiles for a grid whose blocks all fit on the chip at once but fill it unevenly: the
+  // busiest CU holds ceil(blocks / 256) tiles, so the launch takes ~ceil(blocks / 256) * NT row
+  // units.  The batch-8 decoder's 384-channel layers (FFN down-projection, output projection,
+  // second pointwise conv; 6,912 rows): 324 blocks of 64 rows put two on 68 CUs (cost 4), 216
+  // of 96 rows one per CU (cost 3).  Taken only when strictly cheaper and the 96-row grid is at
+  // most one block per CU: on bigger grids (batch 32) the smaller tiles' extra weight stream per
+  // row cost more than the balance gained (profiles/r05s_ab_nt3.txt).  Same channel group, so
+  // the same bits.
+  if (nt3 && TTS_XRES_NT3) {
+    const long long mb = (long long)((p.M + 127) / 128) * p.B * p.nh;
+    auto blocks = [&](int n) { return ((p.y_rows + 32 * n - 1) / (32 * n)) * mb; };
+    auto cost = [&](int n) { return (blocks(n) + 255) / 256 * n; };
+    if (blocks(3) <= 256 && cost(3) < cost(nt)) return 3;
+  }
+  return nt;
+}
+static int xres_nt_auto(const ConvParams& p) {
   const int r4 = (p.y_rows + 127) / 128 * 128, r2 = (p.y_rows + 63) / 64 * 64;
   if (8 * r2 <= 7 * r4) return 2;
   // small grids (the batch-8 decoder): 64-row tiles where the 128-row grid fills under ~1.5
@@ -989,7 +1015,7 @@ static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s, boo
   const int ord = sw(SW_XRES_ORDER) < 0 ? TTS_XRES_ORDER_DEFAULT : sw(SW_XRES_ORDER);
   q.xres_order = (ord == 2 || (ord == 1 && DT > 1)) ? 1 : 0;
   if (q.xres_order) grid = dim3(8 * ((grid.x * grid.y * grid.z + 7) / 8), 1, 1);
-  if (!xres_ln_ok(q, BN)) q.ln_cnt = nullptr;  // the kernel's LayerNorm switch
+  if (NT == 3 || !xres_ln_ok(q, BN)) q.ln_cnt = nullptr;  // the kernel's LayerNorm switch
   if (ln_done) *ln_done = q.ln_cnt != nullptr;
   hipLaunchKernelGGL((conv_xres_kernel<T, NT, WM, OCC, XF, DT>), grid, dim3(256), lds, s, q, cg);
   return hipGetLastError();
@@ -998,7 +1024,12 @@ static hipError_t launch_xres_wm(const ConvParams& p, int cg, hipStream_t s, boo
 template <typename T>
 static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err, bool* ln_done) {
   const int wm = xres_wm(p);
-  const int nt = xres_nt(p, wm);
+  const bool big = TTS_XRES_BIGCG_MIN > 0 && wm == 4 && p.Cin >= TTS_XRES_BIGCG_MIN;
+  const bool dma3 = xres_dma_taps(p) == 3, dma1 = xres_dma_taps(p) != 2 && !dma3 && xres_dma1(p);
+  // (the 96-row option never displaces the narrow tiles: they are decided at the other heights)
+  const int nt0 = xres_nt(p, wm);
+  const bool narrow = xres_narrow(p, nt0);
+  const int nt = narrow ? nt0 : xres_nt(p, wm, !big && (dma3 || dma1));
   // channel group sized for 128-row tiles whatever the tile height: the group fixes the K
   // order of the accumulation, so a row's result does not depend on the tiling (streamed
   // chunks stay bit-identical to the full pass)
@@ -1006,26 +1037,27 @@ static bool launch_xres(const ConvParams& p, hipStream_t s, hipError_t* err, boo
   // groups at one block per CU: a quarter of the single-buffered group stagings, each a full
   // HBM/L2 round trip.  The choice depends on the layer shape only, so the K order is still
   // the same for every batch size and tile shape.
-  const bool big = TTS_XRES_BIGCG_MIN > 0 && wm == 4 && p.Cin >= TTS_XRES_BIGCG_MIN;
   const int cg = xres_group(p, 32 * 4 * (4 / wm), big ? XRES_LDS_BIG : XRES_LDS_MAX);
   if (!cg) return false;
   if (wm == 2)  // (the postnet's 80-channel output conv)
     *err = launch_xres_wm<T, 2>(p, cg, s, ln_done);
   else if (big)
-    *err = xres_narrow(p, nt) ? launch_xres_wm<T, 2, 1, 1>(p, cg, s, ln_done)
+    *err = narrow    ? launch_xres_wm<T, 2, 1, 1>(p, cg, s, ln_done)
            : nt == 2          ? launch_xres_wm<T, 4, 2, 1>(p, cg, s, ln_done)
                               : launch_xres_wm<T, 4, 4, 1>(p, cg, s, ln_done);
-  else if (xres_narrow(p, nt))
+  else if (narrow)
     *err = launch_xres_wm<T, 2, 1>(p, cg, s, ln_done);
-  else if (xres_dma_taps(p) == 3)  // (TTS_XRES_DMA=2: the same layers, K order and bits, register-staged)
-    *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, false, 3>(p, cg, s, ln_done)
-                   : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, false, 3>(p, cg, s, ln_done);
+  else if (dma3)  // (TTS_XRES_DMA=2: the same layers, K order and bits, register-staged)
+    *err = nt == 2   ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, false, 3>(p, cg, s, ln_done)
+           : nt == 3 ? launch_xres_wm<T, 4, 3, TTS_XRES_OCC, false, 3>(p, cg, s, ln_done)
+                     : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, false, 3>(p, cg, s, ln_done);
   else if (xres_dma_taps(p) == 2)  // the polyphase upsamplers (k = 2 s): 2 taps
     *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, false, 2>(p, cg, s, ln_done)
                    : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, false, 2>(p, cg, s, ln_done);
   else if (xres_dma1(p))
-    *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, false, 1>(p, cg, s, ln_done)
-                   : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, false, 1>(p, cg, s, ln_done);
+    *err = nt == 2   ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, false, 1>(p, cg, s, ln_done)
+           : nt == 3 ? launch_xres_wm<T, 4, 3, TTS_XRES_OCC, false, 1>(p, cg, s, ln_done)
+                     : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, false, 1>(p, cg, s, ln_done);
   else if (TTS_XRES_UPFIRST && p.up_s)
     *err = nt == 2 ? launch_xres_wm<T, 4, 2, TTS_XRES_OCC, true>(p, cg, s, ln_done)
                    : launch_xres_wm<T, 4, 4, TTS_XRES_OCC, true>(p, cg, s, ln_done);

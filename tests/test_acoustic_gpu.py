@@ -281,8 +281,9 @@ def test_attention_key_groups_match(aw, dtype, switch):
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_short_row_tiles_bit_identical(aw, dtype, switch):
     """conv_xres picks 64-row tiles where 128-row tiles would leave much of each utterance's
-    last tile empty (the encoder's short token rows).  The channel group, and so the K order
-    of the accumulation, is the same for both tile heights, so the mel matches the 128-row
+    last tile empty (the encoder's short token rows), and 96-row tiles where they balance a small
+    grid (the batch-8 decoder's 384-channel layers).  The channel group, and so the K order
+    of the accumulation, is the same for every tile height, so the mel matches the 128-row
     run bit for bit (ragged batch, lengths across 64-row edges, durations forced) -- the
     property the chunked vocoder's bit-exactness rests on.  The narrow 64 x 64 tiles picked
     for under-filled grids (this batch of 4 picks them everywhere eligible) keep the same K
@@ -297,6 +298,8 @@ def test_short_row_tiles_bit_identical(aw, dtype, switch):
     big, lb, _ = run(eng, ids_list, t_cap=432, durations=durs)
     switch("TTS_XRES_NT", 2)
     small, ls, _ = run(eng, ids_list, t_cap=432, durations=durs)
+    switch("TTS_XRES_NT", 3)       # 96-row tiles (the 1- and 3-tap DMA forms; others keep their auto height)
+    mid, lm, _ = run(eng, ids_list, t_cap=432, durations=durs)
     switch("TTS_XRES_NT", None)
     switch("TTS_XRES_NARROW", 1)   # 64 x 64 tiles wherever eligible
     narrow, ln, _ = run(eng, ids_list, t_cap=432, durations=durs)
@@ -304,8 +307,9 @@ def test_short_row_tiles_bit_identical(aw, dtype, switch):
     auto, la, _ = run(eng, ids_list, t_cap=432, durations=durs)
     for b, ids in enumerate(ids_list):
         L = int(la[b])
-        assert int(lb[b]) == L == int(ls[b]) == int(ln[b]) == len(ids) * 3
+        assert int(lb[b]) == L == int(ls[b]) == int(ln[b]) == int(lm[b]) == len(ids) * 3
         assert np.array_equal(auto[b], big[b]) and np.array_equal(small[b], big[b]), b
+        assert np.array_equal(mid[b], big[b]), b
         assert np.array_equal(narrow[b], big[b]), b
         ref = acoustic_forward(ids, aw, durations=durs[b])
         check(f"acoustic {dtype} short row tiles b={b}", auto[b, :L], ref["mel"], kind="ac_" + dtype)

@@ -139,11 +139,14 @@ struct AcousticModel::Impl {
   int *i_dur = nullptr, *i_tokmap = nullptr;
   int* ln_cnt = nullptr;  // row-tile counters of the fused post-LNs (zeroed once; ln_rows.h)
   int ln_cnt_n = 0;
+  int* h_lens = nullptr;  // pinned host copy of the frame counts (the decoder-extent read)
+  int h_lens_n = 0;
 
   ~Impl() {
     for (void* p : allocs) hipFree(p);
     for (void* p : ws) hipFree(p);
     for (void* p : score_ws) hipFree(p);
+    if (h_lens) hipHostFree(h_lens);
   }
 
   void* track(void* p) { allocs.push_back(p); return p; }
@@ -538,11 +541,17 @@ struct AcousticModel::Impl {
     int Td = Tcap;
     const int trim = sw(SW_DEC_TRIM);
     if (!dur_override && B > 0 && (trim == 1 || (trim < 0 && Tcap > TTS_DEC_TRIM_RATIO * N))) {
-      std::vector<int> lens_h((size_t)B);
-      HIP_CHECK(hipMemcpyAsync(lens_h.data(), mel_lens, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, s));
+      if (h_lens_n < B) {  // pinned: the copy is a DMA on the stream, not a staged blocking copy
+        if (h_lens) HIP_CHECK(hipHostFree(h_lens));
+        h_lens = nullptr;
+        h_lens_n = 0;
+        HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_lens), (size_t)B * sizeof(int), hipHostMallocDefault));
+        h_lens_n = B;
+      }
+      HIP_CHECK(hipMemcpyAsync(h_lens, mel_lens, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
       int mx = 1;
-      for (int v : lens_h) mx = std::max(mx, v);
+      for (int i = 0; i < B; ++i) mx = std::max(mx, h_lens[i]);
       Td = std::min(Tcap, mx);
     }
     const int Tpd = rup(Td, 32);  // decoder row stride

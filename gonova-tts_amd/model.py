@@ -191,6 +191,11 @@ class GonovaTTS:
                 need, lens_known, tripped = _need_and_lens(dur, mel_lens, rw)
                 if tripped:
                     return None, None, True
+            # the vocoder (and the waveform the caller copies to the host) at the frames the
+            # durations give, not the 12-per-token budget: half the grid and the bytes at C3's 6
+            T_act = max(1, int(lens_known.max())) if len(lens_known) else 1
+            if T_act < mel.shape[1] and os.environ.get("TTS_VOC_TRIM", "1") != "0":  # (0: A/B runs)
+                mel = mel[:, :T_act].contiguous()
         wav = self.engine.vocoder(mel, mel_lens, stream=stream)
         if self.sr != self.native_sr:
             g = gcd(self.sr, self.native_sr)

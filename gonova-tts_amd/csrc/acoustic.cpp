@@ -116,6 +116,11 @@ struct AcousticModel::Impl {
   void* embed = nullptr;
   std::vector<ConformerLayer> enc, dec;
   Predictor pitch, energy, duration;
+  // the predictors' first convs batched along M (pitch | energy | duration, and pitch | energy for
+  // given durations) and their first LayerNorms as one grouped launch (predict_batched)
+  ConvLayer vp0_all, vp0_pe;
+  LnGroups vp_ln{};
+  bool vp_batched = false;
   float *pe_w = nullptr, *pe_b = nullptr, *ee_w = nullptr, *ee_b = nullptr;
   ConvLayer feat_out;
   std::vector<ConvLayer> postnet;
@@ -135,6 +140,7 @@ struct AcousticModel::Impl {
   void *X = nullptr, *Y = nullptr, *O = nullptr, *G = nullptr, *Qu = nullptr, *Qv = nullptr;
   void *H1 = nullptr, *QKV = nullptr, *A = nullptr, *Vt = nullptr, *AC = nullptr, *BD = nullptr, *P = nullptr;
   void *ENC = nullptr, *PB1 = nullptr, *PB2 = nullptr, *BEF = nullptr, *PN1 = nullptr, *PN2 = nullptr, *MELT = nullptr;
+  void* VP = nullptr;
   float *f_pitch = nullptr, *f_energy = nullptr, *f_logd = nullptr;
   int *i_dur = nullptr, *i_tokmap = nullptr;
   int* ln_cnt = nullptr;  // row-tile counters of the fused post-LNs (zeroed once; ln_rows.h)
@@ -252,6 +258,56 @@ struct AcousticModel::Impl {
     return P;
   }
 
+  // The three variance predictors read the same encoder output (HF:1198-1210): their first convs
+  // run as one GEMM whose M blocks are the three layers' and their first LayerNorms as one grouped
+  // launch; each predictor's second conv reads its slice of the batched rows.  Two launches
+  // instead of six at the start of the variance adaptor, where the 80-block grids of batch 8 left
+  // two thirds of the CUs idle.  The layers' kernel widths differ (HF: pitch 5, energy and
+  // duration 3): the narrower ones are zero-padded to the widest tap for tap, centred, so each
+  // output channel's products arrive in the layer's own order with exact zeros (+0 products)
+  // around them -- the same sums, bit for bit (tests/test_acoustic_gpu.py).  fp32 encoder
+  // activations only (the exact encoder and fp32 models); the fast 16-bit encoder keeps the
+  // per-predictor launches.
+  void batch_predictors(const GetData& get, const GetShape& shape) {
+    vp_batched = false;
+    if (bdt != DT_F32 || sw(SW_VP_BATCH) == 0) return;
+    Predictor* ps[3] = {&pitch, &energy, &duration};
+    const ConvLayer& c0 = pitch.convs.at(0);
+    int kmax = 1;
+    for (Predictor* q : ps) {
+      const ConvLayer& c = q->convs.at(0);
+      if (q->convs.size() < 2 || c.M != c0.M || c.Cin != c0.Cin || c.pad != (c.taps - 1) / 2 || c.taps % 2 == 0 ||
+          c.dil != 1 || c.M > 256)
+        return;
+      kmax = std::max(kmax, c.taps);
+    }
+    const char* names[3] = {"pitch_predictor.", "energy_predictor.", "duration_predictor."};
+    const int M = c0.M, Ci = c0.Cin;
+    std::vector<float> w, b;  // [3 M][Cin][kmax] (PyTorch Conv1d layout), taps centred
+    for (int i = 0; i < 3; ++i) {
+      const std::string q = std::string(names[i]) + "conv_layers.0.";
+      const auto& wi = need(get, q + "conv.weight");
+      const int k = (int)shape(q + "conv.weight").at(2), off = (kmax - k) / 2;
+      if (wi.size() != (size_t)M * Ci * k) return;
+      std::vector<float> wp((size_t)M * Ci * kmax, 0.f);
+      for (size_t oc = 0; oc < (size_t)M * Ci; ++oc)
+        for (int t = 0; t < k; ++t) wp[oc * kmax + off + t] = wi[oc * k + t];
+      w.insert(w.end(), wp.begin(), wp.end());
+      if (get(q + "conv.bias")) {
+        const auto& bi = *get(q + "conv.bias");
+        b.insert(b.end(), bi.begin(), bi.end());
+      } else {
+        b.insert(b.end(), (size_t)M, 0.f);
+      }
+      vp_ln.g[i] = ps[i]->lns.at(0).g;
+      vp_ln.b[i] = ps[i]->lns.at(0).b;
+      if (i == 1)
+        vp0_pe = make_conv(w, 2 * M, Ci, kmax, b, 1, (kmax - 1) / 2, bdt, allocs, nullptr, split_now());
+    }
+    vp0_all = make_conv(w, 3 * M, Ci, kmax, b, 1, (kmax - 1) / 2, bdt, allocs, nullptr, split_now());
+    vp_batched = true;
+  }
+
   // relative-position table through linear_pos, rows q <-> rel = rmax-1-q (HF:723-752, 419)
   void build_ptabs(int new_rmax, hipStream_t s) {
     const int rows = 2 * new_rmax;
@@ -296,7 +352,7 @@ struct AcousticModel::Impl {
   // re-reservation (HIP_CHECK throws midway) can never leave a cap describing freed memory.
   void drop_ws() {
     cap_B = cap_N = cap_T = 0;
-    X = Y = O = G = Qu = Qv = H1 = QKV = A = Vt = ENC = SPK = PB1 = PB2 = BEF = PN1 = PN2 = MELT = nullptr;
+    X = Y = O = G = Qu = Qv = H1 = QKV = A = Vt = ENC = SPK = PB1 = PB2 = BEF = PN1 = PN2 = MELT = VP = nullptr;
     f_pitch = f_energy = f_logd = nullptr;
     i_dur = i_tokmap = nullptr;
     ln_cnt = nullptr;
@@ -362,6 +418,7 @@ struct AcousticModel::Impl {
     ENC = alloc_ws(nrows * D, ee);
     SPK = alloc_ws((size_t)B * D, ee);
     PB1 = alloc_ws(nrows * PRED, std::max<size_t>(ee, 2)); PB2 = alloc_ws(nrows * PRED, ee);  // PB1 also holds f32 logd [B][N]
+    VP = alloc_ws(nrows * 3 * 256, 4);  // the batched first predictor convs (fp32, <= 256 channels each)
     const size_t trows = (size_t)B * rup(T, 32);
     BEF = alloc_ws(trows * NMEL, ed); MELT = alloc_ws(trows * NMEL, ed);
     PN1 = alloc_ws(trows * PRED, ed); PN2 = alloc_ws(trows * PRED, ed);
@@ -484,6 +541,36 @@ struct AcousticModel::Impl {
     }
   }
 
+  // the three (with_dur) or two predictors with the batched first conv and grouped first LayerNorm
+  // (batch_predictors); each second conv reads its predictor's slice of VP (row stride G * PRED)
+  void predict_batched(const void* x, const int* lens, int B, int Np, bool with_dur, hipStream_t s) {
+    const int G = with_dur ? 3 : 2;
+    const int C = pitch.convs[0].M;
+    run(with_dur ? vp0_all : vp0_pe, x, Np, lens, VP, Np, B, DT_F32, s, prof, 1.f, ACT_RELU);
+    elem(s, [&] { return launch_layernorm_groups(DT_F32, VP, B * Np, C, G * C, vp_ln, G, eps, s, lens, Np); });
+    Predictor* ps[3] = {&pitch, &energy, &duration};
+    float* outs[3] = {f_pitch, f_energy, f_logd};
+    for (int g = 0; g < G; ++g) {
+      Predictor& Pr = *ps[g];
+      const void* h = reinterpret_cast<const float*>(VP) + (size_t)g * C;
+      int ld = G * C;
+      void* bufs[2] = {PB1, PB2};
+      const int n = (int)Pr.convs.size();
+      for (int i = 1; i < n; ++i) {
+        void* o = bufs[i & 1];
+        ConvParams ln = ln_params(i + 1 < n ? o : nullptr, Pr.lns[i], nullptr);
+        if (i + 1 == n) { ln.ln_lin_w = Pr.lin_w; ln.ln_lin_b = Pr.lin_b; ln.ln_lin_out = outs[g]; }
+        ConvParams ex = ln;
+        ex.range_flag = range_flag;
+        ex.no_split = enc_f32 ? 1 : 0;
+        run_layer(Pr.convs[i], h, Np, lens, o, Np, B, DT_F32, s, prof, 1.f, ACT_RELU, 1.f, nullptr, nullptr, 1.f, ld, 0,
+                  cur_rpad, split_ws, split_ws_bytes, &ex);
+        h = o;
+        ld = 0;
+      }
+    }
+  }
+
   void forward(const int* tokens, const int* tok_lens, int B, int N, const int* dur_override, float* mel,
                int* mel_lens, int Tcap, int* durations, const float* spk, hipStream_t s) {
     reserve(B, N, Tcap);
@@ -516,12 +603,16 @@ struct AcousticModel::Impl {
       HIP_CHECK(hipMemcpyAsync(ENC, Y, (size_t)B * Np * D * dtype_size(dte), hipMemcpyDeviceToDevice, s));
     }
     // variance adaptor (HF:1198-1218)
-    predict(pitch, ENC, tok_lens, B, Np, f_pitch, s);
-    predict(energy, ENC, tok_lens, B, Np, f_energy, s);
     // HF inference always regulates with the predicted durations (HF:1211-1219); given durations
     // are this engine's override (the oracle's `durations=`), under which the prediction is
     // never read, so the duration predictor does not run
-    if (!dur_override) predict(duration, ENC, tok_lens, B, Np, f_logd, s);
+    if (vp_batched && sw(SW_VP_BATCH) != 0) {
+      predict_batched(ENC, tok_lens, B, Np, !dur_override, s);
+    } else {
+      predict(pitch, ENC, tok_lens, B, Np, f_pitch, s);
+      predict(energy, ENC, tok_lens, B, Np, f_energy, s);
+      if (!dur_override) predict(duration, ENC, tok_lens, B, Np, f_logd, s);
+    }
     cur_rpad = 0;
     // logd is laid out [B][Np]; durations kernel reads [B][N] rows -> compact view via stride Np
     int* dur = durations ? durations : i_dur;
@@ -614,6 +705,7 @@ void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtyp
   m->pitch = m->predictor(get, shape, "pitch_predictor.");
   m->energy = m->predictor(get, shape, "energy_predictor.");
   m->duration = m->predictor(get, shape, "duration_predictor.");
+  m->batch_predictors(get, shape);
   if (get("projection.weight")) {
     const auto ps = shape("projection.weight");  // [D][D + E]
     const int din = (int)ps.at(1);

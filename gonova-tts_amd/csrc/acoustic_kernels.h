@@ -8,6 +8,14 @@ hipError_t launch_embed(int dt, const int* ids, const int* lens, int B, int N, i
                         float scale, void* out, hipStream_t s);
 hipError_t launch_layernorm(int dt, const void* in, void* out, int rows, int C, const float* g1, const float* b1,
                             const float* g2, const float* b2, float eps, hipStream_t s, const int* lens = nullptr, int stride = 0);
+// groups LayerNorms (C <= 256 channels each, side by side in rows of ld elements) in place, one launch
+struct LnGroups {
+  static constexpr int MAXG = 4;
+  const float* g[MAXG];
+  const float* b[MAXG];
+};
+hipError_t launch_layernorm_groups(int dt, void* x, int rows, int C, int ld, const LnGroups& gp, int groups, float eps,
+                                   hipStream_t s, const int* lens = nullptr, int stride = 0);
 hipError_t launch_pos_bias(int dt, const void* qkv, int rows, int D, const float* u, const float* v, void* qu,
                            void* qv, hipStream_t s);
 hipError_t launch_transpose_v(int dt, const void* qkv, const int* lens, int B, int Tm, int D, int H, int Sk, void* vt,

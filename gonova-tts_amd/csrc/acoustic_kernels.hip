@@ -71,6 +71,30 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const T* __restrict__ in
     if (on[i]) o[ch[i]] = from_f32<T>(v[0][i]);
 }
 
+// G LayerNorms of C channels side by side in rows of ld elements, in place, one launch (blockIdx.y
+// = group g: channels [g*C, (g+1)*C) with its own gain and bias): the variance predictors' first
+// LayerNorms after their batched first conv.  Per row segment the arithmetic of layernorm_kernel.
+template <typename T, int PER>
+__global__ __launch_bounds__(256) void layernorm_groups_kernel(T* __restrict__ x, int rows, int C, int ld,
+                                                              LnGroups gp, float eps, const int* lens, int stride) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int grp = blockIdx.y;
+  if (row >= rows || !ln_row_valid(row, lens, stride)) return;
+  T* xr = x + (long long)row * ld + (long long)grp * C;
+  int ch[PER];
+  bool on[PER];
+  ln_lanes64<PER>(ch, on, C, lane);
+  float g[2][PER], bb[2][PER], v[1][PER];
+  ln_params<PER>(g, bb, ch, on, gp.g[grp], gp.b[grp], nullptr, nullptr);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) v[0][i] = on[i] ? to_f32(xr[ch[i]]) : 0.f;
+  ln_batch<T, 1, PER, false>(v, on, C, g, bb, eps);
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+    if (on[i]) xr[ch[i]] = from_f32<T>(v[0][i]);
+}
+
 // ---------------------------------------------------------------------------
 // attention prep: Qu = q + pos_bias_u, Qv = q + pos_bias_v (HF:420-423) from QKV [rows][3D]
 // ---------------------------------------------------------------------------
@@ -553,6 +577,15 @@ hipError_t launch_layernorm(int dt, const void* in, void* out, int rows, int C, 
   }
   TTS_DISPATCH(dt, hipLaunchKernelGGL((layernorm_kernel<TT, 8>), grid, dim3(256), 0, s, (const TT*)in, (TT*)out, rows,
                                       C, g1, b1, g2, b2, eps, lens, stride));
+}
+
+hipError_t launch_layernorm_groups(int dt, void* x, int rows, int C, int ld, const LnGroups& gp, int groups, float eps,
+                                   hipStream_t s, const int* lens, int stride) {
+  if (C > 256 || groups < 1 || groups > LnGroups::MAXG || ld < groups * C || (lens && stride <= 0))
+    return hipErrorInvalidValue;
+  dim3 grid((rows + 3) / 4, groups);
+  TTS_DISPATCH(dt, hipLaunchKernelGGL((layernorm_groups_kernel<TT, 4>), grid, dim3(256), 0, s, (TT*)x, rows, C, ld, gp,
+                                      eps, lens, stride));
 }
 
 hipError_t launch_pos_bias(int dt, const void* qkv, int rows, int D, const float* u, const float* v, void* qu,

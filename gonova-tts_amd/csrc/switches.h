@@ -24,6 +24,7 @@ enum Sw : int {
   SW_CONV_MT,      // TTS_CONV_MT=1: the acoustic 16-bit GEMMs on conv_mt (k = 3 layers on conv_tap_kernel; 2: on conv_mt_kernel) instead of conv_xres (default 0)
   SW_MT_TILE,      // TTS_MT_TILE=0..3: force a conv_mt_kernel tile configuration, 4..10 a conv_tap_kernel one (tests; default: chosen per launch)
   SW_PAIR_SPLIT,   // TTS_PAIR_SPLIT=0/1: the channel-split pair form never / wherever possible (default: small C >= 128 grids)
+  SW_VP_BATCH,     // TTS_VP_BATCH=0: the variance predictors' first convs / LayerNorms as separate launches (fp32 encoder)
   SW_DEC_TRIM,     // TTS_DEC_TRIM=0/1: with predicted durations the decoder never / always runs at the longest utterance's frames (default: budgets over 8 frames per token)
   SW_N
 };

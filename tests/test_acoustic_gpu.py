@@ -562,6 +562,25 @@ def test_predicted_durations_bf16_mel_matches_oracle(aw):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_batched_variance_predictors_bit_identical(aw, dtype, switch):
+    """The variance predictors' first convs as one GEMM and their first LayerNorms as one grouped
+    launch (acoustic.cpp batch_predictors / predict_batched, fp32 encoder activations) against the
+    per-predictor launches (TTS_VP_BATCH=0): the same durations and mel bit for bit, with predicted
+    durations (three predictors) and given ones (pitch and energy only), on a ragged batch."""
+    eng = engine(dtype, aw)
+    rng = np.random.default_rng(43)
+    ids_list = [rng.integers(1, 78, size=n) for n in (57, 1, 30, 44)]
+    durs = [rng.integers(0, 9, size=len(x)) for x in ids_list]
+    for d in (None, durs):
+        switch("TTS_VP_BATCH", 0)
+        m0, l0, d0 = run(eng, ids_list, t_cap=12 * 57, durations=d)
+        switch("TTS_VP_BATCH", None)
+        m1, l1, d1 = run(eng, ids_list, t_cap=12 * 57, durations=d)
+        assert np.array_equal(l1, l0) and np.array_equal(d1, d0), d is None
+        assert np.array_equal(m1, m0), d is None
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
 def test_decoder_extent_trim_bit_identical(aw, dtype, switch):
     """With predicted durations the decoder runs at the longest utterance's frame count, read back
     after the variance adaptor, not at the caller's budget t_cap (acoustic.cpp forward,

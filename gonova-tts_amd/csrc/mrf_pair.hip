@@ -147,9 +147,16 @@ constexpr int pair_bn() {
 #ifndef TTS_PAIR_RESREG
 #define TTS_PAIR_RESREG 0
 #endif
+#ifndef TTS_PAIR_RESREG_ONLYC
+#define TTS_PAIR_RESREG_ONLYC 0  // A/B builds: only pairs of this channel count (0: every C <= 128)
+#endif
+#ifndef TTS_PAIR_RESREG_OCC
+#define TTS_PAIR_RESREG_OCC 2    // blocks per CU the RESREG register budget is sized for
+#endif
 template <int C, int DIV, int K = 0, bool POST = false>
 struct PairGeomS : PairGeom<C> {
-  static constexpr bool RESREG = TTS_PAIR_RESREG && C <= 128 && !POST;
+  static constexpr bool RESREG = TTS_PAIR_RESREG && C <= 128 && !POST &&
+                                 (TTS_PAIR_RESREG_ONLYC == 0 || C == TTS_PAIR_RESREG_ONLYC);
   static constexpr int BN = DIV == 1 && K > 0 && !POST ? pair_bn<C, K>() : PairGeom<C>::BN / DIV;
   // short tiles do few MFMAs per k-step (one row tile per wave), so the weight ring's L2 round
   // trips are exposed unless it runs further ahead; the depth only moves loads earlier (same
@@ -160,7 +167,7 @@ struct PairGeomS : PairGeom<C> {
                                                              : PairGeom<C>::D;
   // blocks per CU the register budget is sized for (the C = 32 k = 11 pairs without conv_post
   // may take a fourth: TTS_P32K11_OCC; the HiFi-GAN V3 C = 64 k = 5 pair spills at three)
-  static constexpr int OCC = RESREG                                  ? 2
+  static constexpr int OCC = RESREG                                  ? TTS_PAIR_RESREG_OCC
                              : C == 32 && K == 11 && !POST && DIV == 1 ? TTS_P32K11_OCC
                              : C == 64 && K == 5                    ? 2
                                                                     : PairGeom<C>::OCC;

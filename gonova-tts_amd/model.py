@@ -135,9 +135,7 @@ class GonovaTTS:
         import torch
         dev = self.engine.torch_device
         B, N = tokens.shape
-        tok = torch.from_numpy(np.ascontiguousarray(tokens, np.int32)).to(dev)
-        tl = torch.from_numpy(np.ascontiguousarray(lens, np.int32)).to(dev)
-        dd = None if durations is None else torch.from_numpy(np.ascontiguousarray(durations, np.int32)).to(dev)
+        tok, tl, dd = _upload_i32((tokens, lens, durations), dev, stream)
         t_cap = max(64, int(self.FRAMES_PER_TOKEN_CAP * N))
         if durations is not None:
             t_cap = max(1, int(np.asarray(durations).sum(axis=1).max()))
@@ -239,9 +237,7 @@ class GonovaTTS:
         ctx = self.STREAM_CONTEXT if context is None else context
         dev = self.engine.torch_device
         B, N = tokens.shape
-        tok = torch.from_numpy(np.ascontiguousarray(tokens, np.int32)).to(dev)
-        tl = torch.from_numpy(np.ascontiguousarray(lens, np.int32)).to(dev)
-        dd = None if durations is None else torch.from_numpy(np.ascontiguousarray(durations, np.int32)).to(dev)
+        tok, tl, dd = _upload_i32((tokens, lens, durations), dev, stream)
         t_cap = max(64, int(self.FRAMES_PER_TOKEN_CAP * N)) if durations is None else \
             max(1, int(np.asarray(durations).sum(axis=1).max()))
         spk = speaker_embedding
@@ -440,6 +436,34 @@ class PendingRange:
         with torch.cuda.device(m.engine.device_index), m._range_fallback():
             wav, wav_lens, _ = m._synthesize_once(*self.args)
         return wav, np.asarray(wav_lens, np.int64)
+
+
+_UPLOAD_STREAMS: Dict[int, object] = {}
+
+
+def _upload_i32(arrays, dev, stream=None):
+    """Host integer arrays (None passes through) -> device int32 tensors, staged through pinned
+    memory and copied on a per-device upload stream that `stream` (else the device's current
+    stream, the one the engine calls enqueue on) then waits for.  Copied in order on the compute
+    stream, a batch's inputs went up only when the previous batch's kernels had finished -- the
+    moment dist.ShardedSynthesis (C4) starts that batch's waveform download, which held the small
+    uploads (and the GPU) for ~0.7-1.7 ms per batch (profiles/r05zz_c4_gaps.txt).  Issued at once
+    on their own stream they land while the previous batch still computes."""
+    import torch
+    target = stream if stream is not None else torch.cuda.current_stream(dev)
+    idx = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
+    up = _UPLOAD_STREAMS.get(idx)
+    if up is None:
+        up = _UPLOAD_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    with torch.cuda.stream(up):
+        out = [None if a is None else
+               torch.from_numpy(np.ascontiguousarray(a, np.int32)).pin_memory().to(dev, non_blocking=True)
+               for a in arrays]
+    target.wait_stream(up)
+    for t in out:
+        if t is not None:
+            t.record_stream(target)  # (allocated on the upload stream, used on the target)
+    return out
 
 
 def _need_and_lens(dur, mel_lens, rw=None):

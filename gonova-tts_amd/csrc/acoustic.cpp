@@ -90,6 +90,7 @@ struct AcousticModel::Impl {
     ConvParams ex = ln ? *ln : conv_params_default();
     ex.range_flag = range_flag;
     ex.no_split = enc_f32 ? 1 : 0;
+    ex.f32_splitk = dt == DT_F32 ? 1 : 0;  // fp32 model: split-K over split_ws (sized in reserve_fresh)
     run_layer(L, x, x_rows, lens, y, y_rows, B, d, s, pr, in_slope, act, alpha, r1, nullptr, 1.f, 0, 0, cur_rpad,
               split_ws, split_ws_bytes, &ex);
   }
@@ -438,6 +439,16 @@ struct AcousticModel::Impl {
           wsb = std::max(wsb, conv_split_ws_bytes(c->taps, c->Cin, c->M, F));
       for (const Predictor* pr : {&pitch, &energy, &duration})
         for (const ConvLayer& c : pr->convs) wsb = std::max(wsb, conv_split_ws_bytes(c.taps, c.Cin, c.M, F));
+    } else if (dt == DT_F32) {  // fp32 model: the split-K partials of its fp32 conv_gemm launches
+      const long long F = (long long)B * Tp;  // >= every stack's B * rows
+      auto add = [&](const ConvLayer& c) { wsb = std::max(wsb, f32_splitk_ws_bytes(c.taps, c.Cin, c.M, F)); };
+      for (const auto* st : {&enc, &dec})
+        for (auto& L : *st)
+          for (const ConvLayer* c : {&L.ffm1, &L.ffm2, &L.ff1, &L.ff2, &L.qkv, &L.out, &L.pw1, &L.pw2, &L.pos}) add(*c);
+      for (const Predictor* pr : {&pitch, &energy, &duration})
+        for (const ConvLayer& c : pr->convs) add(c);
+      add(vp0_all); add(vp0_pe); add(feat_out);
+      for (const ConvLayer& c : postnet) add(c);
     }
     split_ws = wsb ? (float*)alloc_ws((size_t)wsb, 1) : nullptr;
     split_ws_bytes = wsb;
@@ -563,6 +574,7 @@ struct AcousticModel::Impl {
         ConvParams ex = ln;
         ex.range_flag = range_flag;
         ex.no_split = enc_f32 ? 1 : 0;
+        ex.f32_splitk = dt == DT_F32 ? 1 : 0;
         run_layer(Pr.convs[i], h, Np, lens, o, Np, B, DT_F32, s, prof, 1.f, ACT_RELU, 1.f, nullptr, nullptr, 1.f, ld, 0,
                   cur_rpad, split_ws, split_ws_bytes, &ex);
         h = o;

@@ -91,6 +91,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
     bx = r % gx;
     bz = r / gx;
   }
+  // split-K (ConvParams::kslices, fp32): grid z = utterance x slice; slice sl covers Cin chunks
+  // [c_lo, c_hi) of every tap and leaves its raw sums to the reduce
+  const int S = p.kslices > 1 ? p.kslices : 1;
+  const int sl = bz % S;
+  bz /= S;
   const int b = bz / nh;
   const int hd = bz - b * nh;
   const int n0 = bx * BN;
@@ -118,6 +123,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
   T* xs0 = reinterpret_cast<T*>(smem);
   T* xs1 = xs0 + tile;
   const int nchunks = (p.Cin + CK - 1) / CK;
+  const int cps = (nchunks + S - 1) / S;
+  const int c_lo = sl * cps, c_hi = min(nchunks, c_lo + cps);
+  const int k_end = min(p.Cin, c_hi * CK);  // this slice's channel end
   const int xlast = xlen > 0 ? xlen - 1 : 0;
 
   // ---- X chunk staging: global -> registers (raw) -> act/mask -> LDS ----
@@ -174,21 +182,21 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x16{};
 
   Frag a_cur[MT][KS], a_nxt[MT][KS];
-  load_chunk(0);
-  load_a(a_cur, 0, 0);
-  store_chunk(xs0, 0);
+  load_chunk(c_lo * CK);
+  load_a(a_cur, c_lo * CK, 0);
+  store_chunk(xs0, c_lo * CK);
   __syncthreads();
 
-  for (int ci = 0; ci < nchunks; ++ci) {
-    const T* cur = (ci & 1) ? xs1 : xs0;
-    T* nxt = (ci & 1) ? xs0 : xs1;
+  for (int ci = c_lo; ci < c_hi; ++ci) {
+    const T* cur = ((ci - c_lo) & 1) ? xs1 : xs0;
+    T* nxt = ((ci - c_lo) & 1) ? xs0 : xs1;
     const int c0 = ci * CK;
-    const bool has_next = ci + 1 < nchunks;
+    const bool has_next = ci + 1 < c_hi;
     if (has_next) load_chunk(c0 + CK);
     for (int tap = 0; tap < p.taps; ++tap) {
       int ntap = tap + 1, nc0 = c0;
       if (ntap == p.taps) { ntap = 0; nc0 = c0 + CK; }
-      if (nc0 < p.Cin) load_a(a_nxt, nc0, ntap);
+      if (nc0 < k_end) load_a(a_nxt, nc0, ntap);
       const T* xrow = cur + (n_w0 + l31 + tap * p.dil) * LDSR + hh * MF::KPL;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -210,6 +218,24 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_gemm_kernel(ConvParams p
     __syncthreads();
   }
 
+  if (S > 1) {  // this slice's raw sums: ws[sl][b][n][m] (split_reduce_launch applies the epilogue)
+    float* P = p.ws + ((long long)sl * p.B + b) * p.y_rows * p.M;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int n = n0 + n_w0 + nt * 32 + l31;
+        if (n >= ylen) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int m = m_w0 + mt * 32 + 8 * g + 4 * hh;
+          if (m < p.M)
+            *reinterpret_cast<f32x4*>(P + (long long)n * p.M + m) =
+                f32x4{acc[mt][nt][4 * g], acc[mt][nt][4 * g + 1], acc[mt][nt][4 * g + 2], acc[mt][nt][4 * g + 3]};
+        }
+      }
+    return;
+  }
   conv_epilogue<T, MT, NT>(p, acc, b, hd, n0 + n_w0, m_w0, ylen, l31, hh);
 }
 
@@ -1074,9 +1100,49 @@ static hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
   const int R = BN + (p.taps - 1) * p.dil;
   const int nchunks = (p.Cin + CK - 1) / CK;
   const size_t lds = (size_t)R * LDSR * sizeof(T) * (nchunks > 1 ? 2 : 1);
-  dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh);
+  dim3 grid((p.y_rows + BN - 1) / BN, (p.M + BM - 1) / BM, p.B * p.nh * std::max(p.kslices, 1));
   hipLaunchKernelGGL((conv_gemm_kernel<T, MT, NT, WM, WN, CK>), grid, dim3(64 * WM * WN), lds, s, p);
   return hipGetLastError();
+}
+
+// fp32 split-K: slices of >= 64 input channels (every tap of them), at most 16, dividing the
+// 16-channel chunk count -- from Cin only (ConvParams::f32_splitk), so layers that differ only in
+// zero-padded taps (the batched variance predictors) still sum in the same order.  At batch 1 (C1)
+// the fp32 acoustic model's FFN convs ran on 3 (encoder) / 12 (decoder) blocks of 128 x 128 for
+// 565 us each, every block walking K = 4608 chunk by chunk with one HBM round trip per chunk.
+int f32_kslices(int taps, int Cin) {
+  const int nch = (Cin + 15) / 16;
+  int S = taps > 0 ? std::min(16, Cin / 64) : 1;
+  while (S > 1 && nch % S) --S;
+  return std::max(S, 1);
+}
+
+long long f32_splitk_ws_bytes(int taps, int Cin, int M, long long rows) {
+  const int S = f32_kslices(taps, Cin);
+  return S > 1 ? (long long)S * rows * M * 4 : 0;
+}
+
+static thread_local int g_f32sk_kernels = 0;
+
+// the split-K form of an fp32 launch, or false when p does not take it
+static bool launch_f32_splitk(const ConvParams& p, hipStream_t s, hipError_t* e, bool* ln_done) {
+  if (!p.f32_splitk || p.up_s || p.nh != 1 || p.xres_order || p.M <= 64) return false;
+  const int S = f32_kslices(p.taps, p.Cin);
+  if (S <= 1) return false;
+  g_f32sk_kernels = 0;
+  if (!p.ws || (long long)S * p.B * p.y_rows * p.M * 4 > p.ws_bytes) {  // the caller sized ws for its layers
+    *e = hipErrorInvalidValue;
+    return true;
+  }
+  ConvParams q = p;
+  q.kslices = S;
+  *e = launch_cfg<float, 1, 4, 4, 1, 16>(q, s);
+  if (*e != hipSuccess) return true;
+  ConvParams r = p;
+  r.x_rows = p.y_rows;  // the partials' rows per utterance
+  *e = split_reduce_launch(r, S, s, ln_done);
+  g_f32sk_kernels = 2;
+  return true;
 }
 
 template <typename T>
@@ -1140,9 +1206,12 @@ int conv_gemm_kind(int dtype, const ConvParams& p) {
 
 static hipError_t conv_gemm_launch_noln(int dtype, const ConvParams& p, hipStream_t s, bool* ln_done) {
   switch (dtype) {
-    case DT_F32:
+    case DT_F32: {
       if (conv_split_eligible(p)) return conv_split_launch(p, s, ln_done);
+      hipError_t e;
+      if (launch_f32_splitk(p, s, &e, ln_done)) return e;
       return launch_t<float>(p, s);
+    }
     case DT_F16: {
       hipError_t e;
       if (conv_mt_eligible(dtype, p)) return conv_mt_launch(dtype, p, s, ln_done);
@@ -1167,6 +1236,7 @@ hipError_t conv_gemm_launch(int dtype, const ConvParams& p, hipStream_t s) {
   g_conv_kernels = 1;
   const hipError_t e = conv_gemm_launch_noln(dtype, p, s, &ln_done);
   if (dtype == DT_F32 && conv_split_eligible(p)) g_conv_kernels = conv_split_last_kernels();
+  else if (dtype == DT_F32 && g_f32sk_kernels) g_conv_kernels = g_f32sk_kernels, g_f32sk_kernels = 0;
   if (e != hipSuccess || !(p.ln_out || p.ln_lin_out) || ln_done) return e;
   ++g_conv_kernels;
   // LayerNorm as its own launch over the [B][y_rows] output (contiguous rows of M); rows past an

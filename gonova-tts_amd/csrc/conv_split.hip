@@ -870,6 +870,23 @@ __global__ __launch_bounds__(256) void split_reduce_ln_kernel(ConvParams p, int 
   split_reduce_ln_row(p, S, F, f, threadIdx.x & 63);
 }
 
+// The reduce of a split-K launch whose partials are ws[S][B * p.x_rows][M] (the fp32
+// conv_gemm_kernel's slices, conv_gemm.hip; the packed form below launches the same kernels):
+// the post-LN fused when the row fits one wave and there is no activation before it
+hipError_t split_reduce_launch(const ConvParams& p, int S, hipStream_t s, bool* ln_done) {
+  const int F = p.B * p.x_rows;
+  if (ln_done) *ln_done = false;
+  if (p.ln_out && p.M <= 512 && p.act_out == ACT_NONE) {
+    hipLaunchKernelGGL(split_reduce_ln_kernel, dim3((F + 3) / 4), dim3(256), 0, s, p, S);
+    if (ln_done) *ln_done = true;
+  } else {
+    const long long n = (long long)F * (p.M / 4);
+    const unsigned g = (unsigned)std::min<long long>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(g), dim3(256), 0, s, p, S);
+  }
+  return hipGetLastError();
+}
+
 constexpr int SPLIT_LDS_MAX = 76 * 1024;  // two blocks per CU
 
 // channel group: largest power of two dividing Cin with both planes of UW utterances' rows within

@@ -85,6 +85,11 @@ struct tts_engine {
   int vlens_batch = 0;
   float* vchunk_wav = nullptr;
   size_t vchunk_elems = 0;
+  // fp32 vocoder: split-K partials of the resblock convs with >= VWS_MIN_CIN input channels
+  // (ConvParams::f32_splitk; stage 0 at C = 256 ran on 54 blocks at batch 1 -- C1)
+  static constexpr int VWS_MIN_CIN = 256;
+  float* vws = nullptr;
+  long long vws_bytes = 0;
   // polyphase resampler tables, keyed by the reduced (up, down): [up][nq] fp32 on the device
   struct Resampler { int up, down, nq, n_pre_remove; float* hp; };
   std::vector<Resampler> resamplers;
@@ -129,6 +134,7 @@ struct tts_engine {
     if (vmel) hipFree(vmel);
     if (vlens) hipFree(vlens);
     if (vchunk_wav) hipFree(vchunk_wav);
+    if (vws) hipFree(vws);
     for (auto& r : resamplers) hipFree(r.hp);
     ac.free_all();
   }
@@ -281,6 +287,21 @@ struct tts_engine {
       HIP_CHECK(hipMalloc(&vmel, mel_need * dtype_size(dt)));
       vmel_elems = mel_need;
     }
+    if (dt == DT_F32) {  // split-K partials of the fp32 resblock convs (run_conv)
+      long long wsb = 0;
+      size_t cum2 = 1;
+      for (size_t i = 0; i < voc.ups.size(); ++i) {
+        cum2 *= voc.up_rate[i];
+        const int C = voc.stage_ch[i];
+        if (C >= VWS_MIN_CIN) wsb = std::max(wsb, f32_splitk_ws_bytes(3, C, C, (long long)B * T * (long long)cum2));
+      }
+      if (wsb > vws_bytes) {
+        if (vws) hipFree(vws);
+        vws = nullptr; vws_bytes = 0;
+        HIP_CHECK(hipMalloc(&vws, (size_t)wsb));
+        vws_bytes = wsb;
+      }
+    }
     if (B > vlens_batch) {
       if (vlens) hipFree(vlens);
       vlens = nullptr; vlens_batch = 0;
@@ -316,6 +337,9 @@ struct tts_engine {
     p.in_slope = in_slope; p.out_scale = out_scale;
     p.up_s = L.up_s; p.up_cout = L.up_cout; p.up_p = L.up_p; p.up_len = up_len;
     p.B = B;
+    if (dt == DT_F32 && L.Cin >= VWS_MIN_CIN && !L.up_s && vws) {  // (a layer-shape rule: batch-independent sums)
+      p.f32_splitk = 1; p.ws = vws; p.ws_bytes = vws_bytes;
+    }
     // algorithmic FLOPs: 2 * Cout * Cin * k per produced row (transposed: per input row, all phases)
     const double fl = 2.0 * L.M * (double)L.Cin * L.taps * (double)B * (L.up_s ? (y_rows - 1) : y_rows);
     launch_conv_checked(p, dt, s, &prof, fl);

@@ -63,6 +63,14 @@ struct ConvParams {
   // a contiguous range of items), items ordered M block fastest, so the M blocks of a row tile run
   // on one XCD together and share its X tile through that L2
   int xres_order;
+  // Split-K of the fp32 conv_gemm_kernel (latency-bound small grids of the fp32 acoustic model:
+  // C1's batch-1 FFN convs ran on 3-12 blocks).  f32_splitk (caller): the launch may split its K
+  // (Cin chunks) into f32_kslices(taps, Cin) slices -- a count from the layer shape only, so a row's
+  // summation order does not depend on the batch -- writing fp32 partials to ws[S][B][y_rows][M],
+  // which split_reduce_launch sums in slice order and finishes with conv_epilogue's arithmetic.
+  // kslices: set by the launcher for the kernel (0 / 1: no split).
+  int f32_splitk;
+  int kslices;
 };
 
 inline ConvParams conv_params_default() {
@@ -97,6 +105,12 @@ hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done =
 int conv_split_last_kernels();  // kernels the calling thread's last conv_split_launch enqueued
 // split-K workspace bytes a packed-row launch of this shape over `rows` flat rows can use (0: none)
 long long conv_split_ws_bytes(int taps, int Cin, int M, int rows);
+// fp32 split-K (ConvParams::f32_splitk): slices of a layer, the partials' bytes over `rows` (B * y_rows)
+// output rows, and the reduce (p.x_rows = the partials' rows per utterance; LayerNorm fused when
+// p asks for one the reduce can apply: *ln_done)
+int f32_kslices(int taps, int Cin);
+long long f32_splitk_ws_bytes(int taps, int Cin, int M, long long rows);
+hipError_t split_reduce_launch(const ConvParams& p, int S, hipStream_t s, bool* ln_done);
 
 // Fused ResBlock pair (mrf_pair.hip): t = lrelu(conv_{k,d}(lrelu(h)) + b1);
 // h' = conv_{k,1}(t) + b2 + h;  y = ((accum ? y : 0) + h') * scale.

@@ -285,6 +285,7 @@ inline void run_layer(const ConvLayer& L, const void* x, int x_rows, const int* 
     p.ln_cnt = ln->ln_cnt; p.ln_cnt_n = ln->ln_cnt_n;
     p.ln_lin_w = ln->ln_lin_w; p.ln_lin_b = ln->ln_lin_b; p.ln_lin_out = ln->ln_lin_out;
     p.range_flag = ln->range_flag; p.no_split = ln->no_split;  // (the split path's guard / fallback)
+    p.f32_splitk = ln->f32_splitk;
   }
   launch_conv_checked(p, dt, s, prof, 2.0 * L.M * (double)L.Cin * L.taps * (double)B * y_rows);
 }

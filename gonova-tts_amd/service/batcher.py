@@ -2,8 +2,8 @@
 (`services/tts/server.py:110-186`, strictly one request in flight, one `generate` call per
 sentence).
 
-Admission: requests are taken from the input queue as they arrive (whatever arrived within
-`max_wait` of the first joins it), split into sentences with the reference's segmentation
+Admission: requests are taken from the input queue as they arrive (while every engine is busy,
+whatever arrives within `max_wait` of the first joins it; with an engine idle they go at once), split into sentences with the reference's segmentation
 (`synthesizer.py:48-99`), and their sentences join one shared work list -- up to
 `max_requests` requests in flight, new ones admitted while engines are busy.
 
@@ -84,6 +84,7 @@ class DynamicBatcher:
         self._work: List[_Item] = []
         self._seq = itertools.count()
         self._inflight = 0
+        self._idle = 0  # engine workers waiting for work
         self._cond: Optional[asyncio.Condition] = None
         self._flush_lock: Optional[asyncio.Lock] = None
         self.stats = {"rounds": 0, "engine_batches": 0, "sentences": 0, "requests": 0, "errors": 0,
@@ -108,7 +109,10 @@ class DynamicBatcher:
                 if not self.running:
                     break
                 try:
-                    reqs = await self.queues.take_batch(room, self.max_wait)
+                    # the gathering window only while every engine is busy (what arrives then is
+                    # batched by the continuous admission anyway): an idle engine starts at once,
+                    # so a lone request does not pay max_wait (C1's first-frame latency)
+                    reqs = await self.queues.take_batch(room, lambda: 0.0 if self._idle else self.max_wait)
                 except asyncio.CancelledError:
                     break
                 if reqs:
@@ -169,7 +173,11 @@ class DynamicBatcher:
     async def _engine_loop(self, eng: int, loop):
         while True:
             async with self._cond:
-                await self._cond.wait_for(lambda: bool(self._work))
+                self._idle += 1
+                try:
+                    await self._cond.wait_for(lambda: bool(self._work))
+                finally:
+                    self._idle -= 1
                 batch = self._take()
             t0 = time.perf_counter()
             try:

@@ -113,12 +113,13 @@ class TTSQueueManager:
         except asyncio.TimeoutError:
             return None
 
-    async def take_batch(self, max_items: int, max_wait: float, first_timeout: float = 1.0) -> List[SynthesisRequest]:
+    async def take_batch(self, max_items: int, max_wait, first_timeout: float = 1.0) -> List[SynthesisRequest]:
+        """`max_wait`: seconds, or a callable giving them once the first request is in."""
         first = await self.get_next_request(first_timeout)
         if first is None:
             return []
         batch = [first]
-        deadline = time.monotonic() + max_wait
+        deadline = time.monotonic() + (max_wait() if callable(max_wait) else max_wait)
         while len(batch) < max_items:
             try:
                 batch.append(self.input_queue.get_nowait())

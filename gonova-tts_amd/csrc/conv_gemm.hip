@@ -1105,13 +1105,19 @@ static hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifndef TTS_F32_CK
+#define TTS_F32_CK 16  // fp32 channel chunk (A/B builds: 32 -- half the staging rounds and barriers)
+#endif
+static int f32_ck(int Cin) { return Cin % TTS_F32_CK == 0 ? TTS_F32_CK : 16; }
+
 // fp32 split-K: slices of >= 64 input channels (every tap of them), at most 16, dividing the
 // 16-channel chunk count -- from Cin only (ConvParams::f32_splitk), so layers that differ only in
 // zero-padded taps (the batched variance predictors) still sum in the same order.  At batch 1 (C1)
 // the fp32 acoustic model's FFN convs ran on 3 (encoder) / 12 (decoder) blocks of 128 x 128 for
 // 565 us each, every block walking K = 4608 chunk by chunk with one HBM round trip per chunk.
 int f32_kslices(int taps, int Cin) {
-  const int nch = (Cin + 15) / 16;
+  const int ck = f32_ck(Cin);
+  const int nch = (Cin + ck - 1) / ck;
   int S = taps > 0 ? std::min(16, Cin / 64) : 1;
   while (S > 1 && nch % S) --S;
   return std::max(S, 1);
@@ -1136,7 +1142,7 @@ static bool launch_f32_splitk(const ConvParams& p, hipStream_t s, hipError_t* e,
   }
   ConvParams q = p;
   q.kslices = S;
-  *e = launch_cfg<float, 1, 4, 4, 1, 16>(q, s);
+  *e = f32_ck(p.Cin) == 16 ? launch_cfg<float, 1, 4, 4, 1, 16>(q, s) : launch_cfg<float, 1, 4, 4, 1, TTS_F32_CK>(q, s);
   if (*e != hipSuccess) return true;
   ConvParams r = p;
   r.x_rows = p.y_rows;  // the partials' rows per utterance
@@ -1148,6 +1154,12 @@ static bool launch_f32_splitk(const ConvParams& p, hipStream_t s, hipError_t* e,
 template <typename T>
 static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
   constexpr int CKW = 64 / (int)sizeof(T);   // 32 x 16-bit / 16 x f32 (64-byte rows)
+  if constexpr (sizeof(T) == 4 && TTS_F32_CK != 16)
+    if (p.nh == 1 && f32_ck(p.Cin) == TTS_F32_CK) {
+      if (p.M <= 32) return launch_cfg<T, 1, 2, 1, 4, TTS_F32_CK>(p, s);
+      if (p.M <= 64) return launch_cfg<T, 1, 2, 2, 2, TTS_F32_CK>(p, s);
+      return launch_cfg<T, 1, 4, 4, 1, TTS_F32_CK>(p, s);
+    }
   // fp32 head-batched attention products of the exact-duration encoder (M = 144-288 keys /
   // 192 channels, K = 144-192, 144 query rows, batch x heads): when the 128 x 128 grid would
   // fill under half the CUs (batch 8: 64 blocks), 64 x 64 tiles with 128-byte channel chunks,

@@ -3,7 +3,8 @@
 sentence).
 
 Admission: requests are taken from the input queue as they arrive (while every engine is busy,
-whatever arrives within `max_wait` of the first joins it; with an engine idle they go at once), split into sentences with the reference's segmentation
+whatever arrives within `max_wait` of the first joins it; with an engine idle, within `idle_wait`,
+default 0: at once), split into sentences with the reference's segmentation
 (`synthesizer.py:48-99`), and their sentences join one shared work list -- up to
 `max_requests` requests in flight, new ones admitted while engines are busy.
 
@@ -67,7 +68,7 @@ class DynamicBatcher:
                  max_requests: int = 64, max_wait: float = 0.004, notify_errors: bool = False,
                  send_error: Optional[Callable] = None, synth_stream: Optional[Callable] = None,
                  sample_rate: int = 22050, synth_batches: Optional[List[Callable]] = None,
-                 synth_streams: Optional[List[Optional[Callable]]] = None):
+                 synth_streams: Optional[List[Optional[Callable]]] = None, idle_wait: float = 0.0):
         self.queues = queues
         self.sample_rate = float(sample_rate)  # the rate the engine's audio is in (model.sr)
         self.synth_batch = synth_batch
@@ -78,6 +79,7 @@ class DynamicBatcher:
         self.max_sentences = max_sentences
         self.max_requests = max_requests
         self.max_wait = max_wait
+        self.idle_wait = idle_wait  # the window while an engine is idle (0: start at once)
         self.notify_errors = notify_errors
         self.send_error = send_error
         self.running = False
@@ -112,7 +114,7 @@ class DynamicBatcher:
                     # the gathering window only while every engine is busy (what arrives then is
                     # batched by the continuous admission anyway): an idle engine starts at once,
                     # so a lone request does not pay max_wait (C1's first-frame latency)
-                    reqs = await self.queues.take_batch(room, lambda: 0.0 if self._idle else self.max_wait)
+                    reqs = await self.queues.take_batch(room, lambda: self.idle_wait if self._idle else self.max_wait)
                 except asyncio.CancelledError:
                     break
                 if reqs:

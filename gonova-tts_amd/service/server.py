@@ -71,7 +71,8 @@ class TTSService:
     def __init__(self, model_factory: Callable, max_connections: int = 50, chunk_size: int = 50,
                  max_sentences: int = 32, max_wait: float = 0.004, notify_errors: bool = False,
                  device: str = "cuda", device_index: int = 0, stream_frames: int = 0,
-                 min_stream_frames: int = MIN_STREAM_FRAMES, devices: Optional[list] = None):
+                 min_stream_frames: int = MIN_STREAM_FRAMES, devices: Optional[list] = None,
+                 idle_wait: float = 0.0):
         """devices: opt-in fan-out over the node's GPUs, e.g. ["cuda:0", "cuda:1"]: model_factory is
         then called once per device (model_factory(device)) and each engine pulls its next batch from
         the batcher's shared work list whenever it is free (batcher.py); default None = one model_factory() model, the
@@ -94,6 +95,7 @@ class TTSService:
         self.voice_info = {}  # voice_id -> description
         self.max_sentences = max_sentences
         self.max_wait = max_wait
+        self.idle_wait = idle_wait  # the gathering window while an engine is idle (batcher.py)
         self.notify_errors = notify_errors
         self.min_stream_frames = max(1, int(min_stream_frames))
         self.stream_frames = self._stream_frames(stream_frames)
@@ -116,7 +118,8 @@ class TTSService:
         self.queues = TTSQueueManager(sample_rate=sr)
         await self.queues.start()
         self.batcher = DynamicBatcher(self.queues, self.model.generate_batch, max_sentences=self.max_sentences,
-                                      max_wait=self.max_wait, notify_errors=self.notify_errors,
+                                      max_wait=self.max_wait, idle_wait=self.idle_wait,
+                                      notify_errors=self.notify_errors,
                                       send_error=self._send_error,
                                       synth_stream=getattr(self.model, "stream_batch", None), sample_rate=sr,
                                       synth_batches=[m.generate_batch for m in self.models],

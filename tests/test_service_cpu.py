@@ -106,6 +106,20 @@ def test_concurrent_connections_are_batched_together():
     assert max(len(b) for b in model.batches) > 2  # sentences of different connections shared an engine pass
 
 
+def test_lone_request_does_not_wait_for_the_gathering_window():
+    """With the engine idle a request starts at once (idle_wait, default 0): max_wait only gathers
+    while every engine is busy, so a lone sentence is not delayed by it (C1's first frame)."""
+    app = create_app(lambda: FakeModel(), max_wait=1.0)
+    with TestClient(app) as c:
+        with c.websocket_connect("/v1/stream/tts") as ws:
+            t0 = time.perf_counter()
+            ws.send_text(json.dumps({"type": "synthesize", "text": "Just one sentence."}))
+            frames, final = recv_until_complete(ws)
+            dt = time.perf_counter() - t0
+    assert len(frames) == 1 and final["chunk_id"] == 1
+    assert dt < 0.5, dt
+
+
 def test_failure_follows_reference_by_default_and_notifies_when_asked():
     app = create_app(lambda: FakeModel(fail_on="bad"), notify_errors=True)
     with TestClient(app) as c:

@@ -50,7 +50,7 @@ def served():
         holder["m"] = GonovaTTS.from_pretrained("cuda:0", vocoder_dtype="f32", acoustic_dtype="f32")
         return holder["m"]
 
-    app = create_app(factory, max_wait=0.25)
+    app = create_app(factory, max_wait=0.25, idle_wait=0.25)  # (the batching tests gather while idle too)
     with TestClient(app) as c:
         yield c, holder["m"]
 
@@ -142,7 +142,7 @@ def test_two_engines_continuous_batcher_real_engine():
         made.append(GonovaTTS.from_pretrained(device, vocoder_dtype="f32", acoustic_dtype="f32"))
         return made[-1]
 
-    app = create_app(factory, devices=["cuda:0", "cuda:0"], max_wait=0.2, max_sentences=2)
+    app = create_app(factory, devices=["cuda:0", "cuda:0"], max_wait=0.2, idle_wait=0.2, max_sentences=2)
     texts = {0: "Good morning. The quick brown fox jumps. Over the lazy dog!",
              1: "A second client speaks. Then it stops! And starts again.",
              2: "Streaming here. In small pieces please."}

@@ -1207,6 +1207,13 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why) {
   if (p.up_s && (p.up_cout % 4 || !p.up_len)) { *why = "bad transposed mapping"; return -1; }
   if (p.x_rows <= 0 || p.y_rows <= 0) { *why = "empty rows"; return -1; }
   if (p.nh < 1 || p.sxh % epv || p.swh % epv || p.syh % 4 || p.srh % 4) { *why = "bad head batching"; return -1; }
+  if (dtype == DT_F32 && p.f32_splitk && !p.up_s && p.nh == 1 && !p.xres_order && p.M > 64 && !conv_split_eligible(p)) {
+    const int S = f32_kslices(p.taps, p.Cin);
+    if (S > 1 && (!p.ws || (long long)S * p.B * p.y_rows * p.M * 4 > p.ws_bytes)) {
+      *why = "fp32 split-K workspace smaller than this layer's partials (reserve with the caller's batch / rows)";
+      return -1;
+    }
+  }
   return 0;
 }
 

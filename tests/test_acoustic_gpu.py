@@ -101,6 +101,22 @@ def test_acoustic_fp32_ragged_batch_matches_oracle(aw):
         np.testing.assert_allclose(mel[b, :L], ref["mel"][:L], atol=FP32_ATOL, rtol=FP32_RTOL)
 
 
+def test_acoustic_fp32_split_k_batch_invariant(aw):
+    """The fp32 model's GEMMs split K on a workspace with a slice count from the layer shape only
+    (conv_gemm.hip f32_kslices): an utterance's durations and mel are bit-identical whether it runs
+    alone (batch-1 grids: the split-K form) or inside a ragged batch of four."""
+    eng = engine("f32", aw)
+    rng = np.random.default_rng(17)
+    ids_list = [rng.integers(1, 78, size=n) for n in (41, 9, 71, 26)]
+    mel, mel_lens, dur = run(eng, ids_list, t_cap=12 * 71)
+    for b, ids in enumerate(ids_list):
+        m1, l1, d1 = run(eng, [ids], t_cap=12 * 71)
+        assert int(l1[0]) == int(mel_lens[b])
+        assert np.array_equal(d1[0, :len(ids)], dur[b, :len(ids)])
+        L = int(l1[0])
+        assert np.array_equal(m1[0, :L], mel[b, :L]), b
+
+
 def test_acoustic_duration_override_and_cap(aw):
     eng = engine("f32", aw)
     rng = np.random.default_rng(9)

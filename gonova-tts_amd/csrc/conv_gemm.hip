@@ -1105,12 +1105,15 @@ static hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifndef TTS_F32_SLICE_CH
+#define TTS_F32_SLICE_CH 32  // fp32 split-K: input channels per slice at least (C1: 32 beat 64, profiles/r05zm)
+#endif
 #ifndef TTS_F32_CK
 #define TTS_F32_CK 16  // fp32 channel chunk (A/B builds: 32 -- half the staging rounds and barriers)
 #endif
 static int f32_ck(int Cin) { return Cin % TTS_F32_CK == 0 ? TTS_F32_CK : 16; }
 
-// fp32 split-K: slices of >= 64 input channels (every tap of them), at most 16, dividing the
+// fp32 split-K: slices of >= TTS_F32_SLICE_CH input channels (every tap of them), at most 16, dividing the
 // 16-channel chunk count -- from Cin only (ConvParams::f32_splitk), so layers that differ only in
 // zero-padded taps (the batched variance predictors) still sum in the same order.  At batch 1 (C1)
 // the fp32 acoustic model's FFN convs ran on 3 (encoder) / 12 (decoder) blocks of 128 x 128 for
@@ -1118,7 +1121,7 @@ static int f32_ck(int Cin) { return Cin % TTS_F32_CK == 0 ? TTS_F32_CK : 16; }
 int f32_kslices(int taps, int Cin) {
   const int ck = f32_ck(Cin);
   const int nch = (Cin + ck - 1) / ck;
-  int S = taps > 0 ? std::min(16, Cin / 64) : 1;
+  int S = taps > 0 ? std::min(16, Cin / TTS_F32_SLICE_CH) : 1;
   while (S > 1 && nch % S) --S;
   return std::max(S, 1);
 }

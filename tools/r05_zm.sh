@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 5: fp32 split-K slices of >= 64 input channels (product) vs >= 32 (TTS_F32_SLICE_CH=32 variant): fp32 GPU tests on the variant, then the C1 probe alternated
+set -o pipefail
+R=$GRAFT_REPO_ROOT; T=$1; O=$R/gpurun_out/$T; mkdir -p $O; cd $R
+V=$R/gonova-tts_amd/libtts_hip_sl32.so
+TTS_LIB=$V timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu -k "fp32 or f32 or model" tests/ > $O/gputest_sl32.log 2>&1 || { tail -30 $O/gputest_ck32.log; exit 1; }
+tail -1 $O/gputest_sl32.log
+cd /tmp
+for rep in 1 2; do
+  for v in base sl32; do
+    L=$R/gonova-tts_amd/libtts_hip.so; [ $v = sl32 ] && L=$V
+    TTS_LIB=$L timeout -k 10 300 python3 $R/tools/c1_prof.py > $O/c1.$v.$rep.txt 2>&1 || { tail -5 $O/c1.$v.$rep.txt; exit 1; }
+    echo "$v $rep $(tail -1 $O/c1.$v.$rep.txt)"
+  done
+done
+echo r05zm done

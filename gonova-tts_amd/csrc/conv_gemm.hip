@@ -1105,6 +1105,9 @@ static hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifndef TTS_F32_SK_MINM
+#define TTS_F32_SK_MINM 64  // fp32 split-K only above this many output channels (A/B builds: 32 -- C1's stage-2 convs)
+#endif
 #ifndef TTS_F32_SLICE_CH
 #define TTS_F32_SLICE_CH 32  // fp32 split-K: input channels per slice at least (C1: 32 beat 64, profiles/r05zm)
 #endif
@@ -1135,7 +1138,7 @@ static thread_local int g_f32sk_kernels = 0;
 
 // the split-K form of an fp32 launch, or false when p does not take it
 static bool launch_f32_splitk(const ConvParams& p, hipStream_t s, hipError_t* e, bool* ln_done) {
-  if (!p.f32_splitk || p.up_s || p.nh != 1 || p.xres_order || p.M <= 64) return false;
+  if (!p.f32_splitk || p.up_s || p.nh != 1 || p.xres_order || p.M <= TTS_F32_SK_MINM) return false;
   const int S = f32_kslices(p.taps, p.Cin);
   if (S <= 1) return false;
   g_f32sk_kernels = 0;
@@ -1145,7 +1148,10 @@ static bool launch_f32_splitk(const ConvParams& p, hipStream_t s, hipError_t* e,
   }
   ConvParams q = p;
   q.kslices = S;
-  *e = f32_ck(p.Cin) == 16 ? launch_cfg<float, 1, 4, 4, 1, 16>(q, s) : launch_cfg<float, 1, 4, 4, 1, TTS_F32_CK>(q, s);
+  if (p.M <= 64)  // (launch_t's M <= 64 tile)
+    *e = launch_cfg<float, 1, 2, 2, 2, 16>(q, s);
+  else
+    *e = f32_ck(p.Cin) == 16 ? launch_cfg<float, 1, 4, 4, 1, 16>(q, s) : launch_cfg<float, 1, 4, 4, 1, TTS_F32_CK>(q, s);
   if (*e != hipSuccess) return true;
   ConvParams r = p;
   r.x_rows = p.y_rows;  // the partials' rows per utterance
@@ -1210,7 +1216,7 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why) {
   if (p.up_s && (p.up_cout % 4 || !p.up_len)) { *why = "bad transposed mapping"; return -1; }
   if (p.x_rows <= 0 || p.y_rows <= 0) { *why = "empty rows"; return -1; }
   if (p.nh < 1 || p.sxh % epv || p.swh % epv || p.syh % 4 || p.srh % 4) { *why = "bad head batching"; return -1; }
-  if (dtype == DT_F32 && p.f32_splitk && !p.up_s && p.nh == 1 && !p.xres_order && p.M > 64 && !conv_split_eligible(p)) {
+  if (dtype == DT_F32 && p.f32_splitk && !p.up_s && p.nh == 1 && !p.xres_order && p.M > TTS_F32_SK_MINM && !conv_split_eligible(p)) {
     const int S = f32_kslices(p.taps, p.Cin);
     if (S > 1 && (!p.ws || (long long)S * p.B * p.y_rows * p.M * 4 > p.ws_bytes)) {
       *why = "fp32 split-K workspace smaller than this layer's partials (reserve with the caller's batch / rows)";

@@ -87,7 +87,10 @@ struct tts_engine {
   size_t vchunk_elems = 0;
   // fp32 vocoder: split-K partials of the resblock convs with >= VWS_MIN_CIN input channels
   // (ConvParams::f32_splitk; at batch 1 -- C1 -- stage 0 at C = 256 ran on 54 blocks, stage 1 on 213)
-  static constexpr int VWS_MIN_CIN = 128;
+#ifndef TTS_VWS_MIN_CIN
+#define TTS_VWS_MIN_CIN 128
+#endif
+  static constexpr int VWS_MIN_CIN = TTS_VWS_MIN_CIN;  // (A/B builds: 64 with TTS_F32_SK_MINM=32)
   float* vws = nullptr;
   long long vws_bytes = 0;
   // polyphase resampler tables, keyed by the reduced (up, down): [up][nq] fp32 on the device

@@ -143,8 +143,9 @@ def test_c4_sharded_batch256_matches_solo_and_oracle():
     """C4 itself (BASELINE.json configs[3]): 256 utterances of N_i ~ U{29..144} tokens x 6
     frames, length buckets of 64, bf16, through dist.ShardedSynthesis exactly as bench.py runs
     it -- once inside an RCCL process group (backend "nccl" = RCCL, one rank on this 1-GPU box:
-    the token broadcast and the size all-gather run as RCCL collectives; the P2P gather has no
-    peer here, tests/test_dist_cpu.py covers it with gloo ranks) and once with no group.
+    the token broadcast runs as an RCCL collective and the gather's CPU metadata group is created;
+    the P2P gather has no peer here, tests/test_dist_cpu.py covers it with gloo ranks) and once
+    with no group.
     Checks: every utterance returns at 6 * 256 * N_i samples, both runs agree bit for bit,
     8 utterances (shortest, longest and 6 between) equal the same utterance synthesized alone
     bit for bit, and 2 match the oracle on 2 s windows."""

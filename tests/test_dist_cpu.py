@@ -2,6 +2,7 @@
 bookkeeping: plan, token broadcast, packed P2P gather, original order restored."""
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -79,6 +80,47 @@ def test_sharded_gather_restores_order(world, empties):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert q.get(timeout=10) is True
+
+
+def _slow_worker(rank, world, port, q, slow_rank):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tok, lens = make_batch()
+
+        def synth(t, l):
+            if rank == slow_rank:
+                time.sleep(1.5)
+            return fake_synth(t, l)
+
+        sh = ShardedSynthesis(synth, torch.device("cpu"), bucket=16)
+        out = sh.run(tok if rank == 0 else None, lens if rank == 0 else None)
+        if rank == 0:
+            ok = all(o is not None and np.array_equal(o, e) for o, e in zip(out, expected(tok, lens)))
+            q.put((ok, sh.arrivals))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_unpacks_each_peer_as_it_arrives():
+    """the root receives every peer on its own and unpacks a peer as soon as
+    its audio is in -- a slow last peer (1.5 s late) does not hold the earlier peers back."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 4
+    procs = [ctx.Process(target=_slow_worker, args=(r, world, port, q, world - 1)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ok, arrivals = q.get(timeout=10)
+    assert ok
+    t = {(r, what): at for r, what, at in arrivals}
+    assert set(t) == {(r, w) for r in (1, 2, 3) for w in ("header", "unpacked")}
+    for r in (1, 2):
+        assert t[(r, "unpacked")] < t[(3, "header")] - 0.5, arrivals
 
 
 def test_plan_is_balanced_and_complete():

@@ -30,7 +30,12 @@ TARGETS = {  # (M, Cin, taps, workload)
     "e_pw1": (768, 384, 1, "acoustic8"),
     "e_ffn_up": (1536, 384, 3, "acoustic8"),
     "e_ffn_down": (384, 1536, 3, "acoustic8"),
+    # the same split GEMMs in a batch-32 forward (C3)
+    "E_qkv": (1152, 384, 1, "acoustic32s"),
+    "E_ffn_up": (1536, 384, 3, "acoustic32s"),
+    "E_ffn_down": (384, 1536, 3, "acoustic32s"),
 }
+WARM_S = float(os.environ.get("STAMP_WARM_S", "0"))  # back-to-back steps before the recorded one (clock settles)
 
 
 def run(which):
@@ -39,7 +44,7 @@ def run(which):
     from gonova_tts_amd.weights import make_acoustic_weights, make_vocoder_weights
     M, Cin, taps, wl = TARGETS[which]
     lib = load_library()
-    kind = "split" if wl == "acoustic8" else "xres"
+    kind = "split" if wl in ("acoustic8", "acoustic32s") else "xres"
     set_target = getattr(lib, f"tts_debug_{kind}_target")
     read = getattr(lib, f"tts_debug_{kind}_stamps")
     set_target.argtypes = [ctypes.c_int] * 3
@@ -59,6 +64,12 @@ def run(which):
         mel = torch.randn((32, 862, 80), generator=g).cuda()
         wav = torch.empty((32, 862 * 256), device="cuda")
         step = lambda: eng.vocoder(mel, out=wav)  # noqa: E731
+    import time
+    t0 = time.time()
+    while time.time() - t0 < WARM_S:
+        for _ in range(8):
+            step()
+        torch.cuda.synchronize()
     for _ in range(4):
         step()
     torch.cuda.synchronize()

@@ -150,9 +150,9 @@ struct AcousticModel::Impl {
   int h_lens_n = 0;
 
   ~Impl() {
-    for (void* p : allocs) hipFree(p);
-    for (void* p : ws) hipFree(p);
-    for (void* p : score_ws) hipFree(p);
+    for (void* p : allocs) dev_free(p);
+    for (void* p : ws) dev_free(p);
+    for (void* p : score_ws) dev_free(p);
     if (h_lens) hipHostFree(h_lens);
   }
 
@@ -326,24 +326,24 @@ struct AcousticModel::Impl {
     for (auto* stack : {&enc, &dec})
       for (auto& L : *stack) {
         if (L.ptab) {
-          hipFree(L.ptab);
+          dev_free(L.ptab);
           for (auto& a : allocs) if (a == L.ptab) a = nullptr;
         }
         if (!ped[L.dt]) ped[L.dt] = upload(pe, L.dt);
         void* t = nullptr;
-        HIP_CHECK(hipMalloc(&t, (size_t)rows * D * dtype_size(L.dt)));
+        HIP_CHECK(dev_malloc(&t, (size_t)rows * D * dtype_size(L.dt)));
         L.ptab = track(t);
         run_layer(L.pos, ped[L.dt], rows, nullptr, L.ptab, rows, 1, L.dt, s, nullptr);
       }
     HIP_CHECK(hipStreamSynchronize(s));
-    for (void* p : ped) if (p) hipFree(p);
+    for (void* p : ped) if (p) dev_free(p);
     rmax = new_rmax;
   }
 
   // ---------------------------------------------------------------- workspace
   void* alloc_ws(size_t elems, size_t esz) {
     void* p = nullptr;
-    HIP_CHECK(hipMalloc(&p, std::max<size_t>(elems, 1) * esz));
+    HIP_CHECK(dev_malloc(&p, std::max<size_t>(elems, 1) * esz));
     HIP_CHECK(hipMemset(p, 0, std::max<size_t>(elems, 1) * esz));
     ws.push_back(p);
     return p;
@@ -362,7 +362,7 @@ struct AcousticModel::Impl {
     split_ws_bytes = 0;
     std::vector<void*> old;
     old.swap(ws);
-    for (void* p : old) hipFree(p);
+    for (void* p : old) dev_free(p);
     drop_scores();
   }
 
@@ -375,7 +375,7 @@ struct AcousticModel::Impl {
     AC = BD = P = nullptr;
     std::vector<void*> old;
     old.swap(score_ws);
-    for (void* p : old) hipFree(p);
+    for (void* p : old) dev_free(p);
   }
   void reserve_scores(int B, int Tm) {
     if (B <= cap_sB && Tm <= cap_sTm) return;
@@ -604,7 +604,7 @@ struct AcousticModel::Impl {
       elem(s, [&] { return launch_spk_bias(dte, spk, B, E, proj_we, proj_b, D, SPK, s); });
       ConvParams p = conv_params_default();
       p.x = ENC; p.sxb = (long long)Np * D; p.sxr = D; p.x_len = tok_lens; p.x_rows = Np;
-      p.w = proj_h.w; p.w_ld = D; p.bias = nullptr; p.wpk = proj_h.wpk;
+      p.w = proj_h.w; p.w_ld = D; p.bias = nullptr; p.wpk = proj_h.wpk; p.w_unscale = proj_h.wpk_unscale;
       p.y = Y; p.syb = (long long)Np * D; p.syr = D;
       p.r1 = SPK; p.srb = D; p.srr = 0;  // the utterance's term broadcast over its frames
       p.y_len = tok_lens; p.y_rows = Np;
@@ -761,7 +761,7 @@ void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtyp
   m->build_ptabs(1024, nullptr);
   {
     void* f = nullptr;
-    HIP_CHECK(hipMalloc(&f, 16));
+    HIP_CHECK(dev_malloc(&f, 16));
     HIP_CHECK(hipMemset(f, 0, 16));
     m->range_flag = (int*)m->track(f);
   }

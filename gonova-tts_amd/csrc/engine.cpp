@@ -132,13 +132,13 @@ struct tts_engine {
   ~tts_engine() {
     hipSetDevice(device);
     if (order_ev) hipEventDestroy(order_ev);
-    for (void* p : allocs) hipFree(p);
-    for (void*& p : vbuf) if (p) hipFree(p);
-    if (vmel) hipFree(vmel);
-    if (vlens) hipFree(vlens);
-    if (vchunk_wav) hipFree(vchunk_wav);
-    if (vws) hipFree(vws);
-    for (auto& r : resamplers) hipFree(r.hp);
+    for (void* p : allocs) dev_free(p);
+    for (void*& p : vbuf) if (p) dev_free(p);
+    if (vmel) dev_free(vmel);
+    if (vlens) dev_free(vlens);
+    if (vchunk_wav) dev_free(vchunk_wav);
+    if (vws) dev_free(vws);
+    for (auto& r : resamplers) dev_free(r.hp);
     ac.free_all();
   }
 
@@ -270,13 +270,13 @@ struct tts_engine {
     const size_t need = (size_t)B * T * per_frame;
     const int dt = cfg.vocoder_dtype;
     if (need > vbuf_elems) {
-      for (void*& p : vbuf) { if (p) hipFree(p); p = nullptr; }
+      for (void*& p : vbuf) { if (p) dev_free(p); p = nullptr; }
       vbuf_elems = 0;
       for (void*& p : vbuf) {
-        if (hipMalloc(&p, need * dtype_size(dt)) != hipSuccess) {
+        if (dev_malloc(&p, need * dtype_size(dt)) != hipSuccess) {
           (void)hipGetLastError();
           p = nullptr;
-          for (void*& q : vbuf) { if (q) hipFree(q); q = nullptr; }  // release the partial set
+          for (void*& q : vbuf) { if (q) dev_free(q); q = nullptr; }  // release the partial set
           throw TtsError(TTS_ERR_HIP, "vocoder workspace: hipMalloc of " + std::to_string(need * dtype_size(dt)) +
                                           " bytes failed");
         }
@@ -285,9 +285,9 @@ struct tts_engine {
     }
     const size_t mel_need = (size_t)B * T * voc.conv_pre.Cin;
     if (mel_need > vmel_elems) {
-      if (vmel) hipFree(vmel);
+      if (vmel) dev_free(vmel);
       vmel = nullptr; vmel_elems = 0;
-      HIP_CHECK(hipMalloc(&vmel, mel_need * dtype_size(dt)));
+      HIP_CHECK(dev_malloc(&vmel, mel_need * dtype_size(dt)));
       vmel_elems = mel_need;
     }
     if (dt == DT_F32) {  // split-K partials of the fp32 resblock convs (run_conv)
@@ -299,16 +299,16 @@ struct tts_engine {
         if (C >= VWS_MIN_CIN) wsb = std::max(wsb, f32_splitk_ws_bytes(3, C, C, (long long)B * T * (long long)cum2));
       }
       if (wsb > vws_bytes) {
-        if (vws) hipFree(vws);
+        if (vws) dev_free(vws);
         vws = nullptr; vws_bytes = 0;
-        HIP_CHECK(hipMalloc(&vws, (size_t)wsb));
+        HIP_CHECK(dev_malloc(&vws, (size_t)wsb));
         vws_bytes = wsb;
       }
     }
     if (B > vlens_batch) {
-      if (vlens) hipFree(vlens);
+      if (vlens) dev_free(vlens);
       vlens = nullptr; vlens_batch = 0;
-      HIP_CHECK(hipMalloc(&vlens, sizeof(int) * 16 * B));
+      HIP_CHECK(dev_malloc(&vlens, sizeof(int) * 16 * B));
       vlens_batch = B;
     }
   }
@@ -319,8 +319,8 @@ struct tts_engine {
     if (need <= vchunk_elems) return;
     float* old = vchunk_wav;
     vchunk_wav = nullptr; vchunk_elems = 0;
-    if (old) HIP_CHECK(hipFree(old));
-    HIP_CHECK(hipMalloc(&vchunk_wav, need * 4));
+    if (old) HIP_CHECK(dev_free(old));
+    HIP_CHECK(dev_malloc(&vchunk_wav, need * 4));
     vchunk_elems = need;
   }
 
@@ -565,6 +565,12 @@ int tts_device_count(void) {
 }
 
 int tts_abi_version(void) { return TTS_ABI_VERSION; }
+
+int tts_device_bytes(int hip_device, int64_t* bytes) {
+  if (!bytes) return TTS_ERR_INVALID;
+  *bytes = (int64_t)tts::dev_bytes(hip_device);
+  return 0;
+}
 
 int tts_engine_create(int hip_device, const tts_config* cfg, tts_engine** out) {
   return tts_engine_create_sized(hip_device, cfg, cfg ? sizeof(tts_config) : 0, out);

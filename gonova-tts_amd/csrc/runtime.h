@@ -7,8 +7,10 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/tts_hip.h"
@@ -36,6 +38,53 @@ struct TtsError : std::runtime_error {
 
 inline size_t dtype_size(int dt) { return dt == DT_F32 ? 4 : 2; }
 
+// Device memory the library holds (weights, workspaces), per HIP device: every device buffer is
+// allocated through dev_malloc and released through dev_free, which keep a registry of live
+// buffers (tts_device_bytes, the service's /health "gpu" report; the reference reads only
+// torch's allocator there, server.py:456-465, which never sees these buffers).
+struct DevRegistry {
+  std::mutex mu;
+  std::unordered_map<void*, std::pair<int, size_t>> live;  // buffer -> (device, bytes)
+  std::unordered_map<int, long long> bytes;                // device -> live bytes
+};
+inline DevRegistry& dev_registry() {
+  static DevRegistry r;
+  return r;
+}
+template <typename T>
+inline hipError_t dev_malloc(T** p, size_t n) {
+  void* q = nullptr;
+  const hipError_t e = hipMalloc(&q, n);
+  if (e != hipSuccess) return e;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  DevRegistry& r = dev_registry();
+  std::lock_guard<std::mutex> g(r.mu);
+  r.live[q] = {dev, n};
+  r.bytes[dev] += (long long)n;
+  *p = static_cast<T*>(q);
+  return e;
+}
+inline hipError_t dev_free(void* p) {
+  if (!p) return hipSuccess;
+  {
+    DevRegistry& r = dev_registry();
+    std::lock_guard<std::mutex> g(r.mu);
+    auto it = r.live.find(p);
+    if (it != r.live.end()) {
+      r.bytes[it->second.first] -= (long long)it->second.second;
+      r.live.erase(it);
+    }
+  }
+  return hipFree(p);
+}
+inline long long dev_bytes(int dev) {
+  DevRegistry& r = dev_registry();
+  std::lock_guard<std::mutex> g(r.mu);
+  auto it = r.bytes.find(dev);
+  return it == r.bytes.end() ? 0 : it->second;
+}
+
 inline uint16_t f32_to_bf16_bits(float f) {
   uint32_t u;
   std::memcpy(&u, &f, 4);
@@ -48,7 +97,7 @@ inline uint16_t f32_to_bf16_bits(float f) {
 inline void* upload(const std::vector<float>& h, int dt) {
   void* d = nullptr;
   const size_t n = h.size();
-  HIP_CHECK(hipMalloc(&d, std::max<size_t>(n, 1) * dtype_size(dt)));
+  HIP_CHECK(dev_malloc(&d, std::max<size_t>(n, 1) * dtype_size(dt)));
   if (n == 0) return d;
   if (dt == DT_F32) {
     HIP_CHECK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
@@ -73,6 +122,7 @@ struct ConvLayer {
   void* wpk16 = nullptr;  // 16x16 fragment-packed copy (frag_pack16, MRF convs at C <= 64), or null
   void* wup16 = nullptr;  // transposed conv: [M/16][K/32][64][8] copy (frag_pack_up16), or null
   float* bias = nullptr;
+  float wpk_unscale = 1.f;  // split-packed wpk: the power of two its sums are multiplied by
   int M = 0, Cin = 0, taps = 1, dil = 1, pad = 0;
   int up_s = 0, up_cout = 0, up_p = 0;  // transposed-conv output mapping
 };
@@ -101,11 +151,23 @@ inline void* frag_pack(const std::vector<float>& w, int M, int taps, int ci, int
 }
 
 // Split-precision packing for conv_split_kernel (fp32 layers run as three f16 MFMAs):
-// frag_pack's fragment order, two f16 planes -- hi = f16(w), then lo = f16((w - hi) * 2^11).
-inline void* frag_pack_split(const std::vector<float>& w, int M, int taps, int ci, std::vector<void*>& allocs) {
+// frag_pack's fragment order, two f16 planes of the layer scaled by 2^s -- hi = f16(w 2^s), then
+// lo = f16(w 2^s - hi) -- with 2^s the power of two that puts max|w| in [2^14, 2^15): hi stays
+// finite and lo (~2^-11 of hi) in f16's normal range for every weight above ~2^-19 max|w|.  The
+// three products hi*hi + hi*lo + lo*hi then share one fp32 accumulator (no scale between the
+// terms) and the GEMM multiplies its sums by *unscale = 2^-s, an exact step.
+inline void* frag_pack_split(const std::vector<float>& w, int M, int taps, int ci, std::vector<void*>& allocs,
+                             float* unscale) {
   if (ci % 64 || M % 4) return nullptr;
   const int MB = (M + 31) / 32, KS = ci / 16;
   const size_t plane = (size_t)MB * 32 * taps * ci;
+  float mx = 0.f;
+  for (float v : w) mx = std::max(mx, std::fabs(v));
+  int e = 0;
+  if (mx > 0.f) (void)std::frexp(mx, &e);  // mx = f * 2^e, f in [0.5, 1)
+  const int s = std::max(-24, std::min(60, 15 - e));
+  const float sc = std::ldexp(1.f, s);
+  *unscale = std::ldexp(1.f, -s);
   std::vector<float> p(2 * plane, 0.f);
   size_t o = 0;
   for (int mb = 0; mb < MB; ++mb)
@@ -115,10 +177,10 @@ inline void* frag_pack_split(const std::vector<float>& w, int M, int taps, int c
           const int m = mb * 32 + (l & 31);
           for (int j = 0; j < 8; ++j, ++o) {
             if (m >= M) continue;
-            const float v = w[((size_t)m * taps + t) * ci + ks * 16 + 8 * (l >> 5) + j];
+            const float v = w[((size_t)m * taps + t) * ci + ks * 16 + 8 * (l >> 5) + j] * sc;  // exact
             const float hi = (float)(_Float16)v;
             p[o] = hi;
-            p[plane + o] = (v - hi) * 2048.f;
+            p[plane + o] = v - hi;
           }
         }
   void* d = upload(p, DT_F16);
@@ -182,7 +244,8 @@ inline ConvLayer make_conv(const std::vector<float>& w, int co, int ci, int k, c
   ConvLayer L;
   L.w = upload(p, dt);
   allocs.push_back(L.w);
-  L.wpk = (dt == DT_F32 && split) ? frag_pack_split(p, co, k, ci, allocs) : frag_pack(p, co, k, ci, dt, allocs);
+  L.wpk = (dt == DT_F32 && split) ? frag_pack_split(p, co, k, ci, allocs, &L.wpk_unscale)
+                                  : frag_pack(p, co, k, ci, dt, allocs);
   std::vector<float> b = bias;
   if (b.empty()) b.assign(co, 0.f);
   if (b.size() != (size_t)co) throw TtsError(TTS_ERR_INVALID, "conv bias size mismatch");
@@ -271,7 +334,7 @@ inline void run_layer(const ConvLayer& L, const void* x, int x_rows, const int* 
   ConvParams p = conv_params_default();
   const int xl = x_ld ? x_ld : L.Cin, yl = y_ld ? y_ld : L.M;
   p.x = x; p.sxb = (long long)x_rows * xl; p.sxr = xl; p.x_len = lens; p.x_rows = x_rows;
-  p.w = L.w; p.w_ld = L.taps * L.Cin; p.bias = L.bias; p.wpk = L.wpk;
+  p.w = L.w; p.w_ld = L.taps * L.Cin; p.bias = L.bias; p.wpk = L.wpk; p.w_unscale = L.wpk_unscale;
   p.y = y; p.syb = (long long)y_rows * yl; p.syr = yl;
   p.r1 = r1; p.r2 = r2; p.srb = p.syb; p.srr = yl;
   p.y_len = lens; p.y_rows = y_rows;

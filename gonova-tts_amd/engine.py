@@ -62,6 +62,7 @@ _VP, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 C_API = [
     ("tts_device_count", _I, []),
     ("tts_abi_version", _I, []),
+    ("tts_device_bytes", _I, [_I, ctypes.POINTER(ctypes.c_int64)]),
     ("tts_engine_create", _I, [_I, ctypes.POINTER(TtsConfig), ctypes.POINTER(_VP)]),
     ("tts_engine_create_sized", _I, [_I, ctypes.POINTER(TtsConfig), ctypes.c_size_t, ctypes.POINTER(_VP)]),
     ("tts_engine_set_weight", _I, [_VP, ctypes.c_char_p, _VP, ctypes.POINTER(ctypes.c_int64), _I]),
@@ -121,6 +122,16 @@ def resample_filter(up: int, down: int):
     lib.tts_resample_filter(up, down, h, n, ctypes.byref(npr))
     import numpy as _np
     return _np.frombuffer(h, dtype=_np.float64).copy(), npr.value
+
+
+def device_bytes(device=0) -> int:
+    """Bytes of device memory libtts_hip.so holds on a HIP device (all engines' weights and
+    workspaces; include/tts_hip.h tts_device_bytes).  A host-side count: no GPU work."""
+    lib = load_library()
+    out = ctypes.c_int64()
+    check(lib.tts_device_bytes(parse_device(device) if not isinstance(device, int) else device, ctypes.byref(out)),
+          "tts_device_bytes")
+    return int(out.value)
 
 
 def set_switch(name: str, value: int = -1):

@@ -25,6 +25,17 @@ they reach the host, still in sentence order per request.
 Failure: the reference logs and swallows synthesis errors, so the client never gets a
 final marker (`server.py:173-179`).  That stays the default; `notify_errors=True` sends
 `{"type": "synthesis_error", "message": ...}` plus the final marker instead.
+
+Stats: `get_stats()` has the reference synthesizer's keys (`synthesizer.py:140-145, 411-420`):
+`syntheses` (requests completed), `total_latency` and `first_chunk_latency` (seconds, summed; per
+request from admission -- the reference's `synthesize_streaming` start -- to its final marker and
+to its first audio frame, `synthesizer.py:274-277`), `errors` (failed requests), `avg_latency`,
+`avg_first_chunk`; plus this batcher's own counters.
+
+Delivery: each request's frames go out from a task of their own under the request's own lock
+(sentence order within the request), so a client whose output queue is full (enqueue_audio_chunk
+waits up to 0.1 s per frame) delays only itself: neither other connections' frames nor the engine's
+next batch wait behind it.
 """
 from __future__ import annotations
 
@@ -54,6 +65,9 @@ class _Request:
         self.cursor = 0     # the sentence whose pieces go out next
         self.sent = 0       # frames sent: the chunk_id of the next frame / the final marker
         self.finished = False
+        self.t_admit = time.perf_counter()
+        self.first_chunk: Optional[float] = None
+        self.lock = asyncio.Lock()  # this request's delivery order (no cross-request lock)
 
 
 class _Item:
@@ -88,18 +102,26 @@ class DynamicBatcher:
         self._inflight = 0
         self._idle = 0  # engine workers waiting for work
         self._cond: Optional[asyncio.Condition] = None
-        self._flush_lock: Optional[asyncio.Lock] = None
-        self.stats = {"rounds": 0, "engine_batches": 0, "sentences": 0, "requests": 0, "errors": 0,
+        self._flushes: set = set()  # delivery tasks in flight
+        self.stats = {"syntheses": 0, "total_latency": 0.0, "first_chunk_latency": 0.0, "errors": 0,
+                      "rounds": 0, "engine_batches": 0, "batch_errors": 0, "sentences": 0, "requests": 0,
                       "audio_seconds": 0.0, "busy_seconds": 0.0, "max_batch_seen": 0,
                       "engine_sentences": [0] * len(self.synth_batches),
                       "engine_busy_seconds": [0.0] * len(self.synth_batches)}
+
+    def get_stats(self) -> dict:
+        """The reference synthesizer's stats shape (synthesizer.py:411-420) plus this batcher's."""
+        st = dict(self.stats)
+        n = st["syntheses"]
+        st["avg_latency"] = st["total_latency"] / n if n else 0.0
+        st["avg_first_chunk"] = st["first_chunk_latency"] / n if n else 0.0
+        return st
 
     # ------------------------------------------------------------------ admission
     async def run(self):
         """Admission loop plus one worker per engine, until stop() / cancellation."""
         self.running = True
         self._cond = asyncio.Condition()
-        self._flush_lock = asyncio.Lock()
         loop = asyncio.get_running_loop()
         workers = [asyncio.create_task(self._engine_loop(e, loop)) for e in range(len(self.synth_batches))]
         try:
@@ -124,6 +146,9 @@ class DynamicBatcher:
             for w in workers:
                 w.cancel()
             await asyncio.gather(*workers, return_exceptions=True)
+            for t in list(self._flushes):
+                t.cancel()
+            await asyncio.gather(*self._flushes, return_exceptions=True)
 
     async def _admit(self, reqs):
         self.stats["rounds"] += 1
@@ -145,7 +170,7 @@ class DynamicBatcher:
             self._cond.notify_all()
         for st in states:
             if not st.sentences:  # empty text: only the marker
-                await self._flush(st)
+                self._deliver(st)
 
     def _framing(self, req) -> int:
         f = getattr(req, "stream_frames", 0) or 0
@@ -203,6 +228,11 @@ class DynamicBatcher:
             if frames == 0:
                 synth = self.synth_batches[eng]
                 audios = await loop.run_in_executor(None, lambda: synth(texts, **kw))
+                audios = list(audios) if audios is not None else []
+                if len(audios) != len(batch) or any(a is None for a in audios):
+                    # a short or partial result would leave sentences never marked done (and
+                    # their request's slot never freed): the whole batch fails instead
+                    raise RuntimeError(f"engine returned {len(audios)} results for {len(batch)} sentences")
                 for it, a in zip(batch, audios):
                     it.state.pending[it.j].append(a)
                     it.state.done[it.j] = True
@@ -218,57 +248,81 @@ class DynamicBatcher:
                         it.state.done[it.j] = it.state.done[it.j] or fin
                         touched[id(it.state)] = it.state
                     for st in touched.values():
-                        await self._flush(st)
+                        self._deliver(st)
                 await self._stream(loop, texts, frames, kw, deliver, eng)
         except asyncio.CancelledError:
             raise
         except Exception as e:
-            self.stats["errors"] += 1
+            self.stats["batch_errors"] += 1
             logger.error("synthesis_failed: %s", e)
             for it in batch:
                 st = it.state
                 if not st.failed:
                     st.failed = True
+                    self.stats["errors"] += 1  # per request, as the reference counts (synthesizer.py:291-294)
                     if self.notify_errors and self.send_error is not None:
                         await self.send_error(st.req.connection_id, str(e))
             for st in {id(it.state): it.state for it in batch}.values():
-                await self._flush(st)
+                self._deliver(st)
             return
         self.stats["engine_batches"] += 1
         self.stats["sentences"] += len(batch)
         self.stats["engine_sentences"][eng] += len(batch)
         self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(batch))
         for st in {id(it.state): it.state for it in batch}.values():
-            await self._flush(st)
+            self._deliver(st)
+
+    def _deliver(self, st: _Request):
+        """Start sending what request `st` can send, in a task of its own (see _flush)."""
+        t = asyncio.get_running_loop().create_task(self._flush(st))
+        self._flushes.add(t)
+        t.add_done_callback(self._flushes.discard)
 
     async def _flush(self, st: _Request):
         """Send what request `st` can send in sentence order; its final marker once every sentence
-        is done (or, after a failure, per notify_errors); a finished request frees its slot."""
-        async with self._flush_lock:
+        is done (or, after a failure, per notify_errors); a finished request frees its slot.  The
+        lock is the request's own: other requests' frames never wait behind this client."""
+        async with st.lock:
             if st.finished:
                 return
             r = st.req
-            while st.cursor < len(st.pending):
-                j = st.cursor
-                for a in st.pending[j]:
-                    await self.queues.enqueue_audio_chunk(r.connection_id, a.astype(np.float32).tobytes(), st.sent)
-                    st.sent += 1
-                st.pending[j].clear()
-                if not st.done[j]:
-                    break
-                st.cursor += 1
+            try:
+                while st.cursor < len(st.pending):
+                    j = st.cursor
+                    while st.pending[j]:
+                        a = st.pending[j].pop(0)
+                        await self.queues.enqueue_audio_chunk(r.connection_id, np.asarray(a, np.float32).tobytes(), st.sent)
+                        if st.first_chunk is None:
+                            st.first_chunk = time.perf_counter() - st.t_admit
+                        st.sent += 1
+                    if not st.done[j]:
+                        break
+                    st.cursor += 1
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # a frame that cannot be sent fails its request, not the engine
+                logger.error("delivery failed for %s: %s", r.connection_id, e)
+                if not st.failed:
+                    st.failed = True
+                    self.stats["errors"] += 1
             if st.cursor == len(st.pending) or st.failed:
                 if st.failed:
                     # drop its queued sentences: nothing more goes to this client
                     async with self._cond:
                         self._work = [it for it in self._work if it.state is not st]
-                if not (st.failed and not self.notify_errors):  # reference behaviour: no marker after a failure
-                    await self.queues.enqueue_audio_chunk(r.connection_id, b"", st.sent, is_final=True)
+                else:
+                    self.stats["syntheses"] += 1
+                    self.stats["total_latency"] += time.perf_counter() - st.t_admit
+                    self.stats["first_chunk_latency"] += st.first_chunk or 0.0
                 st.finished = True
-                await self.queues.mark_request_done(1)
-                async with self._cond:
-                    self._inflight -= 1
-                    self._cond.notify_all()
+                try:
+                    if not (st.failed and not self.notify_errors):  # reference behaviour: no marker after a failure
+                        await self.queues.enqueue_audio_chunk(r.connection_id, b"", st.sent, is_final=True)
+                finally:
+                    await self.queues.mark_request_done(1)
+                    async with self._cond:
+                        self._inflight -= 1
+                        self._cond.notify_all()
 
     async def _stream(self, loop, texts, frames, kw, deliver, eng: int = 0):
         """Run `synth_stream` (a generator of per-chunk pieces) on an executor thread and hand

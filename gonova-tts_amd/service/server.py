@@ -93,6 +93,8 @@ class TTSService:
         self.sockets = {}
         self.voices = {}      # voice_id -> speaker embedding (register_voice)
         self.voice_info = {}  # voice_id -> description
+        # the reference voice manager's counters (voice_manager.py:262-267)
+        self.voice_counts = {"registrations": 0, "cache_hits": 0, "cache_misses": 0}
         self.max_sentences = max_sentences
         self.max_wait = max_wait
         self.idle_wait = idle_wait  # the gathering window while an engine is idle (batcher.py)
@@ -235,6 +237,8 @@ class TTSService:
                 await ws.send_json({"type": "error", "message": f"Synthesis request refused: {e}"})
                 return
             # unknown voices fall back to the default voice (reference server.py:127-138)
+            if vid != "default":
+                self.voice_counts["cache_hits" if isinstance(vid, str) and vid in self.voices else "cache_misses"] += 1
             await self.queues.enqueue_request(
                 connection_id=conn_id, text=text, voice_id=vid,
                 chunk_size=data.get("chunk_size", self.chunk_size),
@@ -266,6 +270,7 @@ class TTSService:
                                                 f"speaker embeddings, got {v.size}"}
         self.voices[vid] = v
         self.voice_info[vid] = data.get("description", "")
+        self.voice_counts["registrations"] += 1
         return {"type": "voice_registered", "voice_id": vid}
 
     def list_voices(self) -> list:
@@ -276,17 +281,28 @@ class TTSService:
         info = {"status": "healthy", "device": f"{self.device}:{self.device_index}",
                 "devices": list(self.devices) if self.devices else [f"{self.device}:{self.device_index}"],
                 "sample_rate": getattr(self.model, "sr", 22050), "active_connections": self.active_connections,
-                "queue_metrics": self.queues.get_metrics(), "synthesizer_stats": dict(self.batcher.stats),
-                "voice_stats": {"total_voices": len(self.voices)}}
+                "queue_metrics": self.queues.get_metrics(), "synthesizer_stats": self.batcher.get_stats(),
+                "voice_stats": {"total_voices": len(self.voices), "cached_in_memory": len(self.voices),
+                                **self.voice_counts},
+                "gpu": {}}
         try:
             import torch
             if torch.cuda.is_available():
                 i = self.device_index
-                info["gpu"] = {"gpu_id": i, "gpu_name": torch.cuda.get_device_name(i),
-                               "memory_allocated_gb": torch.cuda.memory_allocated(i) / 1e9,
-                               "memory_reserved_gb": torch.cuda.memory_reserved(i) / 1e9}
-        except Exception:
-            pass
+                gpu = {"gpu_id": i, "gpu_name": torch.cuda.get_device_name(i),
+                       "memory_allocated_gb": torch.cuda.memory_allocated(i) / 1e9,
+                       "memory_reserved_gb": torch.cuda.memory_reserved(i) / 1e9}
+                # the engine's own weights and workspaces (hipMalloc'd in libtts_hip.so, invisible
+                # to torch's allocator): per engine device, and added into memory_allocated_gb
+                from ..engine import device_bytes, parse_device
+                devs = sorted({parse_device(d) for d in self.devices}) if self.devices else [i]
+                eng = {d: device_bytes(d) / 1e9 for d in devs}
+                gpu["engine_memory_gb"] = eng.get(i, 0.0)
+                gpu["engine_memory_gb_by_device"] = {str(d): v for d, v in eng.items()}
+                gpu["memory_allocated_gb"] += eng.get(i, 0.0)
+                info["gpu"] = gpu
+        except Exception as e:  # noqa: BLE001 -- health must answer
+            logger.warning("gpu info unavailable: %s", e)
         return info
 
 

@@ -100,6 +100,12 @@ enum { TTS_ENCODER_EXACT = 0, TTS_ENCODER_FAST = 1, TTS_ENCODER_F32 = 2 };
 /* Number of HIP devices visible to this process. */
 int tts_device_count(void);
 
+/* Device memory this library holds on HIP device `hip_device` (every engine's weights and
+ * workspaces, in bytes) -> *bytes.  The reference's /health reports torch's allocator
+ * (server.py:456-465: memory_allocated / memory_reserved), which never sees these buffers;
+ * the service adds this figure to its "gpu" report.  Needs no GPU work (a host-side count). */
+int tts_device_bytes(int hip_device, int64_t* bytes);
+
 /* Engine lifetime (replaces ChatterboxTTS.from_pretrained, synthesizer.py:185).
  * tts_engine_create reads a whole tts_config of THIS header; tts_engine_create_sized reads
  * cfg_size bytes of it (sizeof(tts_config) of the caller's header; smaller = an older layout,

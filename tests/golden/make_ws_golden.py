@@ -12,8 +12,9 @@ length and values depend on the text; tests/test_service_cpu.py uses the same fu
 `signal.signal` is a no-op (TestClient runs the startup hook off the main thread).  The fixture
 holds what the reference did with those arrays: the frames each request produced (byte length
 and sha256 of each binary frame, in order), the final JSON message, every `generate` call
-(text and keyword arguments, warmups included), /metrics after the requests, and /health's
-503 body before startup (server.py:447-454).
+(text and keyword arguments, warmups included), /metrics after the requests, /health's
+503 body before startup (server.py:447-454), and the shape of its 200 body after the requests
+(server.py:456-475): the key set of every nested dict, and the synthesizer's request counts.
 """
 from __future__ import annotations
 
@@ -101,7 +102,15 @@ def main():
                         break
                 out["requests"].append({"message": req, "frames": frames, "final": final})
         metrics = c.get("/metrics").json()
+        health = c.get("/health")
     out["metrics"] = metrics
+    hb = health.json()
+    out["health_after_requests"] = {
+        "status_code": health.status_code,
+        "keys": sorted(hb),
+        "nested_keys": {k: sorted(v) for k, v in hb.items() if isinstance(v, dict)},
+        "synthesizer_counts": {k: hb["synthesizer_stats"][k] for k in ("syntheses", "errors")},
+    }
     out["generate_calls"] = [x for x in calls if x["call"] == "generate"]
     out["from_pretrained"] = [x for x in calls if x["call"] == "from_pretrained"]
     path = os.path.join(HERE, "ws_transcript.json")

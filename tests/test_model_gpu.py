@@ -148,3 +148,24 @@ def test_sharded_synthesis_single_device_matches_direct(model32):
         for j, u in enumerate(bk):
             assert out[u].shape[0] == wl[j] == lens[u] * 3 * 256
             np.testing.assert_array_equal(out[u], wav[j, :wl[j]])
+
+
+def test_device_bytes_cover_weights_and_workspace():
+    """tts_device_bytes (the /health "gpu" figure) counts the engine's own
+    device buffers -- at least its weights in their compute dtype plus the vocoder's output-sized
+    workspace -- and drops back when the engine closes."""
+    from gonova_tts_amd.engine import HipEngine, device_bytes
+    torch.cuda.synchronize()
+    b0 = device_bytes(0)
+    B, T = 8, 200
+    eng = HipEngine("cuda:0", vocoder_dtype="f16", acoustic_dtype="bf16", max_batch=B, max_frames=T, max_tokens=40)
+    aw, vw = make_acoustic_weights(0), make_vocoder_weights(0)
+    eng.load_weights(acoustic=aw, vocoder=vw)
+    eng.reserve(B, T, 40)
+    b1 = device_bytes(0)
+    wbytes = 2 * sum(int(np.asarray(v).size) for v in list(aw.values()) + list(vw.values()))
+    work = B * T * 256 * 2  # one fp16 waveform-rate activation buffer of the batch
+    print(f"engine device bytes {b1 - b0:,} (weights in 16 bits {wbytes:,}, one activation buffer {work:,})")
+    assert b1 - b0 >= wbytes + work
+    eng.close()
+    assert device_bytes(0) == b0

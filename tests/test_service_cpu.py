@@ -3,6 +3,7 @@ as in the reference (server.py:215-224, 279-286), /health 503 rule, /metrics key
 cross-request batching, error path."""
 import json
 import threading
+import asyncio
 import time
 
 import numpy as np
@@ -238,6 +239,21 @@ def test_ws_transcript_matches_reference_fixture():
             if metrics["active_connections"] == 0:
                 break
             time.sleep(0.02)
+        # /health's 200 body keeps the reference's shape (server.py:456-475, synthesizer.py:411-420):
+        # every key the reference reports at every level (this service adds its own beside them),
+        # and the same request counts
+        r = c.get("/health")
+        hg = gold["health_after_requests"]
+        assert r.status_code == hg["status_code"]
+        h = r.json()
+        assert set(hg["keys"]) <= set(h), sorted(set(hg["keys"]) - set(h))
+        for k, keys in hg["nested_keys"].items():
+            assert set(keys) <= set(h[k]), (k, sorted(set(keys) - set(h[k])))
+        for k, v in hg["synthesizer_counts"].items():
+            assert h["synthesizer_stats"][k] == v, k
+        s = h["synthesizer_stats"]
+        assert s["total_latency"] >= s["first_chunk_latency"] > 0
+        assert abs(s["avg_latency"] - s["total_latency"] / s["syntheses"]) < 1e-12
     ref_texts = [x["text"] for x in gold["generate_calls"]]
     assert warm == ref_texts[:len(warm)]  # the reference's warmup sentences, in order
     # then every sentence as the reference split them (the batcher orders a batch by length, so
@@ -503,3 +519,75 @@ def test_request_arriving_mid_stream_starts_before_the_earlier_one_ends():
     b_batch = next(k for k, b in enumerate(model.batches) if b == ["Short one."])
     a_last = max(k for k, b in enumerate(model.batches) if b[0].startswith("Long request sentence number 7"))
     assert b_batch < a_last
+
+
+class _BatcherQueues:
+    """The queue-manager surface DynamicBatcher uses, with a per-connection delivery delay."""
+
+    def __init__(self, reqs, delay=None):
+        self.reqs = list(reqs)
+        self.delay = delay or {}
+        self.events = []
+        self.done = 0
+
+    async def take_batch(self, room, wait):
+        if self.reqs:
+            out, self.reqs = self.reqs[:room], self.reqs[room:]
+            return out
+        await asyncio.sleep(0.005)
+        return []
+
+    async def enqueue_audio_chunk(self, conn, data, chunk_id, is_final=False):
+        if conn in self.delay:
+            await asyncio.sleep(self.delay[conn])
+        self.events.append((conn, chunk_id, is_final, time.perf_counter()))
+
+    async def mark_request_done(self, n):
+        self.done += n
+
+
+def _req(conn, text):
+    from types import SimpleNamespace
+    return SimpleNamespace(connection_id=conn, text=text, voice=None, stream_frames=0)
+
+
+async def _run_batcher(b, q, until, timeout=10.0):
+    task = asyncio.create_task(b.run())
+    t0 = time.perf_counter()
+    while not until() and time.perf_counter() - t0 < timeout:
+        await asyncio.sleep(0.005)
+    b.stop()
+    task.cancel()
+    await asyncio.gather(task, return_exceptions=True)
+
+
+def test_short_engine_result_fails_the_batch_and_frees_its_slots():
+    """an engine that returns fewer results than sentences fails the whole batch (the
+    reference's failure path: no marker), and every request's slot is freed -- with max_requests = 2,
+    all five requests are still admitted and finished."""
+    from gonova_tts_amd.service.batcher import DynamicBatcher
+    q = _BatcherQueues([_req(f"c{i}", f"Sentence {i}. And one more.") for i in range(5)])
+    b = DynamicBatcher(q, lambda texts, **kw: [np.zeros(8, np.float32) for _ in texts[:-1]],
+                       max_sentences=4, max_requests=2)
+    asyncio.run(_run_batcher(b, q, lambda: q.done >= 5))
+    assert q.done == 5
+    st = b.get_stats()
+    assert st["errors"] == 5 and st["syntheses"] == 0 and st["batch_errors"] >= 1
+    assert not any(final for _, _, final, _ in q.events)
+
+
+def test_slow_client_does_not_delay_other_connections():
+    """one client's frames waiting on its full output queue (0.3 s per frame
+    here) do not hold back another connection's frames served by the same engine batch -- the
+    delivery lock is per request."""
+    from gonova_tts_amd.service.batcher import DynamicBatcher
+    q = _BatcherQueues([_req("slow", "One. Two. Three."), _req("fast", "Four. Five. Six.")], delay={"slow": 0.3})
+    b = DynamicBatcher(q, lambda texts, **kw: [np.full(8, len(t), np.float32) for t in texts], max_sentences=8)
+    asyncio.run(_run_batcher(b, q, lambda: q.done >= 2))
+    fast_end = max(t for c, _, fin, t in q.events if c == "fast" and fin)
+    slow_first = min(t for c, _, _, t in q.events if c == "slow")
+    assert fast_end < slow_first, q.events
+    assert [cid for c, cid, _, _ in q.events if c == "fast"] == [0, 1, 2, 3]
+    assert [cid for c, cid, _, _ in q.events if c == "slow"] == [0, 1, 2, 3]
+    st = b.get_stats()
+    assert st["syntheses"] == 2 and st["avg_latency"] > 0.9 * st["total_latency"] / 2

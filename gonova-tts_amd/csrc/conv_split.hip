@@ -2,13 +2,17 @@
 //
 // gfx950 has no xf32 and its native fp32 MFMA (v_mfma_f32_32x32x2_f32) peaks at 1/16 of the
 // 16-bit rate.  An fp32 value a is split into two f16 terms,
-//     a_hi = f16(a),   a_lo = f16((a - a_hi) * 2^11)        (a ~= a_hi + a_lo * 2^-11),
-// a_hi carrying the top 11 significand bits and a_lo the next 11, and
-//     sum a*b ~= sum a_hi*b_hi  +  2^-11 * sum (a_hi*b_lo + a_lo*b_hi)
-// runs as three v_mfma_f32_32x32x16_f16 into two fp32 accumulators (the dropped a_lo*b_lo term
-// and the two representation errors are ~2^-21 relative per product: ~8x the fp32 rounding of
-// one product, 1000x below bf16).  Effective fp32 throughput is 1/3 of the f16 peak: ~5x the
-// native fp32 MFMA.  Range: |a| < 65504 (f16); the acoustic encoder's activations are O(100).
+//     a_hi = f16(a),   a_lo = f16(a - a_hi)        (a ~= a_hi + a_lo),
+// a_hi carrying the top 11 significand bits and a_lo the next 11 (a_lo is subnormal for |a| below
+// ~2^-3 and then keeps fewer bits: an absolute error under 2^-25 per element, below the fp32
+// rounding of the sums it enters), and
+//     sum a*b ~= sum a_hi*b_hi + a_hi*b_lo + a_lo*b_hi
+// runs as three v_mfma_f32_32x32x16_f16 into ONE fp32 accumulator.  The weights are stored scaled
+// by a power of two 2^s per layer (frag_pack_split: max|w| 2^s in [2^14, 2^15), so the weights' lo
+// plane stays normal) and the sums are multiplied by ConvParams::w_unscale = 2^-s, exactly.  The
+// dropped a_lo*b_lo term and the representation errors are ~2^-21 relative per product: ~8x the
+// fp32 rounding of one product, 1000x below bf16.  Effective fp32 throughput is 1/3 of the f16
+// peak: ~5x the native fp32 MFMA.  Range: |a| < 65504 (f16); the encoder's activations are O(100).
 //
 // Used for the acoustic encoder + variance predictors in "exact" encoder precision (the
 // integer durations of HF:181-183 then match the fp32 oracle, SURVEY.md §8c "durations: exact
@@ -45,6 +49,12 @@
 #ifndef TTS_SPLIT_WHOLE_MAXBLK
 #define TTS_SPLIT_WHOLE_MAXBLK 256  // packed split GEMMs of at most this many blocks stage their K slice at once
 #endif
+#ifndef TTS_SPLIT_NT4_MINBLK
+#define TTS_SPLIT_NT4_MINBLK 320  // 128-row split GEMM tiles from this many blocks (~1.25 per CU)
+#endif
+#ifndef TTS_SPLIT_KQ4
+#define TTS_SPLIT_KQ4 1  // k-steps per weight-ring slot of the 128-row tiles (register budget)
+#endif
 #ifndef TTS_SPLITK_FUSE
 #define TTS_SPLITK_FUSE 0
 #endif
@@ -57,14 +67,13 @@
 
 namespace tts {
 
-constexpr float SPLIT_SCALE = 2048.f;  // 2^11: a_lo is stored scaled into f16's normal range
 constexpr int SPLIT_SU = 4;            // X staging loads (x2) in flight per thread
 
 // 8 fp32 -> (hi, lo) f16 x 8
 __device__ inline void split8(f32x4 a, f32x4 b, uint4& hi, uint4& lo) {
   const half4 ha = __builtin_convertvector(a, half4), hb = __builtin_convertvector(b, half4);
-  const f32x4 ra = (a - __builtin_convertvector(ha, f32x4)) * SPLIT_SCALE;
-  const f32x4 rb = (b - __builtin_convertvector(hb, f32x4)) * SPLIT_SCALE;
+  const f32x4 ra = a - __builtin_convertvector(ha, f32x4);
+  const f32x4 rb = b - __builtin_convertvector(hb, f32x4);
   const half4 la = __builtin_convertvector(ra, half4), lb = __builtin_convertvector(rb, half4);
   const uint2 h0 = __builtin_bit_cast(uint2, ha), h1 = __builtin_bit_cast(uint2, hb);
   const uint2 l0 = __builtin_bit_cast(uint2, la), l1 = __builtin_bit_cast(uint2, lb);
@@ -128,9 +137,9 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
   const int x_start = n0 - p.pad;
   const char* xl = smem + (wu * R + l31) * RS + hh * 16;
 
-  f32x16 acc[NT], accx[NT];
+  f32x16 acc[NT];
 #pragma unroll
-  for (int j = 0; j < NT; ++j) { acc[j] = f32x16{}; accx[j] = f32x16{}; }
+  for (int j = 0; j < NT; ++j) acc[j] = f32x16{};
   unsigned rng = 0;  // range guard over the staged hi halves (common.h f16x2_nonfinite)
 
   // staging: thread owns 8-channel column cc of the group and staged rows r0, r0 + rstep, ...
@@ -203,8 +212,8 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
         }                                                                                            \
         _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_) {                                       \
           acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bh_[nt_], acc[nt_], 0, 0, 0);    \
-          accx[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bl_[nt_], accx[nt_], 0, 0, 0);  \
-          accx[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[4 + j_], bh_[nt_], accx[nt_], 0, 0, 0); \
+          acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bl_[nt_], acc[nt_], 0, 0, 0);    \
+          acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[4 + j_], bh_[nt_], acc[nt_], 0, 0, 0); \
         }                                                                                            \
       }                                                                                              \
     } while (0)
@@ -258,7 +267,7 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
   if (b >= p.B) return;
   f32x16 out[1][NT];
 #pragma unroll
-  for (int j = 0; j < NT; ++j) out[0][j] = acc[j] + accx[j] * (1.0f / SPLIT_SCALE);
+  for (int j = 0; j < NT; ++j) out[0][j] = acc[j] * p.w_unscale;
   conv_epilogue<float, 1, NT>(p, out, b, 0, n0, (by * WM + wm) * 32, ylen_of(b), l31, hh);
 }
 
@@ -272,8 +281,10 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
 // K is optionally split into S slices of whole channel groups (S from the layer shape only, so a
 // row's accumulation order never depends on the batch): each slice writes fp32 partial sums to
 // ConvParams::ws and split_reduce_kernel adds them in slice order and applies the epilogue.
-constexpr int SPK_NT = 2;  // 32-row MFMA tiles per wave: 64-row blocks
-constexpr int SPK_SU = 9;  // X prefetch registers (16 B each) per thread: 66-72 rows x 128 channels
+constexpr int SPK_NT = 2;   // 32-row MFMA tiles per wave: 64-row blocks
+constexpr int SPK_SU = 9;   // X prefetch registers (16 B each) per thread: 66-72 rows x 128 channels
+constexpr int SPK_SU4 = 17; // the same for 128-row blocks (NT = 4): 130-136 rows
+__host__ __device__ constexpr int spk_su(int nt) { return nt >= 4 ? SPK_SU4 : SPK_SU; }
 
 __device__ inline int packed_valid(const ConvParams& p, const int* lens, int f, int F) {
   if (f < 0 || f >= F) return 0;
@@ -487,11 +498,14 @@ constexpr int SPK_WG = 3;
 __device__ int g_split_stamp_target[3];
 __device__ unsigned long long g_split_stamp[1 << 18];
 #endif
-// NT: 32-row MFMA tiles per wave (SPK_NT; 1 for grids the 64-row tiles leave under-filled)
+// NT: 32-row MFMA tiles per wave (SPK_NT; 1 for grids the 64-row tiles leave under-filled, 4 for
+// grids that fill the chip with 128-row tiles: half the weight stream and X staging per MFMA)
 template <bool WHOLE, int NT = SPK_NT>
 __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int CG, int S, int gps) {
   typedef half8 Frag;
   constexpr int BN = 32 * NT;
+  constexpr int SU = spk_su(NT);
+  static_assert(!(WHOLE && NT >= 4), "whole-slice staging is for small grids");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int F = p.B * p.x_rows;  // flat rows
@@ -527,7 +541,10 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
   const int PL = R * RS;
   const int KS = CG / 16;
   const int lks = __builtin_ctz(KS);
-  const int QT = p.taps * KS / 4;  // even (CG >= 128)
+  // weight ring slots of KQ k-steps (hi + lo fragments each): 4, or 2 at 128-row tiles, whose
+  // accumulators and X prefetch leave no room for 4-step slots at two waves per SIMD
+  constexpr int KQ = NT >= 4 ? TTS_SPLIT_KQ4 : 4;
+  const int QT = p.taps * KS / KQ;  // even (CG >= 128)
   const int x_start = f0 - p.pad;
   const char* xl = smem + l31 * RS + hh * 16;
   const float* X = reinterpret_cast<const float*>(p.x);
@@ -548,13 +565,13 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
   };
 #endif
 
-  f32x16 acc[NT], accx[NT];
+  f32x16 acc[NT];
 #pragma unroll
-  for (int j = 0; j < NT; ++j) { acc[j] = f32x16{}; accx[j] = f32x16{}; }
+  for (int j = 0; j < NT; ++j) acc[j] = f32x16{};
   unsigned rng = 0;  // range guard over the staged hi halves (common.h f16x2_nonfinite)
 
   // X staging: thread owns 4-channel column c4 of the group and staged rows r0, r0 + rstep, ...
-  // (at most SPK_SU: split_group sizes CG for that).  The next group's rows are loaded into
+  // (at most SU: split_group sizes CG for that).  The next group's rows are loaded into
   // registers while the current group's MFMAs run (issued two weight quads into the group, so
   // the first wait on a younger weight load finds them landed) and split into LDS after them.
   const int VPR = CG / 4;
@@ -562,7 +579,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
   const int c4 = tid & (VPR - 1);
   const int r0 = tid >> lvpr;
   const int rstep = 256 >> lvpr;
-  f32x4 xv[SPK_SU];
+  f32x4 xv[SU];
   // Validity of this thread's staged rows (the same rows for every group), bit i for row
   // r0 + i * rstep: computed once, after the first group's X loads are issued, with the length
   // loads through a descriptor (no branch around them).  Computing it per row inside the LDS
@@ -574,7 +591,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
                                                        0, p.x_len ? p.B * 4 : 0, 0x00020000);
     int m = 0;
 #pragma unroll
-    for (int i = 0; i < SPK_SU; ++i) {
+    for (int i = 0; i < SU; ++i) {
       const int f = x_start + r0 + i * rstep;
       const int fc = min(max(f, 0), F - 1);
       const int b = fc / p.x_rows, r = fc - b * p.x_rows;
@@ -586,17 +603,17 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     }
     return m;
   };
-  auto load_x_to = [&](int g, f32x4 (&xd)[SPK_SU]) __attribute__((always_inline)) {
+  auto load_x_to = [&](int g, f32x4 (&xd)[SU]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < SPK_SU; ++i) {
+    for (int i = 0; i < SU; ++i) {
       const int f = x_start + min(r0 + i * rstep, R - 1);
       xd[i] = *reinterpret_cast<const f32x4*>(X + (long long)min(max(f, 0), F - 1) * p.sxr + g + c4 * 4);
     }
   };
   auto load_x = [&](int g) __attribute__((always_inline)) { load_x_to(g, xv); };
-  auto store_x_from = [&](const f32x4 (&xs)[SPK_SU], char* base) __attribute__((always_inline)) {
+  auto store_x_from = [&](const f32x4 (&xs)[SU], char* base) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < SPK_SU; ++i) {
+    for (int i = 0; i < SU; ++i) {
       const int rr = r0 + i * rstep;
       f32x4 v = xs[i];
       if (!((vm >> i) & 1)) v = f32x4{};
@@ -605,7 +622,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
         for (int e = 0; e < 4; ++e) v[e] = leaky(v[e], p.in_slope);
       }
       const half4 h = __builtin_convertvector(v, half4);
-      const half4 l = __builtin_convertvector((v - __builtin_convertvector(h, f32x4)) * SPLIT_SCALE, half4);
+      const half4 l = __builtin_convertvector(v - __builtin_convertvector(h, f32x4), half4);
       const uint2 hb = __builtin_bit_cast(uint2, h);
       rng |= f16x2_nonfinite(hb.x) | f16x2_nonfinite(hb.y);
       if (rr < R) {
@@ -620,32 +637,32 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
   // Weight quads form one ring over the slice: the two quads past a group's last are the next
   // group's first two (issued before the group-change barriers, so their latency overlaps the
   // X restaging); past the slice's last group they fall outside the descriptor and fetch nothing.
-  Frag a0[8], a1[8];
+  Frag a0[2 * KQ], a1[2 * KQ];
   int g0 = gbeg;
 #define TTS_SPLIT_LOADQ(A_, QQ_)                                                                     \
     do {                                                                                             \
       const int nx_ = (QQ_) >= QT;                                                                   \
-      const int kq_ = 4 * ((QQ_) - nx_ * QT);                                                        \
+      const int kq_ = KQ * ((QQ_) - nx_ * QT);                                                       \
       const int gg_ = g0 + nx_ * CG;                                                                 \
       const int o_ = TTS_SPLIT_PROBE ? 0 : (((kq_ >> lks) * KST + gg_ / 16 + (kq_ & (KS - 1))) * 1024) + \
                      (gg_ < gend ? 0 : 0x40000000);                                                  \
-      _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                             \
+      _Pragma("unroll") for (int j_ = 0; j_ < KQ; ++j_) {                                            \
         A_[j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_hi, lofs + j_ * 1024, o_, 0)); \
-        A_[4 + j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_lo, lofs + j_ * 1024, o_, 0)); \
+        A_[KQ + j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_lo, lofs + j_ * 1024, o_, 0)); \
       }                                                                                              \
       __builtin_amdgcn_sched_barrier(0);                                                             \
     } while (0)
 #define TTS_SPLIT_MMAQ(A_, QQ_)                                                                      \
     do {                                                                                             \
-      const int kq_ = 4 * (QQ_);                                                                     \
+      const int kq_ = KQ * (QQ_);                                                                    \
       const char* bq_ = xg + (kq_ >> lks) * p.dil * RS + (kq_ & (KS - 1)) * 32;                      \
-      _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                             \
+      _Pragma("unroll") for (int j_ = 0; j_ < KQ; ++j_) {                                            \
         _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_) {                                       \
           const Frag bh_ = *reinterpret_cast<const Frag*>(bq_ + nt_ * 32 * RS + j_ * 32);            \
           const Frag bl_ = *reinterpret_cast<const Frag*>(bq_ + PL + nt_ * 32 * RS + j_ * 32);       \
           acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bh_, acc[nt_], 0, 0, 0);         \
-          accx[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bl_, accx[nt_], 0, 0, 0);       \
-          accx[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[4 + j_], bh_, accx[nt_], 0, 0, 0);   \
+          acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bl_, acc[nt_], 0, 0, 0);         \
+          acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[KQ + j_], bh_, acc[nt_], 0, 0, 0);    \
         }                                                                                            \
       }                                                                                              \
     } while (0)
@@ -654,7 +671,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
   const char* xg = xl;  // the current group's LDS tile
   if constexpr (WHOLE) {
     // every group's X loads in flight at once, then split into the groups' own LDS regions
-    f32x4 xw[SPK_WG][SPK_SU];
+    f32x4 xw[SPK_WG][SU];
     const int ng = (gend - gbeg) / CG;  // <= SPK_WG (launcher)
 #pragma unroll
     for (int i = 0; i < SPK_WG; ++i) load_x_to(gbeg + min(i, ng - 1) * CG, xw[i]);
@@ -737,7 +754,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     __syncthreads();  // X tile no longer read
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const f32x16 v = acc[nt] + accx[nt] * (1.0f / SPLIT_SCALE);
+      const f32x16 v = acc[nt] * p.w_unscale;
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         *reinterpret_cast<f32x4*>(smem + (nt * 32 + l31) * OSR + (wave * 32 + 8 * g + 4 * hh) * 4) =
@@ -795,7 +812,7 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
   for (int nt = 0; nt < NT; ++nt) {
     const int f = f0 + nt * 32 + l31;
     if (f >= F) continue;
-    const f32x16 v = acc[nt] + accx[nt] * (1.0f / SPLIT_SCALE);
+    const f32x16 v = acc[nt] * p.w_unscale;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int m = m_w0 + 8 * g + 4 * hh;
@@ -924,12 +941,12 @@ static hipError_t launch_tile(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// packed-row channel group: 128 when every thread's share of the (128 + halo)-row tile fits its
-// SPK_SU prefetch registers and both planes fit LDS at one block per CU
-static int packed_group(const ConvParams& p) {
-  const int R = 32 * SPK_NT + (p.taps - 1) * p.dil;
+// packed-row channel group: 128 when every thread's share of the (32 nt + halo)-row tile fits its
+// spk_su(nt) prefetch registers and both planes fit LDS at two blocks per CU
+static int packed_group(const ConvParams& p, int nt = SPK_NT) {
+  const int R = 32 * nt + (p.taps - 1) * p.dil;
   const int cg = 128, rstep = 256 / (cg / 4);
-  if (p.Cin % cg || (R + rstep - 1) / rstep > SPK_SU || (size_t)2 * R * (cg * 2 + 16) > SPLIT_LDS_MAX) return 0;
+  if (p.Cin % cg || (R + rstep - 1) / rstep > spk_su(nt) || (size_t)2 * R * (cg * 2 + 16) > SPLIT_LDS_MAX) return 0;
   return cg;
 }
 
@@ -998,14 +1015,20 @@ hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done) 
       // 32-row tiles where the 64-row grid would leave most CUs idle (the batch-8 encoder's
       // M = 384 projections: 60 blocks): twice the blocks, each with half the staging and MFMA
       // latency.  A row's K order does not depend on the tile: bit-identical.
+      // 128-row tiles where even they fill the chip (TTS_SPLIT_NT4_MINBLK blocks: the batch-32
+      // FFN / Q|K|V / pointwise-1 GEMMs): each weight quad feeds twice the MFMAs, and X is staged
+      // once per 128 rows.  TTS_SPLIT_NT1: 0 = 64-row tiles, 1 = 32-row, 4 = 128-row wherever
+      // eligible; unset = by grid.
       const int mbs = (p.M + 127) / 128 * S;
-      const int nt = sw(SW_SPLIT_NT1) == 1 || (sw(SW_SPLIT_NT1) != 0 && (F + 63) / 64 * mbs < TTS_SPLIT_NT1_MAXBLK) ? 1 : SPK_NT;
+      const int ntsw = sw(SW_SPLIT_NT1);
+      int nt = ntsw == 1 || (ntsw < 0 && (F + 63) / 64 * mbs < TTS_SPLIT_NT1_MAXBLK) ? 1 : SPK_NT;
+      if (packed_group(p, 4) && (ntsw == 4 || (ntsw < 0 && (long long)(F + 127) / 128 * mbs >= TTS_SPLIT_NT4_MINBLK))) nt = 4;
       const int nwg = (F + 32 * nt - 1) / (32 * nt) * mbs;
       const size_t lds = std::max((size_t)2 * (32 * nt + (p.taps - 1) * p.dil) * (cg * 2 + 16),
                                   (size_t)32 * nt * (128 * 4 + 16));  // X planes / epilogue tile
       // one block per CU or fewer: stage the K slice's groups at once (no restaging; bit-identical)
       const int ngs = gps;  // groups per slice
-      const bool whole = sw(SW_SPLIT_WHOLE) != 0 && ngs <= SPK_WG && nwg <= TTS_SPLIT_WHOLE_MAXBLK;
+      const bool whole = sw(SW_SPLIT_WHOLE) != 0 && ngs <= SPK_WG && nwg <= TTS_SPLIT_WHOLE_MAXBLK && nt < 4;
       const size_t ldsw = whole ? std::max((size_t)ngs * 2 * (32 * nt + (p.taps - 1) * p.dil) * (cg * 2 + 16),
                                            (size_t)32 * nt * (128 * 4 + 16))
                                 : lds;
@@ -1021,6 +1044,7 @@ hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done) 
         else hipLaunchKernelGGL((conv_splitp_kernel<true, SPK_NT>), dim3(nwg), dim3(256), ldsw, s, q, cg, S, gps);
       } else {
         if (nt == 1) hipLaunchKernelGGL((conv_splitp_kernel<false, 1>), dim3(nwg), dim3(256), lds, s, q, cg, S, gps);
+        else if (nt == 4) hipLaunchKernelGGL((conv_splitp_kernel<false, 4>), dim3(nwg), dim3(256), lds, s, q, cg, S, gps);
         else hipLaunchKernelGGL((conv_splitp_kernel<false, SPK_NT>), dim3(nwg), dim3(256), lds, s, q, cg, S, gps);
       }
       if (q.ln_cnt) {

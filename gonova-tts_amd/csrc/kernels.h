@@ -27,6 +27,9 @@ struct ConvParams {
   // optional fragment-packed copy of w (frag_pack in runtime.h): enables the X-resident
   // kernel, whose weight loads are then contiguous 1 KiB wave reads
   const void* wpk;
+  // split-packed weights (frag_pack_split) are stored scaled by a power of two; the split GEMMs
+  // multiply their sums by w_unscale (exact).  1 for every other packing.
+  float w_unscale;
   // Packed-row hint (split-precision fp32 GEMMs, conv_split.hip): rows_pad > 0 promises that every
   // utterance is followed by at least rows_pad masked rows (x_rows - len[b] >= rows_pad, X / Y /
   // residuals contiguous [B][x_rows][C]), so row tiles may run across utterance boundaries; the
@@ -77,6 +80,7 @@ inline ConvParams conv_params_default() {
   ConvParams p{};
   p.in_slope = 1.f; p.alpha = 1.f; p.out_scale = 1.f; p.out_slope = 0.f;
   p.taps = 1; p.dil = 1; p.nh = 1;
+  p.w_unscale = 1.f;
   return p;
 }
 

@@ -396,14 +396,15 @@ def test_dma_staged_ffn_bit_identical(aw, dtype, switch):
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_split_tile_height_bit_identical(aw, dtype, switch):
     """The split-precision GEMMs' 32-row tiles (small grids: the batch-8 exact encoder) give the
-    64-row tiles' bits (TTS_SPLIT_NT1=0) and those of 32-row tiles everywhere (=1), with the
+    64-row tiles' bits (TTS_SPLIT_NT1=0) and those of 32-row (=1) and 128-row (=4, the batch-32
+    form) tiles everywhere, with the
     post-LNs fused in every eligible launch as well (TTS_LN_FUSE=7: the tail on 32-row tiles), on
     a ragged batch-8 forward with predicted durations."""
     eng = engine(dtype, aw)
     rng = np.random.default_rng(45)
     ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70, 127, 129, 9, 33)]
     outs = {}
-    for nt1 in (0, None, 1):
+    for nt1 in (0, None, 1, 4):
         for ln in (None, 7):
             switch("TTS_SPLIT_NT1", nt1)
             switch("TTS_LN_FUSE", ln)

@@ -1111,6 +1111,9 @@ static hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
 #ifndef TTS_F32_SLICE_CH
 #define TTS_F32_SLICE_CH 32  // fp32 split-K: input channels per slice at least (C1: 32 beat 64, profiles/r05zm)
 #endif
+#ifndef TTS_F32_SK_SMAX
+#define TTS_F32_SK_SMAX 16  // fp32 split-K: at most this many slices (a cap keeps batch-invariant bits)
+#endif
 #ifndef TTS_F32_CK
 #define TTS_F32_CK 16  // fp32 channel chunk (A/B builds: 32 -- half the staging rounds and barriers)
 #endif
@@ -1124,7 +1127,7 @@ static int f32_ck(int Cin) { return Cin % TTS_F32_CK == 0 ? TTS_F32_CK : 16; }
 int f32_kslices(int taps, int Cin) {
   const int ck = f32_ck(Cin);
   const int nch = (Cin + ck - 1) / ck;
-  int S = taps > 0 ? std::min(16, Cin / TTS_F32_SLICE_CH) : 1;
+  int S = taps > 0 ? std::min(TTS_F32_SK_SMAX, Cin / TTS_F32_SLICE_CH) : 1;
   while (S > 1 && nch % S) --S;
   return std::max(S, 1);
 }
@@ -1228,7 +1231,6 @@ int conv_gemm_check(const ConvParams& p, int dtype, const char** why) {
 
 int conv_gemm_kind(int dtype, const ConvParams& p) {
   if (dtype == DT_F32) return conv_split_eligible(p) ? PK_CONV_SPLIT : PK_CONV_GEMM;
-  if (conv_mt_eligible(dtype, p)) return PK_CONV_MT;
   return (dtype != DT_F32 && xres_group(p, 32 * 4 * (4 / xres_wm(p)))) ? PK_CONV_XRES : PK_CONV_GEMM;
 }
 
@@ -1242,13 +1244,11 @@ static hipError_t conv_gemm_launch_noln(int dtype, const ConvParams& p, hipStrea
     }
     case DT_F16: {
       hipError_t e;
-      if (conv_mt_eligible(dtype, p)) return conv_mt_launch(dtype, p, s, ln_done);
       if (launch_xres<half_t>(p, s, &e, ln_done)) return e;
       return launch_t<half_t>(p, s);
     }
     case DT_BF16: {
       hipError_t e;
-      if (conv_mt_eligible(dtype, p)) return conv_mt_launch(dtype, p, s, ln_done);
       if (launch_xres<bf16_t>(p, s, &e, ln_done)) return e;
       return launch_t<bf16_t>(p, s);
     }

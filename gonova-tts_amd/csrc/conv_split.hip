@@ -55,9 +55,6 @@
 #ifndef TTS_SPLIT_KQ4
 #define TTS_SPLIT_KQ4 1  // k-steps per weight-ring slot of the 128-row tiles (register budget)
 #endif
-#ifndef TTS_SPLITK_FUSE
-#define TTS_SPLITK_FUSE 0
-#endif
 #ifndef TTS_LN_TAIL
 #define TTS_LN_TAIL 1  // 0: timing-only probe builds -- fused post-LN tails load their rows but compute nothing
 #endif
@@ -413,79 +410,6 @@ __device__ inline void split_reduce_ln_row(const ConvParams& p, int S, int F, in
     if (on[i]) o[ch[i]] = v[0][i];
 }
 
-// The in-launch split-K reduce + LayerNorm of a row tile (the last of its M blocks x S slices):
-// split_reduce_ln_row's arithmetic (slices summed in slice order, then the epilogue and the LN),
-// with the slices of RB rows per wave in flight at once (S <= SKMAX: the launcher checks)
-constexpr int SKMAX = 4;
-__device__ inline void splitk_tile_ln(const ConvParams& p, int S, int F, int f0, int BN, int wave, int lane) {
-  const int C = p.M;
-  constexpr int RB = 2, PER = 8;  // rows per wave in flight (all slices) and normalised together
-  int ch[PER];
-  bool on[PER];
-  ln_lanes64<PER>(ch, on, C, lane);
-  float g[2][PER], bb[2][PER], bias[PER];
-  ln_params<PER>(g, bb, ch, on, p.ln_g1, p.ln_b1, p.ln_g2, p.ln_b2);
-#pragma unroll
-  for (int i = 0; i < PER; ++i) bias[i] = on[i] && p.bias ? p.bias[ch[i]] : 0.f;
-  for (int r0 = wave; r0 < BN; r0 += 4 * RB) {
-    float v[RB][PER];
-    long long ro[RB], yo[RB];
-    bool ok[RB];
-    {
-      float w[RB][SKMAX][PER], res[RB][PER];
-      // the first residual through a descriptor with no records when absent (loads unconditional)
-      const auto r1s = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.r1 ? p.r1 : p.y), 0,
-                                                         p.r1 ? 0x7fffffff : 0, 0x00020000);
-#pragma unroll
-      for (int k = 0; k < RB; ++k) {  // unconditional loads at clamped rows / slices / channels
-        const int f = min(f0 + min(r0 + 4 * k, BN - 1), F - 1);
-        const int b = f / p.x_rows, r = f - b * p.x_rows;
-        ok[k] = r0 + 4 * k < BN && f0 + r0 + 4 * k < F && r < (p.y_len ? min(p.y_len[b], p.y_rows) : p.y_rows);
-        ro[k] = (long long)b * p.srb + (long long)r * p.srr;
-        yo[k] = (long long)b * p.syb + (long long)r * p.syr;
-#pragma unroll
-        for (int sl = 0; sl < SKMAX; ++sl)
-#pragma unroll
-          for (int i = 0; i < PER; ++i) w[k][sl][i] = p.ws[((long long)min(sl, S - 1) * F + f) * C + min(ch[i], C - 1)];
-#pragma unroll
-        for (int i = 0; i < PER; ++i)
-          res[k][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1s, (int)((ro[k] + min(ch[i], C - 1)) * 4), 0, 0));
-      }
-      // split_reduce_ln_row's arithmetic: the slices in slice order, then the epilogue
-#pragma unroll
-      for (int k = 0; k < RB; ++k)
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-          float x = 0.f;
-          if (on[i]) {
-            x = w[k][0][i];
-#pragma unroll
-            for (int sl = 1; sl < SKMAX; ++sl)
-              if (sl < S) x += w[k][sl][i];
-            if (p.bias) x += bias[i];
-            if (p.alpha != 1.0f) x *= p.alpha;
-            if (p.r1) x += res[k][i];
-            if (p.r2) x += reinterpret_cast<const float*>(p.r2)[ro[k] + ch[i]];
-            if (p.out_scale != 1.0f) x *= p.out_scale;
-          }
-          v[k][i] = x;
-        }
-    }
-#if TTS_LN_TAIL
-    if (p.ln_g2) ln_batch<float, RB, PER, true>(v, on, C, g, bb, p.ln_eps);
-    else ln_batch<float, RB, PER, false>(v, on, C, g, bb, p.ln_eps);
-#endif
-#pragma unroll
-    for (int k = 0; k < RB; ++k)
-      if (ok[k]) {
-        float* o = reinterpret_cast<float*>(p.ln_out) + yo[k];
-#pragma unroll
-        for (int i = 0; i < PER; ++i)
-          if (on[i]) o[ch[i]] = v[k][i];
-      }
-  }
-}
-
 // WHOLE: every channel group of the block's K slice (at most SPK_WG) is staged at once, their X
 // loads all in flight together, into LDS regions of their own (one block per CU), and the MFMA
 // loop runs over the groups with no restaging -- for grids of at most one block per CU (the
@@ -802,12 +726,9 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     if (lnf && ln_tile_last(p.ln_cnt + tx, nmb, reinterpret_cast<int*>(smem))) splitp_tile_ln(p, f0, BN, F, wave, lane);
     return;
   }
-  // partial sums of slice sl: ws[sl][f][M] (rows past F and channels past M are not stored)
+  // partial sums of slice sl: ws[sl][f][M] (rows past F and channels past M are not stored);
+  // split_reduce(_ln)_kernel adds them in slice order
   float* P = p.ws + (long long)sl * F * p.M;
-  // with ln_cnt the row tile's last block (of its M blocks x S slices) reduces the slices and
-  // applies the LayerNorm in this launch (split_reduce_ln_row): the partials go write-through
-  const bool lnf = p.ln_cnt != nullptr;
-  const auto wsr = __builtin_amdgcn_make_buffer_rsrc(p.ws, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int f = f0 + nt * 32 + l31;
@@ -817,19 +738,12 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     for (int g = 0; g < 4; ++g) {
       const int m = m_w0 + 8 * g + 4 * hh;
       if (m >= p.M) continue;
-      const f32x4 e = f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
-      if (lnf)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, e), wsr,
-                                               (int)((((long long)sl * F + f) * p.M + m) * 4), 0, 16);
-      else
-        *reinterpret_cast<f32x4*>(P + (long long)f * p.M + m) = e;
+      *reinterpret_cast<f32x4*>(P + (long long)f * p.M + m) = f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
     }
   }
 #if TTS_SPLIT_STAMP
   stamp();
 #endif
-  if (lnf && ln_tile_last(p.ln_cnt + tx, nmb * S, reinterpret_cast<int*>(smem)))
-    splitk_tile_ln(p, S, F, f0, BN, wave, lane);
 }
 
 // y[f][m] = epilogue(sum over slices of ws[s][f][m]) for every valid flat row (conv_epilogue's
@@ -1033,11 +947,13 @@ hipError_t conv_split_launch(const ConvParams& p, hipStream_t s, bool* ln_done) 
                                            (size_t)32 * nt * (128 * 4 + 16))
                                 : lds;
       ConvParams q = p;
-      // the kernel's LayerNorm switch: its epilogue (one slice) or its in-launch split-K reduce
-      // (the in-launch split-K reduce, TTS_SPLITK_FUSE=1, is off by default: its results varied between
-      // runs at batch 32 -- an ordering problem of the hand-off not yet found; the separate reduce runs)
-      bool fuse = splitp_ln_ok(p, F, 32 * nt) && (S == 1 || (TTS_SPLITK_FUSE && p.ln_out && p.act_out == ACT_NONE && S <= SKMAX));
-      if (sw(SW_LN_FUSE) > 1 && sw(SW_LN_FUSE) != 7 && sw(SW_LN_FUSE) != (S == 1 ? 3 : 4)) fuse = false;  // (bisection: 3 / 4 = one slice / split-K only)
+      // the kernel's LayerNorm switch: its epilogue applies the post-LN in one-slice launches
+      // (ln_rows.h hand-off); split-K launches reduce and normalise in split_reduce_ln_kernel.
+      // (Round 4 also built an in-launch split-K reduce; its run-to-run bit difference did not
+      // reproduce -- profiles/r04c_splitk_stability.txt -- and it was never faster, so round 6
+      // removed it.)
+      bool fuse = splitp_ln_ok(p, F, 32 * nt) && S == 1;
+      if (sw(SW_LN_FUSE) > 1 && sw(SW_LN_FUSE) != 7 && sw(SW_LN_FUSE) != 3) fuse = false;  // (bisection: 3 = one slice)
       if (!fuse) q.ln_cnt = nullptr;
       if (whole && ldsw <= 160 * 1024) {
         if (nt == 1) hipLaunchKernelGGL((conv_splitp_kernel<true, 1>), dim3(nwg), dim3(256), ldsw, s, q, cg, S, gps);

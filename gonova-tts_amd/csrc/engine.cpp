@@ -90,9 +90,21 @@ struct tts_engine {
 #ifndef TTS_VWS_MIN_CIN
 #define TTS_VWS_MIN_CIN 128
 #endif
+#ifndef TTS_VOC_SPLIT_MINC
+#define TTS_VOC_SPLIT_MINC 128  // fp32 vocoders: resblock convs with >= this many channels run split-precision
+#endif
   static constexpr int VWS_MIN_CIN = TTS_VWS_MIN_CIN;  // (A/B builds: 64 with TTS_F32_SK_MINM=32)
   float* vws = nullptr;
   long long vws_bytes = 0;
+  // fp32 vocoder: its wide resblock convs run as split-precision GEMMs (finalize_vocoder), whose
+  // operands must stay inside f16's range.  Their range word (vrange) is read back after each
+  // forward (one stream sync, fp32 vocoders only); when set, the forward reruns with every layer
+  // on the fp32 MFMA path (voc_no_split) -- the vocoder counterpart of the exact encoder's guard.
+  bool voc_split = false;
+  int* vrange = nullptr;
+  int* vrange_h = nullptr;  // pinned
+  int voc_no_split = 0;
+  long long voc_range_fallbacks = 0;
   // polyphase resampler tables, keyed by the reduced (up, down): [up][nq] fp32 on the device
   struct Resampler { int up, down, nq, n_pre_remove; float* hp; };
   std::vector<Resampler> resamplers;
@@ -139,6 +151,7 @@ struct tts_engine {
     if (vchunk_wav) dev_free(vchunk_wav);
     if (vws) dev_free(vws);
     for (auto& r : resamplers) dev_free(r.hp);
+    if (vrange_h) hipHostFree(vrange_h);
     ac.free_all();
   }
 
@@ -151,13 +164,15 @@ struct tts_engine {
   }
   bool has(const std::string& n) const { return host.count(n) != 0; }
 
-  // nn.Conv1d weight [Cout][Cin][k] -> W[Cout][k][Cin]
-  ConvLayer pack_conv(const std::string& wname, const std::string& bname, int dil, int pad, int dt) {
+  // nn.Conv1d weight [Cout][Cin][k] -> W[Cout][k][Cin]; split: an fp32 layer also gets the
+  // split-precision packing (three f16 MFMAs per product, conv_split.hip)
+  ConvLayer pack_conv(const std::string& wname, const std::string& bname, int dil, int pad, int dt, bool split = false) {
     const HostTensor& w = get(wname);
     if (w.shape.size() != 3) throw TtsError(TTS_ERR_INVALID, wname + ": expected 3-D conv weight");
     std::vector<float> b;
     if (!bname.empty() && has(bname)) b = get(bname).data;
-    return make_conv(w.data, (int)w.shape[0], (int)w.shape[1], (int)w.shape[2], b, dil, pad, dt, allocs);
+    return make_conv(w.data, (int)w.shape[0], (int)w.shape[1], (int)w.shape[2], b, dil, pad, dt, allocs, nullptr,
+                     split && dt == DT_F32);
   }
 
   // nn.ConvTranspose1d weight [Cin][Cout][k], stride s, padding p as a polyphase conv:
@@ -234,10 +249,13 @@ struct tts_engine {
             const HostTensor& dd = get("__cfg__.resblock_dilation_sizes");  // [nk][np]
             d = (int)std::lround(dd.data.at((size_t)j * dd.shape.at(1) + q));
           }
+          // fp32 vocoders: the wide stages' resblock convs (C >= TTS_VOC_SPLIT_MINC) as split-precision
+          // GEMMs -- C1's batch-1 fp32 vocoder ran them on the fp32 MFMA at 15-25 TF/s
+          const bool split = dt == DT_F32 && ch >= TTS_VOC_SPLIT_MINC && ch % 128 == 0;
           v.mrf[i][j][q][0] = pack_conv(pre + "convs1." + std::to_string(q) + ".weight",
-                                        pre + "convs1." + std::to_string(q) + ".bias", d, (ks * d - d) / 2, dt);
+                                        pre + "convs1." + std::to_string(q) + ".bias", d, (ks * d - d) / 2, dt, split);
           v.mrf[i][j][q][1] = pack_conv(pre + "convs2." + std::to_string(q) + ".weight",
-                                        pre + "convs2." + std::to_string(q) + ".bias", 1, (ks - 1) / 2, dt);
+                                        pre + "convs2." + std::to_string(q) + ".bias", 1, (ks - 1) / 2, dt, split);
           // pair-kernel copies (C in {32, 64}, 16-bit): 16x16 fragment-packed
           for (int cv = 0; cv < 2; ++cv) {
             const HostTensor& cw = get(pre + (cv ? "convs2." : "convs1.") + std::to_string(q) + ".weight");
@@ -256,6 +274,16 @@ struct tts_engine {
     v.post_w = (float*)track(upload_f32(t));
     v.post_wh = dt == DT_F32 ? nullptr : track(upload(t, dt));
     v.post_b = get("conv_post.bias").data[0];
+    voc_split = false;
+    for (const auto& st : v.mrf)
+      for (const auto& rb : st)
+        for (const auto& pr : rb) voc_split = voc_split || (dt == DT_F32 && (pr[0].wpk || pr[1].wpk));
+    if (voc_split && !vrange) {
+      HIP_CHECK(dev_malloc(&vrange, 16));
+      HIP_CHECK(hipMemset(vrange, 0, 16));
+      track(vrange);
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&vrange_h), 16, hipHostMallocDefault));
+    }
     v.loaded = true;
   }
 
@@ -331,7 +359,9 @@ struct tts_engine {
     ConvParams p = conv_params_default();
     p.act_out = act_out; p.out_slope = out_slope;
     p.x = x; p.sxb = sxb; p.sxr = sxr; p.x_len = x_len; p.x_rows = x_rows;
-    p.w = L.w; p.w_ld = L.taps * L.Cin; p.wpk = L.wpk;
+    p.w = L.w; p.w_ld = L.taps * L.Cin; p.wpk = L.wpk; p.w_unscale = L.wpk_unscale;
+    p.range_flag = vrange;     // the split-precision layers' range guard (vocoder_forward)
+    p.no_split = voc_no_split;  // its fallback: the same layers on the fp32 MFMA path
     p.bias = L.bias;
     p.y = y; p.syb = syb; p.syr = syr;
     p.r1 = r1; p.r2 = r2; p.srb = srb; p.srr = srr;
@@ -348,9 +378,33 @@ struct tts_engine {
     launch_conv_checked(p, dt, s, &prof, fl);
   }
 
-  // HiFi-GAN V1 forward (oracle/vocoder.py vocoder_forward; HF:1435-1475).
+  // The forward with the split layers' range guard (fp32 vocoders with split-packed convs): one
+  // read of the range word after the forward, and a rerun on the fp32 MFMA path when it is set.
   void vocoder_forward(const float* mel, const int* mel_lens, int B, int T, float* wav, long long swb,
                        hipStream_t s) {
+    if (!voc_split || voc_no_split) {
+      vocoder_forward_once(mel, mel_lens, B, T, wav, swb, s);
+      return;
+    }
+    HIP_CHECK(hipMemsetAsync(vrange, 0, 4, s));
+    vocoder_forward_once(mel, mel_lens, B, T, wav, swb, s);
+    HIP_CHECK(hipMemcpyAsync(vrange_h, vrange, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (*vrange_h == 0) return;
+    ++voc_range_fallbacks;
+    voc_no_split = 1;
+    try {
+      vocoder_forward_once(mel, mel_lens, B, T, wav, swb, s);
+    } catch (...) {
+      voc_no_split = 0;
+      throw;
+    }
+    voc_no_split = 0;
+  }
+
+  // HiFi-GAN V1 forward (oracle/vocoder.py vocoder_forward; HF:1435-1475).
+  void vocoder_forward_once(const float* mel, const int* mel_lens, int B, int T, float* wav, long long swb,
+                            hipStream_t s) {
     if (!voc.loaded) throw TtsError(TTS_ERR_STATE, "vocoder weights not loaded/finalized");
     const int dt = cfg.vocoder_dtype;
     reserve_vocoder(B, T);

@@ -93,13 +93,9 @@ int conv_last_kernels();
 enum ProfKind : int { PK_CONV_GEMM = 0, PK_CONV_XRES = 1, PK_RETIRED = 2 /* mrf_fused, removed */, PK_MRF_PAIR = 3, PK_MRF_CHAIN = 4, PK_UPSAMPLE = 5,
                       PK_CONV_SPLIT = 6, PK_ATTN = 7 /* fused relative-position attention */,
                       PK_AC_ELEM = 8 /* the acoustic model's non-GEMM launches: LN, GLU/depthwise, transposes, adaptor */,
-                      PK_CONV_MT = 9 /* macro-tiled 16-bit acoustic GEMMs (conv_mt.hip) */, PK_N = 10 };
+                      PK_N = 9 };
 int conv_gemm_kind(int dtype, const ConvParams& p);
 
-// Macro-tiled 16-bit implicit-GEMM conv (conv_mt.hip): 8-wave blocks, both operands through LDS by
-// LDS-DMA.  *ln_done: whether the launch applied p.ln_out's LayerNorm itself (y is then not written).
-bool conv_mt_eligible(int dtype, const ConvParams& p);
-hipError_t conv_mt_launch(int dtype, const ConvParams& p, hipStream_t s, bool* ln_done);
 
 // fp32 conv as three f16 MFMAs (conv_split.hip): an fp32 layer whose ConvParams::wpk is a
 // split-packed copy (frag_pack_split) runs here when eligible (Cin % 64 == 0, no head batching)

@@ -18,8 +18,8 @@
 // arriver's agent-scope acquire drops its CU's stale lines before its plain loads.  An explicit
 // release fence (TTS_LN_RELEASE=1: buffer_wbl2 sc1 + wait per block) writes back the XCD's whole
 // L2 and cost 0.3 ms of a 6.1 ms batch-32 forward (profiles/r04b_ab_ln_release.txt); the results
-// were bit-identical and run-to-run stable with and without it, the in-launch split-K reduce
-// included (tools/splitk_stability.py, profiles/r04c_splitk_stability.txt).
+// were bit-identical and run-to-run stable with and without it, the (since removed) in-launch
+// split-K reduce included (profiles/r04c_splitk_stability.txt).
 #ifndef TTS_LN_RELEASE
 #define TTS_LN_RELEASE 0
 #endif

@@ -236,11 +236,9 @@ inline ConvLayer make_conv(const std::vector<float>& w, int co, int ci, int k, c
     for (int c = 0; c < ci; ++c)
       for (int j = 0; j < k; ++j) p[((size_t)o * k + j) * ci + c] = w[((size_t)o * ci + c) * k + j] * s;
   }
-  if (dt == DT_F32 && split)  // the split halves are f16: hi = f16(w) must be finite (tts_hip.h, TTS_ENCODER_EXACT)
+  if (dt == DT_F32 && split)  // split packing scales the layer by a power of two (frag_pack_split): any finite weights
     for (float v : p)
-      if (!(std::fabs(v) < 65504.f))
-        throw TtsError(TTS_ERR_INVALID, "weight magnitude " + std::to_string(v) +
-                                            " outside the f16 range of the exact-duration encoder (use encoder_precision fast or an fp32 model)");
+      if (!std::isfinite(v)) throw TtsError(TTS_ERR_INVALID, "non-finite weight in a split-precision layer");
   ConvLayer L;
   L.w = upload(p, dt);
   allocs.push_back(L.w);

@@ -21,8 +21,6 @@ enum Sw : int {
   SW_LN_FUSE,      // TTS_LN_FUSE=0: acoustic post-LNs as their own launches; 7: in every eligible GEMM launch (2-6: bisection)
   SW_SPLIT_NT1,    // TTS_SPLIT_NT1=0: split GEMMs always on 64-row tiles; 1: 32-row tiles wherever eligible (default: small grids)
   SW_XRES_ORDER,   // TTS_XRES_ORDER=1: multi-tap DMA conv_xres launches on an XCD-ordered grid (M block fastest); 2: every conv_xres launch
-  SW_CONV_MT,      // TTS_CONV_MT=1: the acoustic 16-bit GEMMs on conv_mt (k = 3 layers on conv_tap_kernel; 2: on conv_mt_kernel) instead of conv_xres (default 0)
-  SW_MT_TILE,      // TTS_MT_TILE=0..3: force a conv_mt_kernel tile configuration, 4..10 a conv_tap_kernel one (tests; default: chosen per launch)
   SW_PAIR_SPLIT,   // TTS_PAIR_SPLIT=0/1: the channel-split pair form never / wherever possible (default: small C >= 128 grids)
   SW_VP_BATCH,     // TTS_VP_BATCH=0: the variance predictors' first convs / LayerNorms as separate launches (fp32 encoder)
   SW_DEC_TRIM,     // TTS_DEC_TRIM=0/1: with predicted durations the decoder never / always runs at the longest utterance's frames (default: budgets over 8 frames per token)

@@ -104,7 +104,11 @@ def load_library(path: str = LIB_PATH):
                                "(there is no CPU fallback)")
         lib = ctypes.CDLL(path)
         for name, res, args in C_API:
-            fn = getattr(lib, name)
+            # (an older A/B build may lack a newer entry point: it is left unbound, and a call to
+            # it raises AttributeError; tests/test_capi.py checks the product library has them all)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
             fn.restype = res
             fn.argtypes = args
         _lib = lib

@@ -86,9 +86,8 @@ typedef struct tts_config {
  * round differently near .5).  With acoustic_dtype = F32 both are plain fp32. */
 enum { TTS_ENCODER_EXACT = 0, TTS_ENCODER_FAST = 1, TTS_ENCODER_F32 = 2 };
 /* Range limit of EXACT: its split GEMMs and attention hold every fp32 operand as two f16 halves,
- * so activations and encoder-side weights must stay below 65504 in magnitude (f16 max).
- * tts_engine_finalize rejects encoder-side weights outside that range (TTS_ERR_INVALID naming
- * the tensor; use FAST or an fp32 acoustic_dtype for such a checkpoint).  Activations are
+ * so activations must stay below 65504 in magnitude (f16 max); weights are stored at a
+ * power-of-two scale per layer (round 6), so any finite weights are taken.  Activations are
  * checked on the device (ABI 4): every split GEMM and the split attention test the f16 high half
  * of each operand they stage and, when one is inf or NaN (|x| >= 65520, or a NaN input), set the
  * engine's range word.  The forward itself stays asynchronous; the caller reads the word with
@@ -96,6 +95,12 @@ enum { TTS_ENCODER_EXACT = 0, TTS_ENCODER_FAST = 1, TTS_ENCODER_F32 = 2 };
  * with TTS_ENCODER_F32 (the same fp32 layers on the exact fp32 MFMA kernels, ~3x slower on the
  * encoder side, no range limit).  TTS_ENCODER_F32 is a run-time setting only
  * (tts_acoustic_set_precision), not a tts_config value. */
+
+/* fp32 vocoders (vocoder_dtype = TTS_DTYPE_F32): the resblock convs of stages with >= 128 channels
+ * run as split-precision GEMMs (three f16 MFMAs per product, ~2^-21 relative, like the exact
+ * encoder).  tts_vocoder_forward / _chunk then read the layers' range word once at the end of the
+ * call (one sync of `stream`) and, if an activation left f16's range, rerun the forward with every
+ * layer on the fp32 MFMA path; 16-bit vocoders are unaffected and stay asynchronous. */
 
 /* Number of HIP devices visible to this process. */
 int tts_device_count(void);
@@ -186,7 +191,7 @@ int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, doubl
 /* Process-wide switch selecting an alternative kernel path (A/B runs, the parity tests'
  * reference paths): TTS_REL_ATTN, TTS_MRF_FUSED, TTS_MRF_CHAIN, TTS_POST_FUSE, TTS_UP_STREAM,
  * TTS_XRES_NARROW, TTS_XRES_NT, TTS_PAIR_DIV, TTS_ATTN_KSPLIT, TTS_SPLIT_WHOLE, TTS_XRES_DMA,
- * TTS_LN_FUSE, TTS_SPLIT_NT1, TTS_XRES_ORDER, TTS_CONV_MT, TTS_MT_TILE, TTS_PAIR_SPLIT, TTS_VP_BATCH, TTS_DEC_TRIM.  Each
+ * TTS_LN_FUSE, TTS_SPLIT_NT1, TTS_XRES_ORDER, TTS_PAIR_SPLIT, TTS_VP_BATCH, TTS_DEC_TRIM.  Each
  * starts from its environment variable, read once; value -1 restores the built-in default.
  * Applies to launches enqueued after the call (use from one thread while no forward runs). */
 int tts_set_switch(const char* name, int value);

@@ -1,10 +1,10 @@
 """GPU parity of the HIP acoustic model (FastSpeech2-Conformer, through the C-ABI)
 against the CPU oracle and the transformers golden vectors.
 
-Tolerances: fp32 mel atol 2e-4 / rtol 2e-3 (8 conformer layers of fp32 GEMMs vs
-NumPy/torch BLAS); durations exact (except a logit within 1e-3 of a rounding
-boundary); 16-bit mel through tests/parity.py (rel-RMS and max-abs, ~2x the measured error) with
-durations forced.
+Tolerances: fp32 mel atol 1e-5 / rtol 1e-4 (FP32_ATOL / FP32_RTOL below: SURVEY.md §8c's fp32
+bar; measured max error 6.0e-6, profiles/r04zc_fp32_mel_error.txt); durations exact (except a
+logit within 1e-3 of a rounding boundary); 16-bit mel through tests/parity.py (rel-RMS and
+max-abs, ~2x the measured error) with durations forced.
 """
 import os
 
@@ -88,6 +88,7 @@ def test_acoustic_fp32_ragged_batch_matches_oracle(aw):
     rng = np.random.default_rng(3)
     ids_list = [rng.integers(1, 78, size=n) for n in (20, 7, 33, 1)]
     mel, mel_lens, dur = run(eng, ids_list, t_cap=200)
+    skipped = []
     for b, ids in enumerate(ids_list):
         ref = acoustic_forward(ids, aw)
         # durations: exact unless the oracle's exp(x)-1 is within 1e-3 of a .5 rounding boundary
@@ -95,10 +96,13 @@ def test_acoustic_fp32_ragged_batch_matches_oracle(aw):
         ok = frac > 1e-3
         np.testing.assert_array_equal(dur[b, :len(ids)][ok], ref["durations"][ok])
         if not np.array_equal(dur[b, :len(ids)], ref["durations"]):
+            skipped.append(b)  # a boundary token rounded the other way: the frame grids differ
             continue
         L = int(mel_lens[b])
         assert L == min(ref["mel"].shape[0], 200)
         np.testing.assert_allclose(mel[b, :L], ref["mel"][:L], atol=FP32_ATOL, rtol=FP32_RTOL)
+    # the mel comparison may skip at most one utterance (a 1e-3 boundary case), never the batch
+    assert len(skipped) <= 1, skipped
 
 
 def test_acoustic_fp32_split_k_batch_invariant(aw):
@@ -308,7 +312,6 @@ def test_short_row_tiles_bit_identical(aw, dtype, switch):
     rng = np.random.default_rng(12)
     ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70)]
     durs = [np.full(len(x), 3) for x in ids_list]
-    switch("TTS_CONV_MT", 0)       # conv_xres runs the acoustic GEMMs (the default; conv_mt is opt-in)
     switch("TTS_XRES_NARROW", 0)   # 128-channel tiles: the tile-height pair
     switch("TTS_XRES_NT", 4)
     big, lb, _ = run(eng, ids_list, t_cap=432, durations=durs)
@@ -371,7 +374,6 @@ def test_dma_staged_ffn_bit_identical(aw, dtype, switch):
     rng = np.random.default_rng(43)
     ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70, 127, 129, 9, 33)]
     outs = {}
-    switch("TTS_CONV_MT", 0)
     switch("TTS_XRES_NARROW", 0)
     for dma in (None, 3, 2):
         for nt in (2, 4):
@@ -427,7 +429,6 @@ def test_xcd_ordered_xres_grid_bit_identical(aw, dtype, switch):
     rng = np.random.default_rng(46)
     ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70, 127, 129, 9, 33)]
     outs = {}
-    switch("TTS_CONV_MT", 0)
     for order in (0, 1, 2):
         for nt in (None, 2):
             switch("TTS_XRES_ORDER", order)
@@ -439,49 +440,6 @@ def test_xcd_ordered_xres_grid_bit_identical(aw, dtype, switch):
     for k, (m, l, d) in outs.items():
         assert np.array_equal(d, ref_d) and np.array_equal(l, ref_l), k
         assert np.array_equal(m, ref_m), k
-
-
-@pytest.mark.parametrize("dtype", ["bf16", "f16"])
-def test_macro_tile_gemm_configs_bit_identical(aw, dtype, switch):
-    """conv_mt (csrc/conv_mt.hip: 8-wave blocks, both operands through LDS by LDS-DMA; opt-in,
-    TTS_CONV_MT=1) runs the 16-bit acoustic GEMMs, the k = 3 FFN convs on its multi-tap form (one
-    X tile shared by the taps).  Its tile configurations (256 x 224, 192 x 224, 384 x 112 with the post-LN in the
-    launch, 128 x 128; multi-tap 128 x 448, 192 x 224, 256 x 224, 128 x 224, 128 x 128;
-    TTS_MT_TILE forces one wherever the layer's channels divide)
-    share one K order, so predicted durations, frame counts and mel agree bit for bit with the
-    automatic choice, with the post-LN fused or as its own launch (TTS_LN_FUSE=0), on a ragged
-    batch whose lengths cross 112-, 128- and 224-row edges; batch 1 equals its row of the batch;
-    the mel matches the oracle and stays within the 16-bit tolerance of the conv_xres path."""
-    eng = engine(dtype, aw)
-    rng = np.random.default_rng(47)
-    ids_list = [rng.integers(1, 78, size=n) for n in (144, 1, 65, 70, 127, 129, 9, 33)]
-    outs = {}
-    switch("TTS_CONV_MT", 1)  # (opt-in: conv_xres is the default)
-    for tile in (None, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10):  # 4..10: the multi-tap (k = 3) configurations
-        switch("TTS_MT_TILE", tile)
-        outs[tile] = run(eng, ids_list, t_cap=8 * 144)
-    switch("TTS_MT_TILE", None)
-    switch("TTS_LN_FUSE", 0)
-    outs["ln0"] = run(eng, ids_list, t_cap=8 * 144)
-    switch("TTS_LN_FUSE", None)
-    ref_m, ref_l, ref_d = outs[None]
-    for k, (m, l, d) in outs.items():
-        assert np.array_equal(d, ref_d) and np.array_equal(l, ref_l), k
-        assert np.array_equal(m, ref_m), k
-    solo_m, solo_l, solo_d = run(eng, ids_list[4:5], t_cap=8 * 144)
-    L = int(ref_l[4])
-    assert int(solo_l[0]) == L and np.array_equal(solo_m[0, :L], ref_m[4, :L])
-    durs = [ref_d[b, :len(x)] for b, x in enumerate(ids_list)]
-    forced, fl, _ = run(eng, ids_list, t_cap=8 * 144, durations=durs)
-    switch("TTS_CONV_MT", 0)
-    xres, xl, _ = run(eng, ids_list, t_cap=8 * 144, durations=durs)
-    switch("TTS_CONV_MT", 1)
-    for b in (0, 2, 4, 5):
-        L = int(fl[b])
-        assert int(xl[b]) == L
-        ref = acoustic_forward(ids_list[b], aw, durations=durs[b])
-        check(f"acoustic {dtype} conv_mt b={b}", forced[b, :L], ref["mel"], kind="ac_" + dtype)
-        check(f"acoustic {dtype} conv_mt vs conv_xres b={b}", forced[b, :L], xres[b, :L], kind="ac_" + dtype)
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])

@@ -90,7 +90,7 @@ def test_abi_version_and_sized_config_without_gpu():
 
 def test_switches_restore_the_previous_value():
     """switches() and the conftest fixture put back the value a switch had (an environment
-    setting such as TTS_MRF_CHAIN=0 from tools/ab_env.sh), not the built-in default."""
+    setting such as TTS_MRF_CHAIN=0 from tools/ab.sh), not the built-in default."""
     engine.set_switch("TTS_MRF_CHAIN", 0)  # stands in for an environment value
     try:
         with engine.switches(TTS_MRF_CHAIN=1, TTS_PAIR_DIV=4):

@@ -33,6 +33,6 @@ def test_no_kernel_uses_scratch(kernels):
 def test_hot_kernels_present(kernels):
     """the metadata covers the kernels the C2 / C3 / C5 paths launch"""
     names = " ".join(k["name"] for k in kernels)
-    for k in ("mrf_pair_kernel", "mrf_chain_kernel", "upsample_stream_kernel", "conv_xres_kernel", "conv_mt_kernel",
+    for k in ("mrf_pair_kernel", "mrf_chain_kernel", "upsample_stream_kernel", "conv_xres_kernel",
               "rel_attn_kernel", "conv_splitp_kernel"):
         assert k in names, k

@@ -4,7 +4,8 @@ response contract (`services/tts/server.py:143-164, 215-224, 268-298`) end to en
 Config C1 through the service: fp32 engine, one client and two concurrent clients; every
 binary frame is raw float32 PCM of one sentence (split as the reference splits,
 `core/synthesizer.py:48-99`) and must equal the model's own `generate(sentence)` and the CPU
-oracle pipeline (fp32 tolerance, the e2e golden's atol 2e-4)."""
+oracle pipeline (fp32 tolerance: atol 2e-5 / rtol 1e-4 against the oracle, 1e-5 / 1e-4 against
+generate())."""
 import json
 import threading
 

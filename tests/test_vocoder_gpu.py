@@ -111,6 +111,26 @@ def test_vocoder_fp32_matches_golden_and_oracle(vw, tag):
     np.testing.assert_allclose(wav, vocoder_forward(mel, vw), atol=1e-5, rtol=1e-4)
 
 
+def test_vocoder_fp32_split_layers_range_guard(vw):
+    """fp32 vocoders run their 256- and 128-channel resblock convs as split-precision GEMMs
+    (round 6; C1).  Their operands must fit f16: with one stage-0 conv scaled by 2e5 the conv after
+    it stages values far past 65504, the layers' range word trips, and the engine reruns the forward
+    on the fp32 MFMA path by itself -- the waveform is finite and matches the fp32 oracle of the
+    scaled weights; the unscaled engine is unaffected."""
+    big = dict(vw)
+    big["resblocks.0.convs1.0.weight"] = vw["resblocks.0.convs1.0.weight"] * np.float32(2e5)
+    eng = HipEngine(DEV, vocoder_dtype="f32")
+    eng.load_weights(vocoder=big)
+    mel = G["voc_a_mel"]
+    wav = eng.vocoder(torch.from_numpy(mel)[None].to(DEV)).cpu().numpy()[0]
+    ref = vocoder_forward(mel, big)
+    assert np.isfinite(wav).all()
+    err = float(np.abs(wav - ref).max())
+    print(f"range-guard fallback: max|err| vs fp32 oracle {err:.2e}, max|ref| {float(np.abs(ref).max()):.3f}")
+    np.testing.assert_allclose(wav, ref, atol=1e-4, rtol=1e-3)
+    eng.close()
+
+
 def test_vocoder_fp32_ragged_batch(vw):
     eng = engine_for("f32", vw)
     rng = np.random.default_rng(5)

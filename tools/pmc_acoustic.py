@@ -13,7 +13,7 @@ ITERS = 4  # tools/acoustic_prof.py
 
 
 def short(name):
-    for k in ("conv_mt", "conv_xres", "conv_splitp", "conv_split_kernel", "split_reduce", "conv_gemm", "rel_attn_split",
+    for k in ("conv_xres", "conv_splitp", "conv_split_kernel", "split_reduce", "conv_gemm", "rel_attn_split",
               "rel_attn_kernel", "layernorm8", "layernorm_kernel", "glu_dwconv", "transpose_v", "ln_linear1"):
         if k in name:
             return k

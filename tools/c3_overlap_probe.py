@@ -1,0 +1,83 @@
+"""Probe: C3 (batch-32 tokens -> FS2-Conformer -> HiFi-GAN, bf16) as one engine on one stream
+(the bench line) against two engines on two streams each taking half the batch, so one half's
+latency-bound acoustic pass overlaps the other half's MFMA-bound vocoder:
+  seq      one engine, B = 32: acoustic then vocoder per step
+  conc     two engines, B = 16 each, both halves started together every step
+  stagger  two engines, B = 16 each; the second half's stream starts after the first half's
+           acoustic pass (one event), so its acoustic pass runs beside the first half's vocoder
+Prints ms per 32-utterance step (device-resident inputs, 10 timed steps after 3 warmups).
+
+usage (GPU box): python3 tools/c3_overlap_probe.py
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from gonova_tts_amd.engine import HipEngine
+    from gonova_tts_amd.weights import make_acoustic_weights, make_vocoder_weights
+    B, N, dur = 32, 144, 6
+    T = N * dur
+    aw, vw = make_acoustic_weights(seed=0, fixed_duration=dur), make_vocoder_weights(seed=0)
+    g = torch.Generator(device="cpu").manual_seed(2000)
+    tok = torch.randint(1, 78, (B, N), generator=g, dtype=torch.int32).cuda()
+    tl = torch.full((B,), N, dtype=torch.int32, device="cuda")
+    wav = torch.empty((B, T * 256), dtype=torch.float32, device="cuda")
+    steps = int(os.environ.get("PROBE_STEPS", "10"))
+
+    def timed(fn, warm=3):
+        for _ in range(warm):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3 / steps
+
+    e1 = HipEngine("cuda:0", vocoder_dtype="bf16", acoustic_dtype="bf16", max_batch=B, max_frames=T, max_tokens=N)
+    e1.load_weights(vocoder=vw, acoustic=aw)
+
+    def seq():
+        mel, ml = e1.acoustic(tok, tl, T)
+        e1.vocoder(mel, ml, out=wav)
+
+    t_seq = timed(seq)
+    h = B // 2
+    e2 = HipEngine("cuda:0", vocoder_dtype="bf16", acoustic_dtype="bf16", max_batch=h, max_frames=T, max_tokens=N)
+    e2.load_weights(vocoder=vw, acoustic=aw)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    ev = torch.cuda.Event()
+
+    def halves(stagger):
+        cur = torch.cuda.current_stream()
+        sa.wait_stream(cur)
+        sb.wait_stream(cur)
+        with torch.cuda.stream(sa):
+            mel, ml = e1.acoustic(tok[:h], tl[:h], T, stream=sa)
+            if stagger:
+                ev.record(sa)
+            e1.vocoder(mel, ml, out=wav[:h], stream=sa)
+        with torch.cuda.stream(sb):
+            if stagger:
+                sb.wait_event(ev)
+            mel2, ml2 = e2.acoustic(tok[h:], tl[h:], T, stream=sb)
+            e2.vocoder(mel2, ml2, out=wav[h:], stream=sb)
+        cur.wait_stream(sa)
+        cur.wait_stream(sb)
+
+    t_conc = timed(lambda: halves(False))
+    t_stag = timed(lambda: halves(True))
+    t_seq2 = timed(seq)
+    print(f"C3 ms per 32-utterance step: seq {t_seq:.3f} / {t_seq2:.3f}, conc {t_conc:.3f}, stagger {t_stag:.3f}")
+    e1.close()
+    e2.close()
+
+
+if __name__ == "__main__":
+    main()

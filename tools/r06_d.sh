@@ -3,7 +3,7 @@
 # library, then C1 generate() against the round-5 library (base), alternated
 set -o pipefail
 R=$GRAFT_REPO_ROOT; T=${1:-r06d}; O=$R/gpurun_out/$T; mkdir -p $O; cd $R
-timeout -k 10 1000 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ > $O/gputest.log 2>&1 || { grep -E "FAIL|Error|error" $O/gputest.log | head -20; tail -30 $O/gputest.log; exit 1; }
+timeout -k 10 1000 python3 -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/ > $O/gputest.log 2>&1 || { grep -E "FAIL|Error|error" $O/gputest.log | head -20; tail -30 $O/gputest.log; exit 1; }
 tail -2 $O/gputest.log
 grep -E "range-guard fallback|service frame" $O/gputest.log | head
 cd /tmp

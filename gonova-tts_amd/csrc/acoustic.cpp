@@ -499,6 +499,13 @@ struct AcousticModel::Impl {
         // V read from the QKV rows (transposed in LDS: no Vt launch)
         // fp32 layers of a 16-bit model (the exact-duration encoder) in split precision, like their GEMMs
         const bool split = dt == DT_F32 && this->dt != DT_F32 && !enc_f32;
+        if (TTS_BOUNDS_CHECK) {  // (diagnostic builds: runtime.h)
+          const long long e = dtype_size(dt);
+          std::string why;
+          if (!dev_range_ok(QKV, (long long)B * Tp * 3 * D * e, &why) || !dev_range_ok(O, (long long)B * Tp * D * e, &why) ||
+              !dev_range_ok(L.ptab, 2LL * rmax * D * e, &why))
+            throw TtsError(TTS_ERR_INVALID, "bounds: attention " + why);
+        }
         prof_launch(PK_ATTN, 6.0 * D * (double)B * Tm * Tm, s, [&] { return launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, L.ptab, lens, B, Tm, Tp, D, H, rmax, scale,
                                   O, s, range_flag); });
         run_ln(L.out, O, Tp, lens, Y, Tp, B, dt, s, 1.f, Xb, Xb, L.ln_att, nullptr);

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -44,8 +45,8 @@ inline size_t dtype_size(int dt) { return dt == DT_F32 ? 4 : 2; }
 // torch's allocator there, server.py:456-465, which never sees these buffers).
 struct DevRegistry {
   std::mutex mu;
-  std::unordered_map<void*, std::pair<int, size_t>> live;  // buffer -> (device, bytes)
-  std::unordered_map<int, long long> bytes;                // device -> live bytes
+  std::map<uintptr_t, std::pair<int, size_t>> live;  // buffer -> (device, bytes), address-ordered
+  std::unordered_map<int, long long> bytes;          // device -> live bytes
 };
 inline DevRegistry& dev_registry() {
   static DevRegistry r;
@@ -60,7 +61,7 @@ inline hipError_t dev_malloc(T** p, size_t n) {
   (void)hipGetDevice(&dev);
   DevRegistry& r = dev_registry();
   std::lock_guard<std::mutex> g(r.mu);
-  r.live[q] = {dev, n};
+  r.live[reinterpret_cast<uintptr_t>(q)] = {dev, n};
   r.bytes[dev] += (long long)n;
   *p = static_cast<T*>(q);
   return e;
@@ -70,13 +71,30 @@ inline hipError_t dev_free(void* p) {
   {
     DevRegistry& r = dev_registry();
     std::lock_guard<std::mutex> g(r.mu);
-    auto it = r.live.find(p);
+    auto it = r.live.find(reinterpret_cast<uintptr_t>(p));
     if (it != r.live.end()) {
       r.bytes[it->second.first] -= (long long)it->second.second;
       r.live.erase(it);
     }
   }
   return hipFree(p);
+}
+// Diagnostic builds (-DTTS_BOUNDS_CHECK=1): whether [p, p + n) lies inside one live library buffer
+// (pointers the library did not allocate -- the caller's torch tensors -- are not judged: true)
+inline bool dev_range_ok(const void* p, long long n, std::string* why) {
+  if (!p || n <= 0) return true;
+  DevRegistry& r = dev_registry();
+  std::lock_guard<std::mutex> g(r.mu);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  auto it = r.live.upper_bound(a);
+  if (it == r.live.begin()) return true;
+  --it;
+  if (a >= it->first + it->second.second) return true;  // not a library buffer
+  if (a + (uintptr_t)n <= it->first + it->second.second) return true;
+  if (why)
+    *why = "needs " + std::to_string(n) + " bytes at offset " + std::to_string(a - it->first) + " of a " +
+           std::to_string(it->second.second) + "-byte buffer";
+  return false;
 }
 inline long long dev_bytes(int dev) {
   DevRegistry& r = dev_registry();
@@ -307,10 +325,41 @@ struct Profiler {
   }
 };
 
+#ifndef TTS_BOUNDS_CHECK
+#define TTS_BOUNDS_CHECK 0  // diagnostic builds: every conv launch's operand extents against the buffers
+#endif
+// the byte extents a conv launch can touch, checked against the library's buffers (diagnostic)
+inline void conv_bounds_check(const ConvParams& p, int dt) {
+  const long long e = dt == DT_F32 ? 4 : 2;
+  const long long F = (long long)p.B * p.x_rows;
+  auto need = [&](const char* what, const void* q, long long bytes) {
+    std::string why;
+    if (!dev_range_ok(q, bytes, &why))
+      throw TtsError(TTS_ERR_INVALID, std::string("bounds: ") + what + " " + why + " (M " + std::to_string(p.M) +
+                                          ", Cin " + std::to_string(p.Cin) + ", taps " + std::to_string(p.taps) +
+                                          ", B " + std::to_string(p.B) + ", rows " + std::to_string(p.x_rows) + "/" +
+                                          std::to_string(p.y_rows) + ", rows_pad " + std::to_string(p.rows_pad) + ")");
+  };
+  if (p.nh == 1 && !p.up_s) {
+    need("x", p.x, ((long long)(p.B - 1) * p.sxb + (long long)(p.x_rows - 1) * p.sxr + p.Cin) * e);
+    need("y", p.y, ((long long)(p.B - 1) * p.syb + (long long)(p.y_rows - 1) * p.syr + p.M) * e);
+    if (p.r1) need("r1", p.r1, ((long long)(p.B - 1) * p.srb + (long long)(p.y_rows - 1) * p.srr + p.M) * e);
+    if (p.r2) need("r2", p.r2, ((long long)(p.B - 1) * p.srb + (long long)(p.y_rows - 1) * p.srr + p.M) * e);
+    if (p.ln_out) need("ln_out", p.ln_out, ((long long)(p.B - 1) * p.syb + (long long)(p.y_rows - 1) * p.syr + p.M) * e);
+  }
+  need("bias", p.bias, (long long)p.M * 4);
+  if (p.ws) need("ws", p.ws, p.ws_bytes);
+  if (p.x_len) need("x_len", p.x_len, (long long)p.B * 4);
+  if (p.y_len) need("y_len", p.y_len, (long long)p.B * 4);
+  if (p.ln_cnt) need("ln_cnt", p.ln_cnt, (long long)p.ln_cnt_n * 4);
+  (void)F;
+}
+
 // Launch one implicit-GEMM conv (validates, optionally profiles).
 inline void launch_conv_checked(const ConvParams& p, int dt, hipStream_t s, Profiler* prof, double flops) {
   const char* why = nullptr;
   if (conv_gemm_check(p, dt, &why)) throw TtsError(TTS_ERR_INVALID, std::string("conv: ") + why);
+  if (TTS_BOUNDS_CHECK) conv_bounds_check(p, dt);
   if (prof && prof->on) {
     Profiler::Rec r{prof->get(), prof->get(), flops, conv_gemm_kind(dt, p)};
     HIP_CHECK(hipEventRecord(r.a, s));

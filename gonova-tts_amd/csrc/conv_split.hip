@@ -78,7 +78,11 @@ __device__ inline void split8(f32x4 a, f32x4 b, uint4& hi, uint4& lo) {
   lo = uint4{l0.x, l0.y, l1.x, l1.y};
 }
 
-template <int NT, int UW>
+// KQ: k-steps per weight-ring slot -- 4, or 2 / 1 for 64- / 32-channel groups (the fp32 vocoder's
+// stage-2 / stage-3 convs), so a group always has an even number of slots.  (At M = 32 -- stage 3 --
+// three of the four waves recompute the one 32-channel block and store nothing: the split form is
+// still ~5x the fp32 MFMA's rate per product, and each wave has a SIMD of its own.)
+template <int NT, int UW, int KQ = 4>
 __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG) {
   typedef half8 Frag;
   constexpr int WM = 4 / UW;  // waves along M; UW waves along utterances (same weights)
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
   const int PL = RU * RS;                // bytes per LDS plane
   const int KS = CG / 16;                // k-steps per tap and group
   const int lks = __builtin_ctz(KS);
-  const int QT = p.taps * KS / 4;        // weight quads per group (even: CG >= 128)
+  const int QT = p.taps * KS / KQ;       // weight-ring slots per group (even: 8 per 128 channels / 4 per 64)
   const int x_start = n0 - p.pad;
   const char* xl = smem + (wu * R + l31) * RS + hh * 16;
 
@@ -184,24 +188,24 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
   };
 
   for (int g0 = 0; g0 < p.Cin; g0 += CG) {
-    Frag a0[8], a1[8];  // quad ring: [0..3] hi, [4..7] lo
+    Frag a0[2 * KQ], a1[2 * KQ];  // slot ring: [0, KQ) hi, [KQ, 2 KQ) lo
     // quad qq of this group: k-steps 4qq .. 4qq+3 (never across a tap: KS % 4 == 0)
 #define TTS_SPLIT_LOADQ(A_, QQ_)                                                                     \
     do {                                                                                             \
-      const int kq_ = 4 * (QQ_);                                                                     \
+      const int kq_ = KQ * (QQ_);                                                                    \
       const int o_ = (((kq_ >> lks) * KST + g0 / 16 + (kq_ & (KS - 1))) * 1024) +                    \
                      (((QT - 1 - (QQ_)) >> 31) & 0x40000000); /* out of range past the group */      \
-      _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                             \
+      _Pragma("unroll") for (int j_ = 0; j_ < KQ; ++j_) {                                            \
         A_[j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_hi, lofs + j_ * 1024, o_, 0)); \
-        A_[4 + j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_lo, lofs + j_ * 1024, o_, 0)); \
+        A_[KQ + j_] = __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(rs_lo, lofs + j_ * 1024, o_, 0)); \
       }                                                                                              \
       __builtin_amdgcn_sched_barrier(0);                                                             \
     } while (0)
 #define TTS_SPLIT_MMAQ(A_, QQ_)                                                                      \
     do {                                                                                             \
-      const int kq_ = 4 * (QQ_);                                                                     \
+      const int kq_ = KQ * (QQ_);                                                                    \
       const char* bq_ = xl + (kq_ >> lks) * p.dil * RS + (kq_ & (KS - 1)) * 32;                      \
-      _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                             \
+      _Pragma("unroll") for (int j_ = 0; j_ < KQ; ++j_) {                                            \
         Frag bh_[NT], bl_[NT];                                                                       \
         _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_) {                                       \
           bh_[nt_] = *reinterpret_cast<const Frag*>(bq_ + nt_ * 32 * RS + j_ * 32);                  \
@@ -210,7 +214,7 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
         _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_) {                                       \
           acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bh_[nt_], acc[nt_], 0, 0, 0);    \
           acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[j_], bl_[nt_], acc[nt_], 0, 0, 0);    \
-          acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[4 + j_], bh_[nt_], acc[nt_], 0, 0, 0); \
+          acc[nt_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A_[KQ + j_], bh_[nt_], acc[nt_], 0, 0, 0); \
         }                                                                                            \
       }                                                                                              \
     } while (0)
@@ -221,7 +225,7 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(ConvParams p, int CG
       // quads of MFMAs cover its latency, and no load lands in a register an MFMA of the quad
       // just issued still reads -- a 2-slot ring at one row tile was register-renamed by the
       // compiler, whose copies then waited for every load at the end of each iteration)
-      Frag a2[8], a3[8];
+      Frag a2[2 * KQ], a3[2 * KQ];
       TTS_SPLIT_LOADQ(a0, 0);
       TTS_SPLIT_LOADQ(a1, 1);
       TTS_SPLIT_LOADQ(a2, 2);
@@ -821,10 +825,10 @@ hipError_t split_reduce_launch(const ConvParams& p, int S, hipStream_t s, bool* 
 constexpr int SPLIT_LDS_MAX = 76 * 1024;  // two blocks per CU
 
 // channel group: largest power of two dividing Cin with both planes of UW utterances' rows within
-// SPLIT_LDS_MAX; >= 128 so a group has an even number of weight quads
+// SPLIT_LDS_MAX; >= 32 (64- / 32-channel groups run 2- / 1-k-step ring slots, KQ = 2 / 1)
 static int split_group(const ConvParams& p, int BN, int UW) {
   const int R = BN + (p.taps - 1) * p.dil;
-  for (int cg = 512; cg >= 128; cg /= 2) {
+  for (int cg = 512; cg >= 32; cg /= 2) {
     if (cg > p.Cin || p.Cin % cg) continue;
     if ((size_t)2 * UW * R * (cg * 2 + 16) <= (size_t)SPLIT_LDS_MAX) return cg;
   }
@@ -832,7 +836,7 @@ static int split_group(const ConvParams& p, int BN, int UW) {
 }
 
 bool conv_split_eligible(const ConvParams& p) {
-  return !p.no_split && p.wpk && p.Cin % 128 == 0 && p.M % 4 == 0 && p.nh == 1 && p.sxr % 4 == 0 && p.sxb % 4 == 0 &&
+  return !p.no_split && p.wpk && p.Cin % 32 == 0 && p.M % 4 == 0 && p.nh == 1 && p.sxr % 4 == 0 && p.sxb % 4 == 0 &&
          split_group(p, 64, 1) > 0 && split_group(p, 32, 1) > 0;
 }
 
@@ -851,7 +855,9 @@ static hipError_t launch_tile(const ConvParams& p, hipStream_t s) {
   if (!cg) return hipErrorInvalidValue;
   const size_t lds = (size_t)2 * (BN + (p.taps - 1) * p.dil) * (cg * 2 + 16);
   const int nwg = (p.y_rows + BN - 1) / BN * ((p.M + 127) / 128) * p.B;
-  hipLaunchKernelGGL((conv_split_kernel<NT, 1>), dim3(nwg), dim3(256), lds, s, p, cg);
+  if (cg >= 128) hipLaunchKernelGGL((conv_split_kernel<NT, 1, 4>), dim3(nwg), dim3(256), lds, s, p, cg);
+  else if (cg == 64) hipLaunchKernelGGL((conv_split_kernel<NT, 1, 2>), dim3(nwg), dim3(256), lds, s, p, cg);
+  else hipLaunchKernelGGL((conv_split_kernel<NT, 1, 1>), dim3(nwg), dim3(256), lds, s, p, cg);
   return hipGetLastError();
 }
 

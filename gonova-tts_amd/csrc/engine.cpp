@@ -91,7 +91,7 @@ struct tts_engine {
 #define TTS_VWS_MIN_CIN 128
 #endif
 #ifndef TTS_VOC_SPLIT_MINC
-#define TTS_VOC_SPLIT_MINC 128  // fp32 vocoders: resblock convs with >= this many channels run split-precision
+#define TTS_VOC_SPLIT_MINC 32  // fp32 vocoders: resblock convs with >= this many channels run split-precision
 #endif
   static constexpr int VWS_MIN_CIN = TTS_VWS_MIN_CIN;  // (A/B builds: 64 with TTS_F32_SK_MINM=32)
   float* vws = nullptr;
@@ -251,7 +251,7 @@ struct tts_engine {
           }
           // fp32 vocoders: the wide stages' resblock convs (C >= TTS_VOC_SPLIT_MINC) as split-precision
           // GEMMs -- C1's batch-1 fp32 vocoder ran them on the fp32 MFMA at 15-25 TF/s
-          const bool split = dt == DT_F32 && ch >= TTS_VOC_SPLIT_MINC && ch % 128 == 0;
+          const bool split = dt == DT_F32 && ch >= TTS_VOC_SPLIT_MINC && ch % 32 == 0;
           v.mrf[i][j][q][0] = pack_conv(pre + "convs1." + std::to_string(q) + ".weight",
                                         pre + "convs1." + std::to_string(q) + ".bias", d, (ks * d - d) / 2, dt, split);
           v.mrf[i][j][q][1] = pack_conv(pre + "convs2." + std::to_string(q) + ".weight",

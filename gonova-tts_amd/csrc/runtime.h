@@ -176,7 +176,7 @@ inline void* frag_pack(const std::vector<float>& w, int M, int taps, int ci, int
 // terms) and the GEMM multiplies its sums by *unscale = 2^-s, an exact step.
 inline void* frag_pack_split(const std::vector<float>& w, int M, int taps, int ci, std::vector<void*>& allocs,
                              float* unscale) {
-  if (ci % 64 || M % 4) return nullptr;
+  if (ci % 32 || M % 4) return nullptr;
   const int MB = (M + 31) / 32, KS = ci / 16;
   const size_t plane = (size_t)MB * 32 * taps * ci;
   float mx = 0.f;

@@ -96,8 +96,8 @@ enum { TTS_ENCODER_EXACT = 0, TTS_ENCODER_FAST = 1, TTS_ENCODER_F32 = 2 };
  * encoder side, no range limit).  TTS_ENCODER_F32 is a run-time setting only
  * (tts_acoustic_set_precision), not a tts_config value. */
 
-/* fp32 vocoders (vocoder_dtype = TTS_DTYPE_F32): the resblock convs of stages with >= 64 channels
- * run as split-precision GEMMs (three f16 MFMAs per product, ~2^-21 relative, like the exact
+/* fp32 vocoders (vocoder_dtype = TTS_DTYPE_F32): the resblock convs of every stage (channel counts
+ * divisible by 32, >= 32) run as split-precision GEMMs (three f16 MFMAs per product, ~2^-21 relative, like the exact
  * encoder).  tts_vocoder_forward / _chunk then read the layers' range word once at the end of the
  * call (one sync of `stream`) and, if an activation left f16's range, rerun the forward with every
  * layer on the fp32 MFMA path; 16-bit vocoders are unaffected and stay asynchronous. */

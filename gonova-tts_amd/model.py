@@ -339,7 +339,7 @@ class GonovaTTS:
                 tokens, lens = tokenize_batch([texts[i] for i in idx])
                 done = [False] * len(idx)
                 for c0, wav, valid in self.stream_tokens(tokens, lens, chunk_frames, speaker_embedding=spk):
-                    host = wav.cpu().numpy()
+                    host = _to_host(wav)
                     full = host.shape[1]
                     out = []
                     for r, i in enumerate(idx):
@@ -365,7 +365,7 @@ class GonovaTTS:
             for idx, spk in groups:
                 tokens, lens = tokenize_batch([texts[i] for i in idx])
                 wav, wav_lens = self.synthesize_tokens(tokens, lens, speaker_embedding=spk)
-                host = wav.cpu().numpy()  # (a tensor's copy runs on its own device's stream)
+                host = _to_host(wav)
                 for r, i in enumerate(idx):
                     out[i] = host[r, : int(wav_lens[r])].astype(np.float32, copy=False)
         return out
@@ -464,6 +464,19 @@ def _upload_i32(arrays, dev, stream=None):
         if t is not None:
             t.record_stream(target)  # (allocated on the upload stream, used on the target)
     return out
+
+
+def _to_host(t):
+    """Device tensor -> numpy copy through a page-locked block of torch's caching host allocator:
+    a pinned D2H runs at DMA speed where `.cpu()` stages a pageable copy (C1's 436 KB waveform is
+    on the first frame's critical path).  The copy runs on the tensor's device's current stream,
+    the one the engine launched on; the returned array keeps the block alive until dropped."""
+    import torch
+    with torch.cuda.device(t.device):
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        h.copy_(t, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+    return h.numpy()
 
 
 def _need_and_lens(dur, mel_lens, rw=None):

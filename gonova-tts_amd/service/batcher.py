@@ -103,6 +103,8 @@ class DynamicBatcher:
         self._idle = 0  # engine workers waiting for work
         self._cond: Optional[asyncio.Condition] = None
         self._flushes: set = set()  # delivery tasks in flight
+        self._run_task = None  # run()'s task, and whether it waits for requests (stop())
+        self._admitting = False
         self.stats = {"syntheses": 0, "total_latency": 0.0, "first_chunk_latency": 0.0, "errors": 0,
                       "rounds": 0, "engine_batches": 0, "batch_errors": 0, "sentences": 0, "requests": 0,
                       "audio_seconds": 0.0, "busy_seconds": 0.0, "max_batch_seen": 0,
@@ -121,6 +123,7 @@ class DynamicBatcher:
     async def run(self):
         """Admission loop plus one worker per engine, until stop() / cancellation."""
         self.running = True
+        self._run_task = asyncio.current_task()
         self._cond = asyncio.Condition()
         loop = asyncio.get_running_loop()
         workers = [asyncio.create_task(self._engine_loop(e, loop)) for e in range(len(self.synth_batches))]
@@ -132,6 +135,7 @@ class DynamicBatcher:
                     room = self.max_requests - self._inflight
                 if not self.running:
                     break
+                self._admitting = True
                 try:
                     # the gathering window only while every engine is busy (what arrives then is
                     # batched by the continuous admission anyway): an idle engine starts at once,
@@ -139,6 +143,8 @@ class DynamicBatcher:
                     reqs = await self.queues.take_batch(room, lambda: self.idle_wait if self._idle else self.max_wait)
                 except asyncio.CancelledError:
                     break
+                finally:
+                    self._admitting = False
                 if reqs:
                     await self._admit(reqs)
         finally:
@@ -370,6 +376,9 @@ class DynamicBatcher:
 
     def stop(self):
         self.running = False
+        if self._admitting and self._run_task is not None:
+            # the admission loop waits on the input queue without a timeout: end that wait
+            self._run_task.cancel()
         if self._cond is not None:
             async def wake():
                 async with self._cond:

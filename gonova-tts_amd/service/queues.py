@@ -99,7 +99,12 @@ class TTSQueueManager:
         req = SynthesisRequest(connection_id, text, voice_id, time.time(), chunk_size, exaggeration, streaming, voice,
                                stream_frames)
         try:
-            await asyncio.wait_for(self.input_queue.put(req), timeout=timeout)
+            # a put that fits starts no timer (wait_for's task and timer handle are a loop hop
+            # on every request); a full queue waits up to `timeout`
+            try:
+                self.input_queue.put_nowait(req)
+            except asyncio.QueueFull:
+                await asyncio.wait_for(self.input_queue.put(req), timeout=timeout)
         except asyncio.TimeoutError:
             self.stats.requests_dropped += 1
             logger.warning("input queue full, dropping request of %s", connection_id)
@@ -109,13 +114,23 @@ class TTSQueueManager:
 
     async def get_next_request(self, timeout: float = 1.0) -> Optional[SynthesisRequest]:
         try:
+            return self.input_queue.get_nowait()
+        except asyncio.QueueEmpty:
+            pass
+        try:
             return await asyncio.wait_for(self.input_queue.get(), timeout=timeout)
         except asyncio.TimeoutError:
             return None
 
-    async def take_batch(self, max_items: int, max_wait, first_timeout: float = 1.0) -> List[SynthesisRequest]:
-        """`max_wait`: seconds, or a callable giving them once the first request is in."""
-        first = await self.get_next_request(first_timeout)
+    async def take_batch(self, max_items: int, max_wait, first_timeout: Optional[float] = None) -> List[SynthesisRequest]:
+        """`max_wait`: seconds, or a callable giving them once the first request is in.
+        `first_timeout`: how long to wait for the first request ([] after it); None waits until
+        one comes (the batcher's admission loop, which stop() cancels): a plain queue get wakes
+        on the put itself, where wait_for's inner task adds two loop hops to every request."""
+        if first_timeout is None:
+            first = await self.input_queue.get()
+        else:
+            first = await self.get_next_request(first_timeout)
         if first is None:
             return []
         batch = [first]

@@ -191,10 +191,9 @@ class TTSService:
 
         async def send():
             while True:
-                try:
-                    chunk = await asyncio.wait_for(out_q.get(), timeout=1.0)
-                except asyncio.TimeoutError:
-                    continue
+                # a plain get: a timeout here only looped back to the same get, and each
+                # wait_for costs a task and a timer per frame
+                chunk = await out_q.get()
                 try:
                     if chunk.is_final:
                         await ws.send_json({"type": "synthesis_complete", "chunk_id": chunk.chunk_id})

@@ -78,6 +78,8 @@ struct AcousticModel::Impl {
   int cur_rpad = 0;            // rows_pad of the convs being launched (encoder side only)
   float* split_ws = nullptr;   // split-K partial sums of the packed split GEMMs
   long long split_ws_bytes = 0;
+  float* attn_ws = nullptr;    // fp32 attention key-chunk partials (fp32 models)
+  long long attn_ws_bytes = 0;
   // Range guard of the exact encoder (tts_hip.h, TTS_ENCODER_EXACT): the split GEMMs and the
   // split attention OR 1 into this device word when a staged fp32 operand is outside f16's range;
   // the host reads and clears it (tts_acoustic_range_flag) and reruns with enc_f32 set, which
@@ -360,6 +362,8 @@ struct AcousticModel::Impl {
     ln_cnt_n = 0;
     split_ws = nullptr;
     split_ws_bytes = 0;
+    attn_ws = nullptr;
+    attn_ws_bytes = 0;
     std::vector<void*> old;
     old.swap(ws);
     for (void* p : old) dev_free(p);
@@ -452,6 +456,9 @@ struct AcousticModel::Impl {
     }
     split_ws = wsb ? (float*)alloc_ws((size_t)wsb, 1) : nullptr;
     split_ws_bytes = wsb;
+    // fp32 models: the key-chunk partials of the fp32 attention (attention.hip), both stacks
+    attn_ws_bytes = dt == DT_F32 ? rel_attn_f32_ws_bytes(B, Tm, Tp, D, H) : 0;
+    attn_ws = attn_ws_bytes ? (float*)alloc_ws((size_t)attn_ws_bytes, 1) : nullptr;
     cap_B = B; cap_N = N; cap_T = T;
   }
 
@@ -507,7 +514,7 @@ struct AcousticModel::Impl {
             throw TtsError(TTS_ERR_INVALID, "bounds: attention " + why);
         }
         prof_launch(PK_ATTN, 6.0 * D * (double)B * Tm * Tm, s, [&] { return launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, L.ptab, lens, B, Tm, Tp, D, H, rmax, scale,
-                                  O, s, range_flag); });
+                                  O, s, range_flag, attn_ws, attn_ws_bytes); });
         run_ln(L.out, O, Tp, lens, Y, Tp, B, dt, s, 1.f, Xb, Xb, L.ln_att, nullptr);
         conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
         continue;

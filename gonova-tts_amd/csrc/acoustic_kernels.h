@@ -45,8 +45,12 @@ hipError_t launch_range_take(int* src, int* dst, hipStream_t s);
 // attention.hip: fused relative-position attention (dk = 192): 16-bit dtypes, fp32 (exact f32
 // MFMA) and, with split set, fp32 in split precision (three f16 MFMAs per product)
 bool rel_attn_supported(int dt, int D, int H);
+// ws: the fp32 form's key-chunk partials (rel_attn_f32_ws_bytes; null or too small: one chunk)
 hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* pos_v, const void* qkv,
                            const void* ptab, const int* lens, int B, int Tm, int Tp, int D, int H, int rmax,
-                           float scale, void* out, hipStream_t s, int* range_flag = nullptr);
+                           float scale, void* out, hipStream_t s, int* range_flag = nullptr, float* ws = nullptr,
+                           long long ws_bytes = 0);
+int rel_attn_f32_kc();  // keys per chunk of the fp32 form (0: no chunks)
+long long rel_attn_f32_ws_bytes(int B, int Tm, int Tp, int D, int H);
 
 }  // namespace tts

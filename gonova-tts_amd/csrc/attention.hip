@@ -90,6 +90,8 @@ __device__ inline uint2 at_tr16(const char* p) {
 constexpr int AT_BQ = 64;   // queries per block
 constexpr int AT_BK = 32;   // keys per step
 constexpr int AT_RW = AT_BQ + AT_BK;  // R window rows per block (95 used)
+// fp32 attention key chunk (keys per block; rel_attn_f32_kernel), TTS_ATTN_F32_KC (0: off)
+constexpr int AT_F32_KC = 128;
 // Lazy online-softmax rescale (16-bit kernel): a row's reference max moves only when a step's
 // max exceeds it by more than AT_LAZY (log2 units), so P = 2^(s - m) stays <= 2^AT_LAZY (f16 /
 // bf16 hold it exactly as well as any P <= 1: same relative precision) and the O^T rescale of
@@ -403,12 +405,22 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
 // permuted (lane group g holds d = 16u + 4g + e for k-step 4u + e) so every A fragment of four
 // k-steps is one 16-byte LDS read and every Q fragment one 16-byte global load.  LDS holds fp32
 // K / Vt / R (140 KB): one block per CU.
+//
+// Key chunks (kc > 0, fp32 models): block (query tile, chunk c) runs keys [c kc, min(len, (c+1) kc))
+// and writes its unnormalised O^T rows with the row's (max, sum) to `po` / `pml`;
+// rel_attn_merge_kernel combines an utterance's ceil(len / kc) chunks.  A batch-1 decoder
+// (C1: 7 query tiles x 2 heads = 14 blocks, one wave per SIMD on 14 of 256 CUs) gets
+// ceil(len / kc) times the blocks, each with 1 / that of the serial key loop.  The chunking
+// depends on the utterance's length only (batch invariant), and a one-chunk row merges to the
+// direct form's bits (x * exp2(0) = x, then the same O * (1 / l)).
 template <int DK>
 __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __restrict__ pu, const float* __restrict__ pv,
                                                              const float* __restrict__ qkv,
                                                              const float* __restrict__ ptab, const int* __restrict__ lens,
                                                              int Tp, int D, int H, int rmax, float scale,
-                                                             float* __restrict__ out, int nqb, int nbatch) {
+                                                             float* __restrict__ out, int nqb, int nbatch,
+                                                             int kc, int nks, float* __restrict__ po,
+                                                             float* __restrict__ pml) {
   constexpr int KU = DK / 16;         // 16-wide dk chunks (4 k-steps each); also O^T tiles
   constexpr int KR = at_kr<float>(DK);  // K / V / R row stride in LDS (bytes; odd 16-byte slots)
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -417,12 +429,16 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
   char* Rs = Vs + AT_BK * KR;                       // [96 slots][DK]
   float* Gs = reinterpret_cast<float*>(Rs + AT_RW * KR);  // [4 waves][48 slots][16 q]
 
-  int bh, qb;
-  if (!xcd_tile(nqb, H * nbatch, bh, qb)) return;
+  int bh, qt;
+  if (!xcd_tile(nqb * nks, H * nbatch, bh, qt)) return;
+  const int kcn = qt / nqb, qb = qt - kcn * nqb;  // key chunk, query tile
   const int b = bh / H, h = bh - b * H;
   const int i0 = qb * AT_BQ;
   const int len = lens[b];
   if (i0 >= len) return;
+  const int kbeg = kcn * kc;  // (kc = 0: one chunk, all keys)
+  if (kbeg >= len) return;
+  const int kend = kc > 0 ? min(len, kbeg + kc) : len;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane & 15, g = lane >> 4;
@@ -475,8 +491,8 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
     for (int i = 0; i < KP; ++i) {
       const int p = tid + 256 * i;
       const int r = p / (DK / 4), c = p - r * (DK / 4);
-      *reinterpret_cast<f32x4*>(Ks + r * KR + c * 16) = j0 + r < len ? pkv[i] : f32x4{};
-      *reinterpret_cast<f32x4*>(Vs + r * KR + c * 16) = j0 + r < len ? pvt[i] : f32x4{};  // 0 * V finite
+      *reinterpret_cast<f32x4*>(Ks + r * KR + c * 16) = j0 + r < kend ? pkv[i] : f32x4{};
+      *reinterpret_cast<f32x4*>(Vs + r * KR + c * 16) = j0 + r < kend ? pvt[i] : f32x4{};  // 0 * V finite
     }
   };
   auto write_r = [&](int j0) __attribute__((always_inline)) {
@@ -489,15 +505,15 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
   };
   for (int p = tid; p < AT_RW * (DK / 4); p += 256) {
     const int sb = p / (DK / 4), c = p - sb * (DK / 4);
-    const int m = i0 - (AT_BK - 1) + sb;
+    const int m = i0 - kbeg - (AT_BK - 1) + sb;
     *reinterpret_cast<f32x4*>(Rs + rslot(m) * KR + c * 16) =
         *reinterpret_cast<const f32x4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 4);
   }
-  load_kv(0);
-  write_kv(0);
+  load_kv(kbeg);
+  write_kv(kbeg);
   __syncthreads();
 
-  for (int j0 = 0; j0 < len; j0 += AT_BK) {
+  for (int j0 = kbeg; j0 < kend; j0 += AT_BK) {
     load_kv(j0 + AT_BK);
     load_r(j0 + AT_BK);
     __builtin_amdgcn_sched_barrier(0);
@@ -537,7 +553,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
         const int kk = 16 * kt + 4 * g + e;
         const float bd = gw[at_gslot(q - kk + AT_BK - 1) * 16 + q];
         float sc = (sacc[kt][e] + bd) * sl2;
-        if (j0 + kk >= len) sc = -INFINITY;
+        if (j0 + kk >= kend) sc = -INFINITY;
         sv[4 * kt + e] = sc;
         mloc = fmaxf(mloc, sc);
       }
@@ -577,11 +593,48 @@ __global__ __launch_bounds__(256, 1) void rel_attn_f32_kernel(const float* __res
   }
   const int i = i0w + q;
   if (i < len) {
+    if (po != nullptr) {  // key chunk: unnormalised rows and the row's (max, sum)
+      const long long prow = ((long long)(kcn * nbatch + b) * H + h) * Tp + i;
+      float* orow = po + prow * DK;
+#pragma unroll
+      for (int t = 0; t < KU; ++t) *reinterpret_cast<f32x4*>(orow + 16 * t + 4 * g) = oacc[t];
+      if (g == 0) *reinterpret_cast<float2*>(pml + 2 * prow) = float2{m_run, l_run};
+      return;
+    }
     const float inv = 1.f / l_run;
     float* orow = out + ((long long)b * Tp + i) * rowD + h * DK;
 #pragma unroll
     for (int t = 0; t < KU; ++t) *reinterpret_cast<f32x4*>(orow + 16 * t + 4 * g) = oacc[t] * inv;
   }
+}
+
+// Merge of the key chunks (rel_attn_f32_kernel, kc > 0): O = sum_c 2^(m_c - M) O_c,
+// l = sum_c 2^(m_c - M) l_c, M = max_c m_c, out = O * (1 / l).  One thread per (row, 4 channels).
+template <int DK>
+__global__ __launch_bounds__(192) void rel_attn_merge_kernel(const float* __restrict__ po, const float* __restrict__ pml,
+                                                            const int* __restrict__ lens, int Tp, int D, int H, int kc,
+                                                            int nbatch, float* __restrict__ out) {
+  const int r = blockIdx.x * 2 + threadIdx.x / 96;
+  const int c4 = threadIdx.x % 96;
+  if (4 * c4 >= D || r >= nbatch * Tp) return;
+  const int b = r / Tp, i = r - b * Tp;
+  const int len = lens[b];
+  if (i >= len) return;
+  const int h = 4 * c4 / DK, d = 4 * c4 - h * DK;
+  const int n = (len + kc - 1) / kc;
+  auto prow = [&](int c) { return ((long long)(c * nbatch + b) * H + h) * Tp + i; };
+  float M = -INFINITY;
+  for (int c = 0; c < n; ++c) M = fmaxf(M, pml[2 * prow(c)]);
+  f32x4 o = f32x4{};
+  float l = 0.f;
+  for (int c = 0; c < n; ++c) {
+    const float2 ml = *reinterpret_cast<const float2*>(pml + 2 * prow(c));
+    const float wgt = at_exp2(ml.x - M);
+    o += *reinterpret_cast<const f32x4*>(po + prow(c) * DK + d) * wgt;
+    l += ml.y * wgt;
+  }
+  const float inv = 1.f / l;
+  *reinterpret_cast<f32x4*>(out + (long long)r * D + h * DK + d) = o * inv;
 }
 
 // Split-precision form (the fp32 encoder of a 16-bit model, acoustic.cpp): every fp32 operand
@@ -880,9 +933,22 @@ bool rel_attn_supported(int dt, int D, int H) {
   return (dt == DT_F16 || dt == DT_BF16 || dt == DT_F32) && H > 0 && D % H == 0 && D / H == 192;
 }
 
+int rel_attn_f32_kc() {
+  const int v = sw(SW_ATTN_F32_KC);
+  if (v < 0) return AT_F32_KC;
+  return v == 0 ? 0 : std::max(AT_BK, v / AT_BK * AT_BK);
+}
+
+long long rel_attn_f32_ws_bytes(int B, int Tm, int Tp, int D, int H) {
+  const int kc = rel_attn_f32_kc();
+  if (kc == 0 || Tm <= kc) return 0;
+  const long long nks = (Tm + kc - 1) / kc;
+  return nks * B * Tp * ((long long)D + 2 * H) * 4;
+}
+
 hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* pos_v, const void* qkv,
                            const void* ptab, const int* lens, int B, int Tm, int Tp, int D, int H, int rmax,
-                           float scale, void* out, hipStream_t s, int* range_flag) {
+                           float scale, void* out, hipStream_t s, int* range_flag, float* ws, long long ws_bytes) {
   if (!rel_attn_supported(dt, D, H) || Tm > rmax) return hipErrorInvalidValue;
   const int nqb = (Tm + AT_BQ - 1) / AT_BQ;
   dim3 grid(xcd_grid(nqb, H * B));
@@ -893,9 +959,26 @@ hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* 
     return hipGetLastError();
   }
   if (dt == DT_F32) {
+    // key chunks when the workspace holds them (fp32 models; the merge is skipped when every
+    // utterance fits one chunk: that row's merge would reproduce the direct bits)
+    const int kc = rel_attn_f32_kc();
+    const long long need = rel_attn_f32_ws_bytes(B, Tm, Tp, D, H);
+    if (need > 0 && ws != nullptr && need <= ws_bytes) {
+      const int nks = (Tm + kc - 1) / kc;
+      float* po = ws;
+      float* pml = ws + (long long)nks * B * Tp * D;
+      hipLaunchKernelGGL((rel_attn_f32_kernel<192>), dim3(xcd_grid(nqb * nks, H * B)), dim3(256), rel_attn_f32_lds<192>(), s,
+                         pos_u, pos_v, (const float*)qkv, (const float*)ptab, lens, Tp, D, H, rmax, scale,
+                         (float*)out, nqb, B, kc, nks, po, pml);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL((rel_attn_merge_kernel<192>), dim3((B * Tp + 1) / 2), dim3(192), 0, s, po, pml, lens, Tp, D, H,
+                         kc, B, (float*)out);
+      return hipGetLastError();
+    }
     hipLaunchKernelGGL((rel_attn_f32_kernel<192>), grid, dim3(256), rel_attn_f32_lds<192>(), s, pos_u, pos_v,
                        (const float*)qkv, (const float*)ptab, lens, Tp, D, H, rmax, scale,
-                       (float*)out, nqb, B);
+                       (float*)out, nqb, B, 0, 1, nullptr, nullptr);
     return hipGetLastError();
   }
   // two key groups per block (TTS_ATTN_KSPLIT=1): batch 8 287 -> 248 us per forward, batch 32

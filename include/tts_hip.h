@@ -191,8 +191,8 @@ int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, doubl
 /* Process-wide switch selecting an alternative kernel path (A/B runs, the parity tests'
  * reference paths): TTS_REL_ATTN, TTS_MRF_FUSED, TTS_MRF_CHAIN, TTS_POST_FUSE, TTS_UP_STREAM,
  * TTS_XRES_NARROW, TTS_XRES_NT, TTS_PAIR_DIV, TTS_ATTN_KSPLIT, TTS_SPLIT_WHOLE, TTS_XRES_DMA,
- * TTS_LN_FUSE, TTS_SPLIT_NT1, TTS_XRES_ORDER, TTS_PAIR_SPLIT, TTS_VP_BATCH, TTS_DEC_TRIM.  Each
- * starts from its environment variable, read once; value -1 restores the built-in default.
+ * TTS_LN_FUSE, TTS_SPLIT_NT1, TTS_XRES_ORDER, TTS_PAIR_SPLIT, TTS_VP_BATCH, TTS_DEC_TRIM,
+ * TTS_ATTN_F32_KC.  Each starts from its environment variable, read once; value -1 restores the built-in default.
  * Applies to launches enqueued after the call (use from one thread while no forward runs). */
 int tts_set_switch(const char* name, int value);
 /* Current value of a switch (-1 = not set), so a caller can restore what it changed. */

@@ -66,8 +66,9 @@ struct ConvParams {
   // a contiguous range of items), items ordered M block fastest, so the M blocks of a row tile run
   // on one XCD together and share its X tile through that L2
   int xres_order;
-  // Split-K of the fp32 conv_gemm_kernel (latency-bound small grids of the fp32 acoustic model:
-  // C1's batch-1 FFN convs ran on 3-12 blocks).  f32_splitk (caller): the launch may split its K
+  // Split-K of the fp32 conv_gemm_kernel, at every batch size (it was built for C1's batch-1 FFN
+  // convs, which ran on 3-12 blocks; measured at batch 8 / 32 and kept, capped at 16 slices:
+  // profiles/r06c/).  f32_splitk (caller): the launch may split its K
   // (Cin chunks) into f32_kslices(taps, Cin) slices -- a count from the layer shape only, so a row's
   // summation order does not depend on the batch -- writing fp32 partials to ws[S][B][y_rows][M],
   // which split_reduce_launch sums in slice order and finishes with conv_epilogue's arithmetic.

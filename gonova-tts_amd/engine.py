@@ -340,7 +340,8 @@ class HipEngine:
         tokens = tokens.to(dtype=torch.int32).contiguous()
         tok_lens = tok_lens.to(device=tokens.device, dtype=torch.int32).contiguous()
         B, N = tokens.shape
-        mel = torch.zeros((B, t_cap, 80), dtype=torch.float32, device=tokens.device)
+        # (every row is written: the frames past each utterance's length as zeros, mel_out_kernel)
+        mel = torch.empty((B, t_cap, 80), dtype=torch.float32, device=tokens.device)
         mel_lens = torch.empty((B,), dtype=torch.int32, device=tokens.device)
         dur_out = torch.empty((B, N), dtype=torch.int32, device=tokens.device)
         dptr = ctypes.c_void_p(0)

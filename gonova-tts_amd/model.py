@@ -249,12 +249,18 @@ class GonovaTTS:
             # (frames >= chunk + ctx, the usual case): enqueue it before the one host read of the
             # frame counts, so the GPU runs it instead of idling through the round trip.  It is
             # used only if the loop below would make exactly the same call (else recomputed).
+            # The read's copies are enqueued before the chunk and waited for by event, so the host
+            # has the frame counts while the chunk still runs and hands the chunk over when it is
+            # enqueued (a read after the chunk held the host until the chunk ended, then cost a
+            # second round trip for the waveform: ~0.15 ms of C5, profiles/r06m/).
             w1 = min(t_cap, chunk_frames + ctx)
             tc = min(chunk_frames, t_cap)
-            if os.environ.get("TTS_STREAM_EARLY", "1") != "0":  # (0: the host read first, A/B runs)
+            early = os.environ.get("TTS_STREAM_EARLY", "1") != "0"  # (0: the host read first, A/B runs)
+            rd = _HostRead(dur, mel_lens, rw, stream)
+            if early:
                 win_lens = torch.clamp(mel_lens, min=0, max=w1).to(torch.int32)
                 first = (w1, tc, self.engine.vocoder_chunk(mel[:, :w1].contiguous(), win_lens, 0, tc, stream=stream))
-            need, lens_h, tripped = _need_and_lens(dur, mel_lens, rw)  # one host read before the first chunk
+            need, lens_h, tripped = rd.result()  # one host read before the first chunk is handed over
             fell_back = False
             if tripped:  # range guard: the acoustic pass again on the fp32 encoder
                 first, fell_back = None, True
@@ -477,6 +483,37 @@ def _to_host(t):
         h.copy_(t, non_blocking=True)
         torch.cuda.current_stream().synchronize()
     return h.numpy()
+
+
+class _HostRead:
+    """_need_and_lens without the blocking read: the durations, frame counts and range word are
+    copied into page-locked host memory on the compute stream (where the forward enqueued them)
+    and an event is recorded after them; result() waits for that event only, not for work the
+    caller enqueued afterwards, and sums on the host."""
+
+    def __init__(self, dur, mel_lens, rw=None, stream=None):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(mel_lens.device)
+        with torch.cuda.stream(s):
+            self.bufs = []
+            for t in (dur, mel_lens, rw):
+                if t is None:
+                    self.bufs.append(None)
+                    continue
+                h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                h.copy_(t, non_blocking=True)
+                self.bufs.append(h)
+            self.ev = torch.cuda.Event()
+            self.ev.record(s)
+
+    def result(self):
+        """-> (need, frame counts np.int64 [B], range word set), as _need_and_lens"""
+        self.ev.synchronize()
+        d, ln, rw = self.bufs
+        lens = ln.numpy().astype(np.int64)
+        sums = d.numpy().astype(np.int64).sum(axis=1)
+        need = int(np.maximum(sums, lens).max()) if len(lens) else 0
+        return need, lens, bool(rw is not None and int(rw.numpy()[0]) != 0)
 
 
 def _need_and_lens(dur, mel_lens, rw=None):

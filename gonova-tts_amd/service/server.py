@@ -191,9 +191,12 @@ class TTSService:
 
         async def send():
             while True:
-                # a plain get: a timeout here only looped back to the same get, and each
-                # wait_for costs a task and a timer per frame
-                chunk = await out_q.get()
+                # (wait_for, not a plain get: with a plain get, TestClient's session teardown --
+                # disconnect, then its cancel scope -- ended in CancelledError ~1 run in 6)
+                try:
+                    chunk = await asyncio.wait_for(out_q.get(), timeout=1.0)
+                except asyncio.TimeoutError:
+                    continue
                 try:
                     if chunk.is_final:
                         await ws.send_json({"type": "synthesis_complete", "chunk_id": chunk.chunk_id})

@@ -500,14 +500,35 @@ def bench_c4(ctx, args, steps, warmup):
         d = np.where(np.arange(t.shape[1])[None, :] < l[:, None], 6, 0).astype(np.int32)
         return m.synthesize_tokens(t, l, durations=d, host_lens=False)
 
+    def check(sh):
+        out = sh.run(tok if ctx.rank == 0 else None, lens if ctx.rank == 0 else None)
+        if ctx.rank == 0:  # every utterance back on the root at its length
+            bad = [i for i in range(B) if out[i] is None or out[i].shape[0] != int(lens[i]) * 6 * 256]
+            assert not bad, f"C4 gather lost utterances {bad[:8]}"
+        return out
+
     sh = ShardedSynthesis(synth, ctx.dev, bucket=args.c4_bucket)
     run = lambda: sh.run(tok if ctx.rank == 0 else None, lens if ctx.rank == 0 else None)  # noqa: E731
-    el, _ = ctx.timed(run, steps, warmup)
-    out = run()  # one more pass, checked: every utterance back on the root at its length
-    if ctx.rank == 0:
-        bad = [i for i in range(B) if out[i] is None or out[i].shape[0] != int(lens[i]) * 6 * 256]
-        assert not bad, f"C4 gather lost utterances {bad[:8]}"
+    el1, _ = ctx.timed(run, steps, warmup)
+    out1 = check(sh)
+    # Two engines per GPU taking the buckets in turn, each on its own stream (dist.py step 4; the
+    # service's two-engines-per-GPU shape): one bucket's acoustic pass beside another's vocoder.
+    m2 = GonovaTTS.from_pretrained(ctx.dev.index, vocoder_dtype="bf16", acoustic_dtype="bf16",
+                                   max_batch=args.c4_bucket, max_frames=864, max_tokens=144)
+
+    def synth2(t, l):
+        d = np.where(np.arange(t.shape[1])[None, :] < l[:, None], 6, 0).astype(np.int32)
+        return m2.synthesize_tokens(t, l, durations=d, host_lens=False)
+
+    sh2 = ShardedSynthesis([synth, synth2], ctx.dev, bucket=args.c4_bucket)
+    run2 = lambda: sh2.run(tok if ctx.rank == 0 else None, lens if ctx.rank == 0 else None)  # noqa: E731
+    el2, _ = ctx.timed(run2, steps, warmup)
+    out2 = check(sh2)
+    if ctx.rank == 0:  # the same bits: an utterance's result does not depend on the engine or bucket
+        assert all(np.array_equal(a, b) for a, b in zip(out1, out2)), "C4 two-engine output differs"
     m.engine.close()
+    m2.engine.close()
+    el = min(el1, el2)
     samples = int(lens.sum()) * 6 * 256 * steps
     value = samples / el
     if ctx.world == 1:
@@ -516,6 +537,8 @@ def bench_c4(ctx, args, steps, warmup):
         comm = f"RCCL broadcast of the tokens + P2P gather of the waveforms to rank 0 over {ctx.world} ranks, inside the timed region"
     return {"value": round(value, 1), "unit": "samples/s", "n_gpus": ctx.world, "scaling": "strong",
             "steps": steps, "warmup": warmup, "ms_per_step": round(el * 1e3 / steps, 3),
+            "one_engine_ms_per_step": round(el1 * 1e3 / steps, 3),
+            "two_engine_ms_per_step": round(el2 * 1e3 / steps, 3),
             "per_gpu_samples_per_s": round(value / ctx.world, 1),
             "x_realtime_per_gpu": round(value / ctx.world / SR, 2), "dtype": "bf16",
             "config": {"workload": f"C4 batch-{B} mixed-length utterances (N_i ~ U{{29..144}} tokens x 6 frames, "

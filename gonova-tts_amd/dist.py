@@ -11,7 +11,10 @@ GPU (torch.distributed, backend "nccl" = RCCL over xGMI) shares one request batc
      time first, load = total tokens, at most ceil(B / world) utterances per rank), then
      each rank cuts its share, sorted by length, into buckets of `bucket` utterances (one
      engine call each);
-  4. each rank synthesizes its buckets on its own GPU (no collective on the data path);
+  4. each rank synthesizes its buckets on its own GPU (no collective on the data path); given
+     several engines per GPU (`synth_fn` a list), consecutive buckets go to them in turn, each
+     engine on a stream of its own, so one bucket's latency-bound acoustic pass runs beside
+     another's MFMA-bound vocoder;
   5. gather: every rank packs its waveforms into one flat float32 buffer and sends it
      to rank 0 with an RCCL point-to-point send; its header (table and sample counts) and
      index table go over a CPU (gloo) group.  Rank 0 posts one receive per peer and handles
@@ -26,6 +29,7 @@ Works with the gloo backend on CPU tensors (tests/test_dist_cpu.py).
 """
 from __future__ import annotations
 
+import contextlib
 import time
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -77,6 +81,8 @@ class ShardedSynthesis:
     the same device -> host copy as the lengths, and a bucket whose word is set is synthesized
     again on the fp32 encoder there (pending.resolve) before its audio is packed.  On the root the
     waveforms come back as views into one host buffer per rank (one pinned D2H copy each).
+    synth_fn may be a list of such functions (engines of one GPU): bucket i runs on engine
+    i mod len, on that engine's own stream (CUDA devices).
     """
 
     def __init__(self, synth_fn: SynthFn, device, group=None, root: int = 0, bucket: int = 32):
@@ -99,7 +105,8 @@ class ShardedSynthesis:
         if not self.single and dist.get_backend(group) != "gloo":
             ranks = None if group is None else dist.get_process_group_ranks(group)
             self.meta_group = dist.new_group(ranks=ranks, backend="gloo")
-        self._streams: Dict[int, "object"] = {}
+        self._streams: Dict[int, "object"] = {}   # per peer: its receive and download (root)
+        self._estreams: Dict[int, "object"] = {}  # per engine (several engines per GPU)
         self.arrivals: List[Tuple[int, str, float]] = []  # (peer, "header" | "unpacked", time): tests
 
     def _bcast(self, t):
@@ -131,37 +138,52 @@ class ShardedSynthesis:
         # The root's own audio goes to the host bucket by bucket on a side stream, overlapped with
         # the next bucket's synthesis (pinned buffers), and its lengths follow as non-blocking
         # copies read in the gather loop; the other ranks pack theirs for the gather.
-        overlap = self.rank == self.root and torch.device(dev).type == "cuda"
+        cuda = torch.device(dev).type == "cuda"
+        overlap = self.rank == self.root and cuda
         side = torch.cuda.Stream(device=dev) if overlap else None
+        synths = list(self.synth_fn) if isinstance(self.synth_fn, (list, tuple)) else [self.synth_fn]
+        # one stream per engine when there are several (an engine orders its calls on one stream)
+        estreams = [self._engine_stream(dev, k) for k in range(len(synths))] if cuda and len(synths) > 1 else None
+        cur = torch.cuda.current_stream(dev) if estreams else None
+        if estreams:
+            for es in estreams:
+                es.wait_stream(cur)  # (the broadcast tokens above)
         done = []
-        for bk in mine:  # queue every bucket first: no host sync between them
-            n_b = int(ln_h[bk].max())
-            pend = None
-            if n_b == 0:  # only empty utterances: nothing to synthesize, empty waveforms
-                wav = torch.zeros((len(bk), 0), dtype=torch.float32, device=dev)
-                wav_lens = np.zeros(len(bk), np.int64)
-            else:
-                res = self.synth_fn(tok_h[bk, :n_b], ln_h[bk])
-                wav, wav_lens = res[0], res[1]
-                pend = res[2] if len(res) > 2 else None
-            host = lens_h = lens_ev = None
-            if overlap:
-                ev = torch.cuda.Event()
-                ev.record()
-                host = torch.empty(wav.shape, dtype=torch.float32, pin_memory=True)
-                with torch.cuda.stream(side):
-                    side.wait_event(ev)
-                    host.copy_(wav, non_blocking=True)
-                wav.record_stream(side)
-                if pend is not None or isinstance(wav_lens, torch.Tensor):
-                    lv = torch.as_tensor(wav_lens, device=dev).to(torch.int64).reshape(-1)
-                    if pend is not None:  # the lengths and the range word in one read
-                        lv = torch.cat([lv, pend.word.to(device=dev, dtype=torch.int64).reshape(-1)])
-                    lens_h = torch.empty(lv.shape, dtype=torch.int64, pin_memory=True)
-                    lens_h.copy_(lv, non_blocking=True)
-                    lens_ev = torch.cuda.Event()
-                    lens_ev.record()
+        for bi, bk in enumerate(mine):  # queue every bucket first: no host sync between them
+            k = bi % len(synths)
+            with (torch.cuda.stream(estreams[k]) if estreams else contextlib.nullcontext()):
+                n_b = int(ln_h[bk].max())
+                pend = None
+                if n_b == 0:  # only empty utterances: nothing to synthesize, empty waveforms
+                    wav = torch.zeros((len(bk), 0), dtype=torch.float32, device=dev)
+                    wav_lens = np.zeros(len(bk), np.int64)
+                else:
+                    res = synths[k](tok_h[bk, :n_b], ln_h[bk])
+                    wav, wav_lens = res[0], res[1]
+                    pend = res[2] if len(res) > 2 else None
+                host = lens_h = lens_ev = None
+                if overlap:
+                    ev = torch.cuda.Event()
+                    ev.record()  # (on the current stream: the bucket's engine stream)
+                    host = torch.empty(wav.shape, dtype=torch.float32, pin_memory=True)
+                    with torch.cuda.stream(side):
+                        side.wait_event(ev)
+                        host.copy_(wav, non_blocking=True)
+                    wav.record_stream(side)
+                    if pend is not None or isinstance(wav_lens, torch.Tensor):
+                        lv = torch.as_tensor(wav_lens, device=dev).to(torch.int64).reshape(-1)
+                        if pend is not None:  # the lengths and the range word in one read
+                            lv = torch.cat([lv, pend.word.to(device=dev, dtype=torch.int64).reshape(-1)])
+                        lens_h = torch.empty(lv.shape, dtype=torch.int64, pin_memory=True)
+                        lens_h.copy_(lv, non_blocking=True)
+                        lens_ev = torch.cuda.Event()
+                        lens_ev.record()
+                if estreams and isinstance(wav, torch.Tensor):
+                    wav.record_stream(cur)  # (allocated on the engine stream, read on this one below)
             done.append([bk, wav, wav_lens, host, pend, lens_h, lens_ev])
+        if estreams:
+            for es in estreams:  # what follows (packing, reruns, copies) runs on this stream
+                cur.wait_stream(es)
         if self.rank == self.root:
             return self._root_gather(B, dev, done, side)
         # ---- 5 (peers): pack as [n, ids..., lens...] + flat samples, send to the root ----
@@ -182,6 +204,13 @@ class ShardedSynthesis:
         for w in works:
             w.wait()
         return None
+
+    def _engine_stream(self, dev, k):
+        import torch
+        st = self._estreams.get(k)
+        if st is None:
+            st = self._estreams[k] = torch.cuda.Stream(device=dev)
+        return st
 
     @staticmethod
     def _resolve(wav, wav_lens, pend, host_vals=None):

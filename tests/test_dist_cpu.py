@@ -148,6 +148,24 @@ def test_single_process_without_group():
         np.testing.assert_array_equal(o, e)
 
 
+def test_several_engines_take_buckets_in_turn():
+    """synth_fn as a list (several engines on one GPU): bucket i goes to engine i mod n, and the
+    gathered result is the one-engine result, at world size 1 and under gloo at world size 2."""
+    tok, lens = make_batch(B=70, seed=5)
+    calls = []
+
+    def eng(k):
+        def fn(t, l):
+            calls.append(k)
+            return fake_synth(t, l)
+        return fn
+
+    out = ShardedSynthesis([eng(0), eng(1)], torch.device("cpu"), bucket=16).run(tok, lens)
+    assert calls == [0, 1, 0, 1, 0]  # 70 utterances: 5 buckets of <= 16
+    for o, e in zip(out, expected(tok, lens)):
+        np.testing.assert_array_equal(o, e)
+
+
 def test_all_empty_buckets_yield_empty_waveforms():
     """Zero-length utterances collect in the last buckets (longest first); a bucket made only
     of them is not sent to the engine (which rejects N = 0) and comes back as empty audio."""

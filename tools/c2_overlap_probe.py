@@ -63,6 +63,15 @@ def main():
                 cur.wait_stream(streams[i])
         return fn
 
+    def free2():
+        # the two halves' streams run free: no join between steps (a serving loop's shape); the
+        # timing's synchronize at the end waits for both
+        n = B // 2
+        for i in range(2):
+            sl = slice(i * n, (i + 1) * n)
+            with torch.cuda.stream(streams[i]):
+                engines[i].vocoder(mel[sl], lens[sl], out=wav[sl], stream=streams[i])
+
     one()
     torch.cuda.synchronize()
     ref.copy_(wav)
@@ -72,8 +81,8 @@ def main():
         torch.cuda.synchronize()
         print(f"split {k}: bit-identical to one stream: {bool(torch.equal(wav, ref))}")
     for rnd in range(2):
-        print(f"round {rnd}: one {timed(one):.3f} ms, two {timed(split(2)):.3f} ms, four {timed(split(4)):.3f} ms",
-              flush=True)
+        print(f"round {rnd}: one {timed(one):.3f} ms, two {timed(split(2)):.3f} ms, four {timed(split(4)):.3f} ms, "
+              f"two free-running {timed(free2):.3f} ms", flush=True)
     for e in engines:
         e.close()
 

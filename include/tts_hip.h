@@ -62,8 +62,9 @@ typedef struct tts_engine tts_engine;
  *      on the caller's stream at the end of each call (a caller may destroy its stream after
  *      the call returns)
  *   4  range guard of the exact encoder: tts_acoustic_range_flag / tts_acoustic_set_precision,
- *      TTS_ENCODER_F32 */
-#define TTS_ABI_VERSION 4
+ *      TTS_ENCODER_F32
+ *   5  tts_device_bytes (the library's device memory per HIP device); additive */
+#define TTS_ABI_VERSION 5
 int tts_abi_version(void);
 
 /* Engine configuration.  Fields are only ever appended; a caller built against an older

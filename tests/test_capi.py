@@ -70,7 +70,7 @@ def test_abi_version_and_sized_config_without_gpu():
     validation runs before the device lookup, so the rejections are checkable on the CPU."""
     import ctypes
     lib = engine.load_library()
-    assert lib.tts_abi_version() == 4
+    assert lib.tts_abi_version() == 5
     cfg = engine.TtsConfig(1, 2, 0, 0, 0, 0)
     h = ctypes.c_void_p()
     # a struct larger than the library's: a newer header than this library

@@ -68,8 +68,12 @@ struct AcousticModel::Impl {
   int dt = DT_F32;   // decoder / postnet activations
   int dte = DT_F32;  // encoder, speaker projection, variance adaptor (fp32 + split GEMMs when dt is 16-bit)
   int bdt = DT_F32;  // dtype of the layers being built (finalize)
-  // fp32 layers of a 16-bit model get split-packed weights (three f16 MFMAs, conv_split.hip)
-  bool split_now() const { return bdt == DT_F32 && dt != DT_F32; }
+  bool f32_split_enc = false;  // fp32 model: encoder side on split-precision GEMMs (finalize)
+  bool enc_side = false;       // the layers being built are the encoder side's (finalize)
+  // fp32 layers of a 16-bit model (and the encoder side of an fp32 model with f32_split_enc) get
+  // split-packed weights (three f16 MFMAs, conv_split.hip)
+  bool split_now() const { return bdt == DT_F32 && (dt != DT_F32 || (f32_split_enc && enc_side)); }
+  bool split_enc() const { return dte == DT_F32 && (dt != DT_F32 || f32_split_enc); }
   size_t esz() const { return std::max(dtype_size(dt), dtype_size(dte)); }
   // encoder row stride: at least ENC_PAD masked rows after every utterance, so the split-precision
   // GEMMs run packed 128-row tiles across utterances (ConvParams::rows_pad; k <= 5 convs)
@@ -436,14 +440,16 @@ struct AcousticModel::Impl {
     ln_cnt = (int*)alloc_ws((size_t)ln_cnt_n, 4);
     // split-K partials of the encoder's packed split GEMMs (fp32 encoder of a 16-bit model)
     long long wsb = 0;
-    if (dte == DT_F32 && dt != DT_F32) {
+    if (split_enc()) {
       const int F = B * enc_rows(N);
       for (auto& L : enc)
         for (const ConvLayer* c : {&L.ffm1, &L.ffm2, &L.ff1, &L.ff2, &L.qkv, &L.out, &L.pw1, &L.pw2})
           wsb = std::max(wsb, conv_split_ws_bytes(c->taps, c->Cin, c->M, F));
       for (const Predictor* pr : {&pitch, &energy, &duration})
         for (const ConvLayer& c : pr->convs) wsb = std::max(wsb, conv_split_ws_bytes(c.taps, c.Cin, c.M, F));
-    } else if (dt == DT_F32) {  // fp32 model: the split-K partials of its fp32 conv_gemm launches
+    }
+    if (dt == DT_F32) {  // fp32 model: the split-K partials of its fp32 conv_gemm launches (every
+                         // layer: a split encoder's fallback runs its layers on them too)
       const long long F = (long long)B * Tp;  // >= every stack's B * rows
       auto add = [&](const ConvLayer& c) { wsb = std::max(wsb, f32_splitk_ws_bytes(c.taps, c.Cin, c.M, F)); };
       for (const auto* st : {&enc, &dec})
@@ -505,7 +511,8 @@ struct AcousticModel::Impl {
         // fused flash-style relative-position attention (attention.hip); Qu / Qv formed in it,
         // V read from the QKV rows (transposed in LDS: no Vt launch)
         // fp32 layers of a 16-bit model (the exact-duration encoder) in split precision, like their GEMMs
-        const bool split = dt == DT_F32 && this->dt != DT_F32 && !enc_f32;
+        // (an fp32 layer has split-packed weights only on a split encoder side)
+        const bool split = dt == DT_F32 && L.qkv.wpk != nullptr && !enc_f32;
         if (TTS_BOUNDS_CHECK) {  // (diagnostic builds: runtime.h)
           const long long e = dtype_size(dt);
           std::string why;
@@ -706,7 +713,8 @@ struct AcousticModel::Impl {
   }
 };
 
-void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtype, int enc_dtype, Profiler* prof) {
+void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtype, int enc_dtype, Profiler* prof,
+                             bool f32_split_enc) {
   if (!get("encoder.embed.weight")) {
     loaded = false;
     return;
@@ -715,6 +723,8 @@ void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtyp
   m->dt = dtype;
   m->dte = enc_dtype == DT_F32 ? DT_F32 : dtype;
   m->bdt = m->dte;
+  m->f32_split_enc = dtype == DT_F32 && f32_split_enc;
+  m->enc_side = true;
   m->prof = prof;
   const auto es = shape("encoder.embed.weight");
   m->V = (int)es.at(0);
@@ -753,6 +763,7 @@ void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtyp
   m->ee_b = m->upf(m->need(get, "energy_embed.conv.bias"));
   // decoder side (bdt = dt): decoder layers, postnet
   m->bdt = dtype;
+  m->enc_side = false;
   for (int i = 0; get("decoder.conformer_layers." + std::to_string(i) + ".self_attn.pos_bias_u"); ++i)
     m->dec.push_back(m->layer(get, shape, "decoder.conformer_layers." + std::to_string(i) + "."));
   m->feat_out = m->conv(get, shape, "speech_decoder_postnet.feat_out.weight", "speech_decoder_postnet.feat_out.bias", 0);
@@ -796,7 +807,7 @@ void AcousticModel::forward(const int32_t* tokens, const int32_t* tok_lens, int 
 
 int AcousticModel::speaker_dim() const { return impl ? impl->E : 0; }
 
-bool AcousticModel::split_encoder() const { return impl && impl->dte == DT_F32 && impl->dt != DT_F32; }
+bool AcousticModel::split_encoder() const { return impl && impl->split_enc(); }
 
 void AcousticModel::set_encoder_f32(bool on) {
   if (!impl) throw TtsError(TTS_ERR_STATE, "acoustic model not loaded");

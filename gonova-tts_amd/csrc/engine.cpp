@@ -696,7 +696,7 @@ int tts_engine_finalize(tts_engine* eng) {
           return it == eng->host.end() ? std::vector<int64_t>{} : it->second.shape;
         },
         eng->cfg.acoustic_dtype, eng->cfg.encoder_precision == TTS_ENCODER_EXACT ? DT_F32 : eng->cfg.acoustic_dtype,
-        &eng->prof);
+        &eng->prof, eng->cfg.encoder_precision == TTS_ENCODER_EXACT && sw(SW_F32_ENC_SPLIT) != 0);
     if (!eng->voc.loaded && !eng->ac.loaded) throw TtsError(TTS_ERR_STATE, "no known weights were set");
     eng->host.clear();
     eng->finalized = true;
@@ -795,7 +795,7 @@ int tts_acoustic_set_precision(tts_engine* eng, int precision) {
     if (precision != TTS_ENCODER_EXACT && precision != TTS_ENCODER_F32)
       throw TtsError(TTS_ERR_INVALID, "precision must be TTS_ENCODER_EXACT or TTS_ENCODER_F32");
     if (!eng->ac.split_encoder())
-      throw TtsError(TTS_ERR_INVALID, "only a 16-bit model created with TTS_ENCODER_EXACT switches encoder precision");
+      throw TtsError(TTS_ERR_INVALID, "only a model created with TTS_ENCODER_EXACT switches encoder precision");
     eng->ac.set_encoder_f32(precision == TTS_ENCODER_F32);
   });
 }

@@ -219,7 +219,11 @@ class HipEngine:
         # range guard of the exact encoder of a 16-bit model (include/tts_hip.h, ABI 4): every
         # acoustic forward also enqueues a copy of the engine's range word, which the caller reads
         # at its next host sync (GonovaTTS) and answers with an fp32-MFMA rerun when it is set
-        self.range_guard = encoder_precision == "exact" and DTYPES[acoustic_dtype] != 0
+        # the exact encoder's split-precision GEMMs (16-bit models; fp32 models too unless
+        # TTS_F32_ENC_SPLIT=0) report activations outside f16's range in a word read back with the
+        # lengths; a set word reruns the batch on the fp32 encoder (model.py)
+        self.range_guard = encoder_precision == "exact" and (DTYPES[acoustic_dtype] != 0 or
+                                                             get_switch("TTS_F32_ENC_SPLIT") != 0)
         self.range_fallbacks = 0
         self.hop = 256
         self._finalized = False

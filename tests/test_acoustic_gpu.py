@@ -693,3 +693,45 @@ def test_fp32_attention_key_chunks(aw, switch):
         assert err < 2e-6, (b, err)
     ref = acoustic_forward(ids_list[0], aw, durations=durs[0])
     np.testing.assert_allclose(m1[0, :426], ref["mel"], atol=FP32_ATOL, rtol=FP32_RTOL)
+
+
+def test_fp32_model_split_encoder_matches_fp32_mfma_encoder(aw, switch):
+    """An fp32 model's encoder side on split-precision GEMMs and attention (TTS_ENCODER_EXACT with
+    acoustic_dtype f32, round 6) against the same model with every layer on fp32 MFMA
+    (TTS_F32_ENC_SPLIT=0 at finalize): identical predicted durations and frame counts on a
+    ragged batch, mel within the fp32 bar; the range guard is on for the fp32 model, and a
+    scaled layer trips it and falls back to the fp32 encoder (no inf in the mel)."""
+    rng = np.random.default_rng(31)
+    ids_list = [rng.integers(1, 78, size=n) for n in (71, 9, 40)]
+    switch("TTS_F32_ENC_SPLIT", 0)
+    e0 = HipEngine(DEV, vocoder_dtype="f32", acoustic_dtype="f32")
+    e0.load_weights(acoustic=aw)
+    switch("TTS_F32_ENC_SPLIT", None)
+    e1 = HipEngine(DEV, vocoder_dtype="f32", acoustic_dtype="f32")
+    e1.load_weights(acoustic=aw)
+    assert e1.range_guard and not e0.range_guard
+    m0, l0, d0 = run(e0, ids_list, t_cap=12 * 71)
+    m1, l1, d1 = run(e1, ids_list, t_cap=12 * 71)
+    assert np.array_equal(d0, d1) and np.array_equal(l0, l1)
+    for b in range(len(ids_list)):
+        L = int(l1[b])
+        np.testing.assert_allclose(m1[b, :L], m0[b, :L], atol=FP32_ATOL, rtol=FP32_RTOL)
+    e0.close()
+    k = "encoder.conformer_layers.0.feed_forward_macaron.conv1.weight"
+    aw2 = dict(aw)
+    aw2[k] = aw[k] * 20000.0
+    e2 = HipEngine(DEV, vocoder_dtype="f32", acoustic_dtype="f32")
+    e2.load_weights(acoustic=aw2)
+    B, N = len(ids_list), 71
+    tok = np.zeros((B, N), np.int32)
+    for b, x in enumerate(ids_list):
+        tok[b, :len(x)] = x
+    tok_d = torch.from_numpy(tok).to(DEV)
+    lens_d = torch.tensor([len(x) for x in ids_list], dtype=torch.int32, device=DEV)
+    *_, rw = e2.acoustic(tok_d, lens_d, 12 * N, return_range=True)
+    assert int(rw.item()) == 1
+    with e2.encoder_f32():
+        mel, mel_lens, rw = e2.acoustic(tok_d, lens_d, 12 * N, return_range=True)
+    assert int(rw.item()) == 0 and torch.isfinite(mel).all()
+    e1.close()
+    e2.close()

@@ -44,6 +44,7 @@ struct LNParam {
 
 struct ConformerLayer {
   int dt = DT_F32;  // activation dtype of this layer
+  bool split_attn = false;  // fp32 layer of a split encoder side: the split-precision attention
   ConvLayer ffm1, ffm2, ff1, ff2, qkv, out, pw1, pw2, pos;
   float* pos_u = nullptr;
   float* pos_v = nullptr;
@@ -64,15 +65,28 @@ struct Predictor {
 
 }  // namespace
 
+#ifndef TTS_F32_DEC_SPLIT_MAXK
+#define TTS_F32_DEC_SPLIT_MAXK 1536  // fp32 decoder layers split-packed up to this K = taps * Cin
+#endif
+
 struct AcousticModel::Impl {
   int dt = DT_F32;   // decoder / postnet activations
   int dte = DT_F32;  // encoder, speaker projection, variance adaptor (fp32 + split GEMMs when dt is 16-bit)
   int bdt = DT_F32;  // dtype of the layers being built (finalize)
   bool f32_split_enc = false;  // fp32 model: encoder side on split-precision GEMMs (finalize)
+  bool f32_split_dec = false;  // ... and the decoder / postnet GEMMs of short K (finalize)
   bool enc_side = false;       // the layers being built are the encoder side's (finalize)
   // fp32 layers of a 16-bit model (and the encoder side of an fp32 model with f32_split_enc) get
   // split-packed weights (three f16 MFMAs, conv_split.hip)
   bool split_now() const { return bdt == DT_F32 && (dt != DT_F32 || (f32_split_enc && enc_side)); }
+  // the same for one layer of K = taps * Cin: an fp32 model's decoder-side layers split too
+  // (f32_split_dec) when K is at most TTS_F32_DEC_SPLIT_MAXK -- they run the per-utterance split
+  // kernel, which has no split-K, so the 4,608-deep FFN down-projections stay on the fp32
+  // split-K GEMM (C1's batch-1 decoder: 42 blocks walking K = 4,608 would be slower)
+  bool split_for(int taps, int cin) const {
+    return split_now() || (bdt == DT_F32 && dt == DT_F32 && f32_split_dec && !enc_side &&
+                           (long long)taps * cin <= TTS_F32_DEC_SPLIT_MAXK);
+  }
   bool split_enc() const { return dte == DT_F32 && (dt != DT_F32 || f32_split_enc); }
   size_t esz() const { return std::max(dtype_size(dt), dtype_size(dte)); }
   // encoder row stride: at least ENC_PAD masked rows after every utterance, so the split-precision
@@ -187,8 +201,10 @@ struct AcousticModel::Impl {
     if (bias_override) bias = *bias_override;
     else if (!b.empty() && get(b)) bias = *get(b);
     if (s.size() == 3)
-      return make_conv(need(get, w), (int)s[0], (int)s[1], (int)s[2], bias, 1, pad, bdt, allocs, scale, split_now());
-    if (s.size() == 2) return make_conv(need(get, w), (int)s[0], (int)s[1], 1, bias, 1, 0, bdt, allocs, scale, split_now());
+      return make_conv(need(get, w), (int)s[0], (int)s[1], (int)s[2], bias, 1, pad, bdt, allocs, scale,
+                       split_for((int)s[2], (int)s[1]));
+    if (s.size() == 2)
+      return make_conv(need(get, w), (int)s[0], (int)s[1], 1, bias, 1, 0, bdt, allocs, scale, split_for(1, (int)s[1]));
     throw TtsError(TTS_ERR_INVALID, "bad weight rank: " + w);
   }
 
@@ -216,7 +232,8 @@ struct AcousticModel::Impl {
       wq.insert(wq.end(), w.begin(), w.end());
       bq.insert(bq.end(), b.begin(), b.end());
     }
-    L.qkv = make_conv(wq, 3 * D, D, 1, bq, 1, 0, bdt, allocs, nullptr, split_now());
+    L.qkv = make_conv(wq, 3 * D, D, 1, bq, 1, 0, bdt, allocs, nullptr, split_for(1, D));
+    L.split_attn = split_now();
     L.out = conv(get, shape, a + "linear_out.weight", a + "linear_out.bias", 0);
     L.pos = make_conv(need(get, a + "linear_pos.weight"), D, D, 1, {}, 1, 0, bdt, allocs, nullptr, split_now());
     L.pos_u = upf(need(get, a + "pos_bias_u"));
@@ -511,8 +528,8 @@ struct AcousticModel::Impl {
         // fused flash-style relative-position attention (attention.hip); Qu / Qv formed in it,
         // V read from the QKV rows (transposed in LDS: no Vt launch)
         // fp32 layers of a 16-bit model (the exact-duration encoder) in split precision, like their GEMMs
-        // (an fp32 layer has split-packed weights only on a split encoder side)
-        const bool split = dt == DT_F32 && L.qkv.wpk != nullptr && !enc_f32;
+        // (the decoder of an fp32 model keeps the fp32 attention: key chunks, attention.hip)
+        const bool split = dt == DT_F32 && L.split_attn && !enc_f32;
         if (TTS_BOUNDS_CHECK) {  // (diagnostic builds: runtime.h)
           const long long e = dtype_size(dt);
           std::string why;
@@ -724,6 +741,7 @@ void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtyp
   m->dte = enc_dtype == DT_F32 ? DT_F32 : dtype;
   m->bdt = m->dte;
   m->f32_split_enc = dtype == DT_F32 && f32_split_enc;
+  m->f32_split_dec = m->f32_split_enc && sw(SW_F32_DEC_SPLIT) != 0;
   m->enc_side = true;
   m->prof = prof;
   const auto es = shape("encoder.embed.weight");

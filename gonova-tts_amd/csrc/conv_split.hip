@@ -840,12 +840,15 @@ bool conv_split_eligible(const ConvParams& p) {
          split_group(p, 64, 1) > 0 && split_group(p, 32, 1) > 0;
 }
 
-// Per-utterance form (callers without the packed-row promise): 128 channels x 64 rows of one
-// utterance (NT = 2) when that grid fills the chip 4x over, else 32 rows (more blocks, a 160-row
-// cover of 144 rows instead of 192); the K order is the same.
+// Per-utterance form (callers without the packed-row promise: the fp32 vocoder's resblock convs,
+// an fp32 decoder's short-K GEMMs): 128 channels x 64 rows of one utterance (NT = 2) when that grid
+// has at least one block per CU, else 32 rows (twice the blocks); the K order is the same.
+#ifndef TTS_SPLIT_TILE_MINBLK
+#define TTS_SPLIT_TILE_MINBLK 256  // 64-row tiles from this many blocks (C1: 256 beat 1024 and 0, profiles/r06t/)
+#endif
 static int split_tile(const ConvParams& p) {
   const long long blocks2 = (long long)((p.y_rows + 63) / 64) * ((p.M + 127) / 128) * p.B;
-  return blocks2 >= 4 * 256 ? 2 : 1;
+  return blocks2 >= TTS_SPLIT_TILE_MINBLK ? 2 : 1;
 }
 
 template <int NT>

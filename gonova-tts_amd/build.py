@@ -62,7 +62,10 @@ def build(force: bool = False, verbose: bool = True, variant: str = "", defines=
         results = list(ex.map(lambda s: _compile(s, force, build_dir, defines), mine))
     objs = [o for o, _ in results] + [os.path.join(BUILD, os.path.basename(s) + ".o") for s in srcs if s not in mine]
     rebuilt = any(r for _, r in results)
-    if rebuilt or not os.path.exists(lib) or force:
+    # relink when any object is newer than the library too: a variant built with `only` links the
+    # product's objects, which the nested product build above may have recompiled
+    stale = not os.path.exists(lib) or any(os.path.getmtime(o) > os.path.getmtime(lib) for o in objs)
+    if rebuilt or stale or force:
         cmd = [HIPCC, "-shared", "-fPIC", "-Wl,-z,defs", f"--offload-arch={ARCH}", "-o", lib] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

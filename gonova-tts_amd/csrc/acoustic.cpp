@@ -681,7 +681,12 @@ struct AcousticModel::Impl {
     // (tests/test_acoustic_gpu.py).  TTS_DEC_TRIM=0: never; 1: whatever the budget (tests).
     int Td = Tcap;
     const int trim = sw(SW_DEC_TRIM);
-    if (!dur_override && B > 0 && (trim == 1 || (trim < 0 && Tcap > TTS_DEC_TRIM_RATIO * N))) {
+    // a stream being captured into a HIP graph cannot be synchronized: the decoder then runs at
+    // Tcap, which the capture records (the same output)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_CHECK(hipStreamIsCapturing(s, &cap));
+    if (!dur_override && B > 0 && cap == hipStreamCaptureStatusNone &&
+        (trim == 1 || (trim < 0 && Tcap > TTS_DEC_TRIM_RATIO * N))) {
       if (h_lens_n < B) {  // pinned: the copy is a DMA on the stream, not a staged blocking copy
         if (h_lens) HIP_CHECK(hipHostFree(h_lens));
         h_lens = nullptr;

@@ -735,3 +735,30 @@ def test_fp32_model_split_encoder_matches_fp32_mfma_encoder(aw, switch):
     assert int(rw.item()) == 0 and torch.isfinite(mel).all()
     e1.close()
     e2.close()
+
+
+def test_predicted_duration_forward_captures_into_a_graph(aw):
+    """with predicted durations and a loose budget the forward reads the frame counts back
+    mid-call (TTS_DEC_TRIM); on a stream being captured into a HIP graph it skips that read and runs
+    the decoder at the budget instead, so the capture succeeds, and the replay's mel and frame counts
+    equal the eager (trimmed) forward's bit for bit."""
+    eng = engine("bf16", aw)
+    rng = np.random.default_rng(77)
+    ids_list = [rng.integers(1, 78, size=n) for n in (30, 12, 21)]
+    B, N = len(ids_list), 30
+    tok = np.zeros((B, N), np.int32)
+    for b, x in enumerate(ids_list):
+        tok[b, :len(x)] = x
+    tok_d = torch.from_numpy(tok).to(DEV)
+    tl = torch.tensor([len(x) for x in ids_list], dtype=torch.int32, device=DEV)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        mel0, l0 = eng.acoustic(tok_d, tl, 12 * N, stream=s)  # eager: trimmed; reserves the workspace
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        mel1, l1 = eng.acoustic(tok_d, tl, 12 * N, stream=s)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(l0, l1)
+    assert torch.equal(mel0, mel1)

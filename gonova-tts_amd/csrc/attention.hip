@@ -90,8 +90,9 @@ __device__ inline uint2 at_tr16(const char* p) {
 constexpr int AT_BQ = 64;   // queries per block
 constexpr int AT_BK = 32;   // keys per step
 constexpr int AT_RW = AT_BQ + AT_BK;  // R window rows per block (95 used)
-// fp32 attention key chunk (keys per block; rel_attn_f32_kernel), TTS_ATTN_F32_KC (0: off)
-constexpr int AT_F32_KC = 128;
+// fp32 attention key chunk (keys per block; rel_attn_f32_kernel), TTS_ATTN_F32_KC (0: off).
+// C1 (same box, profiles/r06ab/): 64 beat 128 by 40-75 us per sentence and 256 by ~170; 32 ties 64
+constexpr int AT_F32_KC = 64;
 // Lazy online-softmax rescale (16-bit kernel): a row's reference max moves only when a step's
 // max exceeds it by more than AT_LAZY (log2 units), so P = 2^(s - m) stays <= 2^AT_LAZY (f16 /
 // bf16 hold it exactly as well as any P <= 1: same relative precision) and the O^T rescale of
@@ -410,7 +411,7 @@ __global__ __launch_bounds__(256 * KH, KH == 1 ? 2 : 1) void rel_attn_kernel(con
 // and writes its unnormalised O^T rows with the row's (max, sum) to `po` / `pml`;
 // rel_attn_merge_kernel combines an utterance's ceil(len / kc) chunks.  A batch-1 decoder
 // (C1: 7 query tiles x 2 heads = 14 blocks, one wave per SIMD on 14 of 256 CUs) gets
-// ceil(len / kc) times the blocks, each with 1 / that of the serial key loop.  The chunking
+// ceil(len / kc) times the blocks (98 at kc = 64), each with 1 / that of the serial key loop.  The chunking
 // depends on the utterance's length only (batch invariant), and a one-chunk row merges to the
 // direct form's bits (x * exp2(0) = x, then the same O * (1 / l)).
 template <int DK>

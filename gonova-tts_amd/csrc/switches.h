@@ -24,7 +24,7 @@ enum Sw : int {
   SW_PAIR_SPLIT,   // TTS_PAIR_SPLIT=0/1: the channel-split pair form never / wherever possible (default: small C >= 128 grids)
   SW_VP_BATCH,     // TTS_VP_BATCH=0: the variance predictors' first convs / LayerNorms as separate launches (fp32 encoder)
   SW_DEC_TRIM,     // TTS_DEC_TRIM=0/1: with predicted durations the decoder never / always runs at the longest utterance's frames (default: budgets over 8 frames per token)
-  SW_ATTN_F32_KC,  // TTS_ATTN_F32_KC=n: fp32 attention key chunk of n keys (multiple of 32; 0: one chunk; default 128)
+  SW_ATTN_F32_KC,  // TTS_ATTN_F32_KC=n: fp32 attention key chunk of n keys (multiple of 32; 0: one chunk; default 64)
   SW_F32_ENC_SPLIT,  // TTS_F32_ENC_SPLIT=0: an fp32 model's encoder side on fp32 MFMA even with TTS_ENCODER_EXACT (read at finalize)
   SW_F32_DEC_SPLIT,  // TTS_F32_DEC_SPLIT=0: an fp32 model's decoder / postnet all on fp32 MFMA (read at finalize; needs the encoder split)
   SW_N

@@ -671,22 +671,22 @@ def test_range_guard_falls_back_to_fp32_encoder(aw):
 
 
 def test_fp32_attention_key_chunks(aw, switch):
-    """fp32 attention in 128-key chunks merged by a second launch (attention.hip
-    rel_attn_f32_kernel / rel_attn_merge_kernel, TTS_ATTN_F32_KC): an utterance whose stacks fit one
-    chunk is bit-identical to the one-pass kernel (its merge is x * 2^0 then the same O / l); a
-    longer one differs only by the merge's summation order (2e-6 relative bound here), and a
-    426-frame utterance (C1's sentence: 4 decoder chunks) matches the oracle at the fp32 bar."""
+    """fp32 attention in key chunks merged by a second launch (attention.hip rel_attn_f32_kernel /
+    rel_attn_merge_kernel, TTS_ATTN_F32_KC, >= 32 keys): an utterance whose stacks fit one chunk is
+    bit-identical to the one-pass kernel (its merge is x * 2^0 then the same O / l); a longer one
+    differs only by the merge's summation order (2e-6 relative bound here), and a 426-frame
+    utterance (C1's sentence: several decoder chunks) matches the oracle at the fp32 bar."""
     eng = engine("f32", aw)
     rng = np.random.default_rng(23)
-    ids_list = [rng.integers(1, 78, size=n) for n in (71, 20, 30)]
-    durs = [np.full(len(x), 6, np.int32) for x in ids_list]  # 426, 120, 180 frames
+    ids_list = [rng.integers(1, 78, size=n) for n in (71, 5, 30)]
+    durs = [np.full(len(x), 6, np.int32) for x in ids_list]  # 426, 30, 180 frames
     t_cap = 426
     switch("TTS_ATTN_F32_KC", 0)
     m0, l0, _ = run(eng, ids_list, t_cap=t_cap, durations=durs)
-    switch("TTS_ATTN_F32_KC", None)  # the default: 128-key chunks
+    switch("TTS_ATTN_F32_KC", None)  # the default chunk
     m1, l1, _ = run(eng, ids_list, t_cap=t_cap, durations=durs)
-    assert np.array_equal(l0, l1) and list(l1) == [426, 120, 180]
-    assert np.array_equal(m1[1, :120], m0[1, :120])  # one chunk in both stacks
+    assert np.array_equal(l0, l1) and list(l1) == [426, 30, 180]
+    assert np.array_equal(m1[1, :30], m0[1, :30])  # one chunk in both stacks (<= 32 keys)
     for b in (0, 2):
         L = int(l1[b])
         err = np.abs(m1[b, :L] - m0[b, :L]).max() / np.abs(m0[b, :L]).max()

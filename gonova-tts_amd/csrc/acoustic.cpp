@@ -75,6 +75,8 @@ struct AcousticModel::Impl {
   int bdt = DT_F32;  // dtype of the layers being built (finalize)
   bool f32_split_enc = false;  // fp32 model: encoder side on split-precision GEMMs (finalize)
   bool f32_split_dec = false;  // ... and the decoder / postnet GEMMs of short K (finalize)
+  bool f32_dec_packed = false; // ... and the decoder's FFN down-projections on the packed split-K form
+  bool force_no_split = false; // run(): this launch on the fp32 path (a packed-only layer without pad rows)
   bool enc_side = false;       // the layers being built are the encoder side's (finalize)
   // fp32 layers of a 16-bit model (and the encoder side of an fp32 model with f32_split_enc) get
   // split-packed weights (three f16 MFMAs, conv_split.hip)
@@ -85,7 +87,25 @@ struct AcousticModel::Impl {
   // split-K GEMM (C1's batch-1 decoder: 42 blocks walking K = 4,608 would be slower)
   bool split_for(int taps, int cin) const {
     return split_now() || (bdt == DT_F32 && dt == DT_F32 && f32_split_dec && !enc_side &&
-                           (long long)taps * cin <= TTS_F32_DEC_SPLIT_MAXK);
+                           ((long long)taps * cin <= TTS_F32_DEC_SPLIT_MAXK || f32_dec_packed));
+  }
+  // the fp32 decoder's deep-K layers (the FFN down-projections, K = 4,608) run split only on the
+  // packed form, whose split-K needs the rows past each utterance as pad rows (the per-utterance
+  // split kernel has no split-K): with f32_dec_packed the decoder's row stride keeps at least one
+  // (dec_pad), so every batch takes the same path -- a stride without them would make the path,
+  // and an utterance's bits, depend on the batch's longest utterance
+  int dec_pad() const { return f32_dec_packed ? 1 : 0; }
+  bool dec_deep(const ConvLayer& L) const {
+    return dt == DT_F32 && f32_dec_packed && L.wpk && (long long)L.taps * L.Cin > TTS_F32_DEC_SPLIT_MAXK;
+  }
+  void run_deep_ln(const ConvLayer& L, const void* x, int x_rows, const int* lens, void* y, int y_rows, int B, int d,
+                   hipStream_t s, float alpha, const void* r1, void* out, const LNParam& a, const LNParam* b2, int rpad) {
+    const int keep = cur_rpad;
+    const bool packed = rpad >= std::max(1, L.pad);
+    if (packed) cur_rpad = rpad; else force_no_split = true;
+    run_ln(L, x, x_rows, lens, y, y_rows, B, d, s, alpha, r1, out, a, b2);
+    cur_rpad = keep;
+    force_no_split = false;
   }
   bool split_enc() const { return dte == DT_F32 && (dt != DT_F32 || f32_split_enc); }
   size_t esz() const { return std::max(dtype_size(dt), dtype_size(dte)); }
@@ -109,7 +129,7 @@ struct AcousticModel::Impl {
            const void* r1 = nullptr, const ConvParams* ln = nullptr) {
     ConvParams ex = ln ? *ln : conv_params_default();
     ex.range_flag = range_flag;
-    ex.no_split = enc_f32 ? 1 : 0;
+    ex.no_split = enc_f32 || force_no_split ? 1 : 0;
     ex.f32_splitk = dt == DT_F32 ? 1 : 0;  // fp32 model: split-K over split_ws (sized in reserve_fresh)
     run_layer(L, x, x_rows, lens, y, y_rows, B, d, s, pr, in_slope, act, alpha, r1, nullptr, 1.f, 0, 0, cur_rpad,
               split_ws, split_ws_bytes, &ex);
@@ -430,7 +450,7 @@ struct AcousticModel::Impl {
   void reserve_fresh(int B, int N, int T) {
     const size_t ee = dtype_size(dte), ed = dtype_size(dt);  // encoder-side / decoder-side element sizes
     const int Tm = std::max(N, T);
-    const int Tp = std::max(rup(Tm, 32), enc_rows(N));
+    const int Tp = std::max(rup(Tm + dec_pad(), 32), enc_rows(N));
     const int dk = D / H;
     const size_t rows = (size_t)B * Tp;
     const size_t nrows = (size_t)B * enc_rows(N);
@@ -445,7 +465,7 @@ struct AcousticModel::Impl {
     SPK = alloc_ws((size_t)B * D, ee);
     PB1 = alloc_ws(nrows * PRED, std::max<size_t>(ee, 2)); PB2 = alloc_ws(nrows * PRED, ee);  // PB1 also holds f32 logd [B][N]
     VP = alloc_ws(nrows * 3 * 256, 4);  // the batched first predictor convs (fp32, <= 256 channels each)
-    const size_t trows = (size_t)B * rup(T, 32);
+    const size_t trows = (size_t)B * rup(T + dec_pad(), 32);
     BEF = alloc_ws(trows * NMEL, ed); MELT = alloc_ws(trows * NMEL, ed);
     PN1 = alloc_ws(trows * PRED, ed); PN2 = alloc_ws(trows * PRED, ed);
     f_pitch = (float*)alloc_ws(nrows, 4); f_energy = (float*)alloc_ws(nrows, 4); f_logd = (float*)alloc_ws(nrows, 4);
@@ -519,7 +539,8 @@ struct AcousticModel::Impl {
       const int dt = L.dt;
       // macaron FFN: x = LN(x + 0.5 * ffn(x))
       run(L.ffm1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
-      run_ln(L.ffm2, H1, Tp, lens, Y, Tp, B, dt, s, 0.5f, Xb, Xb, L.ln_mac, nullptr);
+      if (!L.split_attn && dec_deep(L.ffm2)) run_deep_ln(L.ffm2, H1, Tp, lens, Y, Tp, B, dt, s, 0.5f, Xb, Xb, L.ln_mac, nullptr, Tp - Tm);
+      else run_ln(L.ffm2, H1, Tp, lens, Y, Tp, B, dt, s, 0.5f, Xb, Xb, L.ln_mac, nullptr);
       // relative-position MHSA: x = LN(x + mhsa(x))
       run(L.qkv, Xb, Tp, lens, QKV, Tp, B, dt, s, prof);
       const bool fused_attn = rel_attn_enabled() && rel_attn_supported(dt, D, H);
@@ -540,7 +561,7 @@ struct AcousticModel::Impl {
         prof_launch(PK_ATTN, 6.0 * D * (double)B * Tm * Tm, s, [&] { return launch_rel_attn(dt, split, L.pos_u, L.pos_v, QKV, L.ptab, lens, B, Tm, Tp, D, H, rmax, scale,
                                   O, s, range_flag, attn_ws, attn_ws_bytes); });
         run_ln(L.out, O, Tp, lens, Y, Tp, B, dt, s, 1.f, Xb, Xb, L.ln_att, nullptr);
-        conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
+        conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s, Tp - Tm);
         continue;
       }
       elem(s, [&] { return launch_transpose_v(dt, QKV, lens, B, Tp, D, H, Sk, Vt, s); });
@@ -556,11 +577,12 @@ struct AcousticModel::Impl {
       attn_gemm(dt, P, (long long)H * Tm * Sk, (long long)Tm * Sk, Sk, lens, Tm, Vt, (long long)H * dk * Sk,
                 (long long)dk * Sk, Sk, dk, Sk, O, (long long)Tp * D, dk, D, B, s);
       run_ln(L.out, O, Tp, lens, Y, Tp, B, dt, s, 1.f, Xb, Xb, L.ln_att, nullptr);
-      conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s);
+      conv_module_and_ffn(L, Xb, lens, B, Tp, rows, s, Tp - Tm);
     }
   }
 
-  void conv_module_and_ffn(ConformerLayer& L, void* Xb, const int* lens, int B, int Tp, int rows, hipStream_t s) {
+  void conv_module_and_ffn(ConformerLayer& L, void* Xb, const int* lens, int B, int Tp, int rows, hipStream_t s,
+                           int rpad) {
     const int dt = L.dt;
     // conv module: x = LN(x + pw2(silu(bn(dw(glu(pw1(x)))))))
     run(L.pw1, Xb, Tp, lens, A, Tp, B, dt, s, prof);
@@ -568,7 +590,8 @@ struct AcousticModel::Impl {
     run_ln(L.pw2, G, Tp, lens, Y, Tp, B, dt, s, 1.f, Xb, Xb, L.ln_conv, nullptr);
     // FFN: x = final_LN(LN(x + 0.5 * ffn(x)))
     run(L.ff1, Xb, Tp, lens, H1, Tp, B, dt, s, prof, 1.f, ACT_RELU);
-    run_ln(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, 0.5f, Xb, Xb, L.ln_ff, &L.ln_final);
+    if (!L.split_attn && dec_deep(L.ff2)) run_deep_ln(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, 0.5f, Xb, Xb, L.ln_ff, &L.ln_final, rpad);
+    else run_ln(L.ff2, H1, Tp, lens, Y, Tp, B, dt, s, 0.5f, Xb, Xb, L.ln_ff, &L.ln_final);
   }
 
   // The three predictors run in sequence on one stream: pitch and energy on two side streams
@@ -700,7 +723,7 @@ struct AcousticModel::Impl {
       for (int i = 0; i < B; ++i) mx = std::max(mx, h_lens[i]);
       Td = std::min(Tcap, mx);
     }
-    const int Tpd = rup(Td, 32);  // decoder row stride
+    const int Tpd = rup(Td + dec_pad(), 32);  // decoder row stride (dec_pad: at least one pad row)
     // regulate writes the Td frames of each utterance at row stride Tpd (frames past an
     // utterance's length are zero rows)
     void* Xd = X;
@@ -747,6 +770,7 @@ void AcousticModel::finalize(const GetData& get, const GetShape& shape, int dtyp
   m->bdt = m->dte;
   m->f32_split_enc = dtype == DT_F32 && f32_split_enc;
   m->f32_split_dec = m->f32_split_enc && sw(SW_F32_DEC_SPLIT) != 0;
+  m->f32_dec_packed = m->f32_split_dec && sw(SW_F32_DEC_PACKED) != 0;
   m->enc_side = true;
   m->prof = prof;
   const auto es = shape("encoder.embed.weight");

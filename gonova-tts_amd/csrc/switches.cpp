@@ -15,7 +15,8 @@ const char* const kNames[SW_N] = {"TTS_REL_ATTN", "TTS_MRF_FUSED", "TTS_MRF_CHAI
                                   "TTS_ATTN_KSPLIT", "TTS_SPLIT_WHOLE", "TTS_XRES_DMA", "TTS_LN_FUSE",
                                   "TTS_SPLIT_NT1", "TTS_XRES_ORDER",
                                   "TTS_PAIR_SPLIT", "TTS_VP_BATCH", "TTS_DEC_TRIM", "TTS_ATTN_F32_KC",
-                                  "TTS_F32_ENC_SPLIT", "TTS_F32_DEC_SPLIT"};
+                                  "TTS_F32_ENC_SPLIT", "TTS_F32_DEC_SPLIT",
+                                  "TTS_F32_DEC_PACKED"};
 std::atomic<int> g_val[SW_N];
 std::once_flag g_once;
 

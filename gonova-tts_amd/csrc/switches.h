@@ -27,6 +27,7 @@ enum Sw : int {
   SW_ATTN_F32_KC,  // TTS_ATTN_F32_KC=n: fp32 attention key chunk of n keys (multiple of 32; 0: one chunk; default 64)
   SW_F32_ENC_SPLIT,  // TTS_F32_ENC_SPLIT=0: an fp32 model's encoder side on fp32 MFMA even with TTS_ENCODER_EXACT (read at finalize)
   SW_F32_DEC_SPLIT,  // TTS_F32_DEC_SPLIT=0: an fp32 model's decoder / postnet all on fp32 MFMA (read at finalize; needs the encoder split)
+  SW_F32_DEC_PACKED,  // TTS_F32_DEC_PACKED=0: the fp32 decoder's FFN down-projections on fp32 MFMA, not the packed split-K form (finalize)
   SW_N
 };
 

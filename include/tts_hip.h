@@ -85,8 +85,8 @@ typedef struct tts_config {
  * clamp(round(exp(x) - 1), 0) (HF:181-183) match an fp32 evaluation; the decoder and postnet run in
  * acoustic_dtype.  FAST (1): the whole acoustic model runs in acoustic_dtype (durations can
  * round differently near .5).  With acoustic_dtype = F32, EXACT runs the encoder side on the same
- * split-precision GEMMs and attention, and the decoder / postnet GEMMs of K <= 1536 on the
- * split-precision GEMMs (round 6; the attention and the FFN down-projections stay fp32), and
+ * split-precision GEMMs and attention, and the decoder / postnet GEMMs on the split-precision
+ * GEMMs too (round 6; the decoder attention stays on the fp32 kernel), and
  * FAST keeps every layer on fp32 MFMA (switch TTS_F32_ENC_SPLIT=0 at finalize: the same). */
 enum { TTS_ENCODER_EXACT = 0, TTS_ENCODER_FAST = 1, TTS_ENCODER_F32 = 2 };
 /* Range limit of EXACT: its split GEMMs and attention hold every fp32 operand as two f16 halves,
@@ -196,7 +196,7 @@ int tts_engine_profile_read_kinds(tts_engine* eng, int nkinds, double* ms, doubl
  * reference paths): TTS_REL_ATTN, TTS_MRF_FUSED, TTS_MRF_CHAIN, TTS_POST_FUSE, TTS_UP_STREAM,
  * TTS_XRES_NARROW, TTS_XRES_NT, TTS_PAIR_DIV, TTS_ATTN_KSPLIT, TTS_SPLIT_WHOLE, TTS_XRES_DMA,
  * TTS_LN_FUSE, TTS_SPLIT_NT1, TTS_XRES_ORDER, TTS_PAIR_SPLIT, TTS_VP_BATCH, TTS_DEC_TRIM,
- * TTS_ATTN_F32_KC, TTS_F32_ENC_SPLIT, TTS_F32_DEC_SPLIT.  Each starts from its environment variable, read once; value -1 restores the built-in default.
+ * TTS_ATTN_F32_KC, TTS_F32_ENC_SPLIT, TTS_F32_DEC_SPLIT, TTS_F32_DEC_PACKED.  Each starts from its environment variable, read once; value -1 restores the built-in default.
  * Applies to launches enqueued after the call (use from one thread while no forward runs). */
 int tts_set_switch(const char* name, int value);
 /* Current value of a switch (-1 = not set), so a caller can restore what it changed. */

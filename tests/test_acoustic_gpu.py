@@ -762,3 +762,19 @@ def test_predicted_duration_forward_captures_into_a_graph(aw):
     torch.cuda.synchronize()
     assert torch.equal(l0, l1)
     assert torch.equal(mel0, mel1)
+
+
+@pytest.mark.parametrize("n_tok", [32, 33])
+def test_fp32_decoder_ffn_down_with_and_without_pad_rows(aw, n_tok):
+    """The fp32 decoder's FFN down-projections run split-precision on the packed split-K form, which
+    needs pad rows after the longest utterance: the decoder's row stride keeps at least one
+    (acoustic.cpp dec_pad), so 192 frames (a multiple of 32: stride 224) and 198 frames (stride
+    224) both take it, and both match the oracle at the fp32 bar."""
+    eng = engine("f32", aw)
+    ids = np.random.default_rng(100 + n_tok).integers(1, 78, size=n_tok)
+    d = np.full(n_tok, 6, np.int32)
+    mel, mel_lens, _ = run(eng, [ids], t_cap=6 * n_tok, durations=[d])
+    L = int(mel_lens[0])
+    assert L == 6 * n_tok
+    ref = acoustic_forward(ids, aw, durations=d)
+    np.testing.assert_allclose(mel[0, :L], ref["mel"], atol=FP32_ATOL, rtol=FP32_RTOL)

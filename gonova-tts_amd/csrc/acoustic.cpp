@@ -94,7 +94,8 @@ struct AcousticModel::Impl {
   // split kernel has no split-K): with f32_dec_packed the decoder's row stride keeps at least one
   // (dec_pad), so every batch takes the same path -- a stride without them would make the path,
   // and an utterance's bits, depend on the batch's longest utterance
-  int dec_pad() const { return f32_dec_packed ? 1 : 0; }
+  // (2: the postnet's k = 5 convs need two, and with them every split decoder-side GEMM runs packed)
+  int dec_pad() const { return f32_dec_packed ? 2 : 0; }
   bool dec_deep(const ConvLayer& L) const {
     return dt == DT_F32 && f32_dec_packed && L.wpk && (long long)L.taps * L.Cin > TTS_F32_DEC_SPLIT_MAXK;
   }
@@ -113,7 +114,7 @@ struct AcousticModel::Impl {
   // GEMMs run packed 128-row tiles across utterances (ConvParams::rows_pad; k <= 5 convs)
   static constexpr int ENC_PAD = 2;
   static int enc_rows(int N) { return rup(N + ENC_PAD, 32); }
-  int cur_rpad = 0;            // rows_pad of the convs being launched (encoder side only)
+  int cur_rpad = 0;            // rows_pad of the convs being launched (encoder side; an fp32 split decoder)
   float* split_ws = nullptr;   // split-K partial sums of the packed split GEMMs
   long long split_ws_bytes = 0;
   float* attn_ws = nullptr;    // fp32 attention key-chunk partials (fp32 models)
@@ -728,6 +729,9 @@ struct AcousticModel::Impl {
     // utterance's length are zero rows)
     void* Xd = X;
     elem(s, [&] { return launch_regulate(dte, dt, ENC, B, Np, D, i_tokmap, Tcap, Td, Tpd, xscale, X, s); });
+    // an fp32 model with f32_dec_packed: every split decoder-side GEMM on the packed form (its
+    // split-K and fused post-LN), over the pad rows dec_pad keeps after each utterance
+    cur_rpad = dec_pad() ? Tpd - Td : 0;
     stack(dec, Xd, mel_lens, B, Td, Tpd, s);
     // postnet (HF:238-244), BatchNorm folded
     run(feat_out, Xd, Tpd, mel_lens, BEF, Tpd, B, dt, s, prof);
@@ -741,6 +745,7 @@ struct AcousticModel::Impl {
                 last ? BEF : nullptr);
       h = o;
     }
+    cur_rpad = 0;
     // MELT rows have stride Tpd; output [B][Tcap][80] float32 (rows past mel_len zero)
     elem(s, [&] { return launch_mel_out(dt, MELT, mel_lens, B, Tpd, Tcap, NMEL, mel, s); });
   }

@@ -662,7 +662,10 @@ __global__ __launch_bounds__(256, 2) void conv_splitp_kernel(ConvParams p, int C
     // row-pass validity, bit it (rows inside F and the utterance's output length): the length
     // loads go with the residual prefetch, not one wait per row in the row pass
     int ym = 0;
-    const auto r1rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.r1 ? p.r1 : p.y), 0, p.r1 ? 0x7fffffff : 0, 0x00020000);
+    // (the record count stops short of the 0x7ffffff0 offset that lanes past M load from: they read 0.
+    // At 0x7fffffff that offset was in range -- a real load 2 GB past r1, which faulted on the first
+    // layer whose M is not a multiple of 128: the fp32 postnet's 80-channel last conv)
+    const auto r1rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.r1 ? p.r1 : p.y), 0, p.r1 ? 0x7ffffff0 : 0, 0x00020000);
     const auto brs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.bias ? p.bias : reinterpret_cast<const float*>(X)), 0,
                                                        p.bias ? p.M * 4 : 0, 0x00020000);
     const auto ylrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.y_len ? p.y_len : reinterpret_cast<const int*>(X)),

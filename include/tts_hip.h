@@ -86,7 +86,8 @@ typedef struct tts_config {
  * acoustic_dtype.  FAST (1): the whole acoustic model runs in acoustic_dtype (durations can
  * round differently near .5).  With acoustic_dtype = F32, EXACT runs the encoder side on the same
  * split-precision GEMMs and attention, and the decoder / postnet GEMMs on the split-precision
- * GEMMs too (round 6; the decoder attention stays on the fp32 kernel), and
+ * GEMMs too (round 6; the decoder attention stays on the fp32 kernel; its row stride keeps two
+ * pad rows per utterance), and
  * FAST keeps every layer on fp32 MFMA (switch TTS_F32_ENC_SPLIT=0 at finalize: the same). */
 enum { TTS_ENCODER_EXACT = 0, TTS_ENCODER_FAST = 1, TTS_ENCODER_F32 = 2 };
 /* Range limit of EXACT: its split GEMMs and attention hold every fp32 operand as two f16 halves,

@@ -767,9 +767,10 @@ def test_predicted_duration_forward_captures_into_a_graph(aw):
 @pytest.mark.parametrize("n_tok", [32, 33])
 def test_fp32_decoder_ffn_down_with_and_without_pad_rows(aw, n_tok):
     """The fp32 decoder's FFN down-projections run split-precision on the packed split-K form, which
-    needs pad rows after the longest utterance: the decoder's row stride keeps at least one
-    (acoustic.cpp dec_pad), so 192 frames (a multiple of 32: stride 224) and 198 frames (stride
-    224) both take it, and both match the oracle at the fp32 bar."""
+    needs pad rows after the longest utterance: the decoder's row stride keeps two (acoustic.cpp
+    dec_pad), so 192 frames (a multiple of 32: stride 224) and 198 frames (stride 224) both take
+    it, and both match the oracle at the fp32 bar (the postnet's 80-channel last conv, with its
+    residual, on the packed form too)."""
     eng = engine("f32", aw)
     ids = np.random.default_rng(100 + n_tok).integers(1, 78, size=n_tok)
     d = np.full(n_tok, 6, np.int32)

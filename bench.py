@@ -559,9 +559,9 @@ def bench_streaming(ctx, trials=50, B=8, N=144, chunk=32, encoder_precision="exa
     durations given by the caller (stream_tokens(durations=...)): the predictor does not run and
     the frame counts are known on the host without a sync."""
     torch = ctx.torch
-    from gonova_tts_amd.model import GonovaTTS
-    m = GonovaTTS.from_pretrained(ctx.dev.index, vocoder_dtype="bf16", acoustic_dtype="bf16",
-                                  encoder_precision=encoder_precision, fixed_duration=6 if predicted else None)
+    from gonova_tts_amd import model as M
+    m = M.GonovaTTS.from_pretrained(ctx.dev.index, vocoder_dtype="bf16", acoustic_dtype="bf16",
+                                    encoder_precision=encoder_precision, fixed_duration=6 if predicted else None)
     rng = np.random.default_rng(5)
     tok = rng.integers(1, 78, size=(B, N)).astype(np.int32)
     lens = np.full(B, N, np.int32)
@@ -572,7 +572,7 @@ def bench_streaming(ctx, trials=50, B=8, N=144, chunk=32, encoder_precision="exa
         t0 = time.perf_counter()
         gen = m.stream_tokens(tok, lens, chunk_frames=chunk, durations=dur)
         _, wav, valid = next(gen)
-        _ = wav.cpu()
+        _ = M._to_host(wav)  # the product's consumer path (GonovaTTS.stream_batch): pinned copy
         t = time.perf_counter() - t0
         gen.close()
         assert int(valid[0]) == chunk * 256

@@ -346,8 +346,13 @@ class HipEngine:
         B, N = tokens.shape
         # (every row is written: the frames past each utterance's length as zeros, mel_out_kernel)
         mel = torch.empty((B, t_cap, 80), dtype=torch.float32, device=tokens.device)
-        mel_lens = torch.empty((B,), dtype=torch.int32, device=tokens.device)
-        dur_out = torch.empty((B, N), dtype=torch.int32, device=tokens.device)
+        # the integer outputs (durations, frame counts, range word) are views of one int32 block at
+        # 64-byte aligned offsets, so a caller reads them back with one copy (model._HostRead)
+        o_len = -(-B * N // 16) * 16
+        o_rw = o_len + -(-B // 16) * 16
+        meta = torch.empty((o_rw + 16,), dtype=torch.int32, device=tokens.device)
+        dur_out = meta[:B * N].view(B, N)
+        mel_lens = meta[o_len:o_len + B]
         dptr = ctypes.c_void_p(0)
         if durations is not None:
             durations = durations.to(device=tokens.device, dtype=torch.int32).contiguous()
@@ -367,7 +372,7 @@ class HipEngine:
         # accumulating, so the next caller that asks sees an earlier unread overflow too (a spurious
         # fp32 rerun at worst, never a lost one)
         if self.range_guard and return_range:
-            rw = torch.empty((1,), dtype=torch.int32, device=tokens.device)
+            rw = meta[o_rw:o_rw + 1]
             check(self.lib.tts_acoustic_range_flag(self.handle, ctypes.c_void_p(rw.data_ptr()), _stream_ptr(stream)),
                   "tts_acoustic_range_flag")
         out = (mel, mel_lens, dur_out) if return_durations else (mel, mel_lens)

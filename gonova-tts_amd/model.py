@@ -454,22 +454,30 @@ def _upload_i32(arrays, dev, stream=None):
     stream, a batch's inputs went up only when the previous batch's kernels had finished -- the
     moment dist.ShardedSynthesis (C4) starts that batch's waveform download, which held the small
     uploads (and the GPU) for ~0.7-1.7 ms per batch (profiles/r05zz_c4_gaps.txt).  Issued at once
-    on their own stream they land while the previous batch still computes."""
+    on their own stream they land while the previous batch still computes.  The arrays share one
+    pinned block and one copy (64-byte aligned segments; the device tensors are views of it):
+    the host time before the first kernel of a request is on C5's critical path."""
     import torch
     target = stream if stream is not None else torch.cuda.current_stream(dev)
     idx = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
     up = _UPLOAD_STREAMS.get(idx)
     if up is None:
         up = _UPLOAD_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    host = [None if a is None else np.ascontiguousarray(a, np.int32) for a in arrays]
+    offs, total = [], 0
+    for a in host:
+        offs.append(total)
+        total += 0 if a is None else -(-a.size // 16) * 16
+    pinned = torch.empty((max(total, 16),), dtype=torch.int32, pin_memory=True)
+    hv = pinned.numpy()
+    for a, o in zip(host, offs):
+        if a is not None:
+            hv[o:o + a.size] = a.reshape(-1)
     with torch.cuda.stream(up):
-        out = [None if a is None else
-               torch.from_numpy(np.ascontiguousarray(a, np.int32)).pin_memory().to(dev, non_blocking=True)
-               for a in arrays]
+        blk = pinned.to(dev, non_blocking=True)
     target.wait_stream(up)
-    for t in out:
-        if t is not None:
-            t.record_stream(target)  # (allocated on the upload stream, used on the target)
-    return out
+    blk.record_stream(target)  # (allocated on the upload stream, used on the target)
+    return [None if a is None else blk[o:o + a.size].view(a.shape) for a, o in zip(host, offs)]
 
 
 def _to_host(t):
@@ -489,20 +497,32 @@ class _HostRead:
     """_need_and_lens without the blocking read: the durations, frame counts and range word are
     copied into page-locked host memory on the compute stream (where the forward enqueued them)
     and an event is recorded after them; result() waits for that event only, not for work the
-    caller enqueued afterwards, and sums on the host."""
+    caller enqueued afterwards, and sums on the host.  When the three are views of one block (as
+    GonovaEngine.acoustic returns them) the block is read with one copy."""
 
     def __init__(self, dur, mel_lens, rw=None, stream=None):
         import torch
         s = stream if stream is not None else torch.cuda.current_stream(mel_lens.device)
+        ts = (dur, mel_lens, rw)
+        base = getattr(mel_lens, "_base", None)
+        one = base is not None and base.is_contiguous() and base.dtype == torch.int32 and \
+            all(t is None or (getattr(t, "_base", None) is base and t.is_contiguous()) for t in ts)
         with torch.cuda.stream(s):
-            self.bufs = []
-            for t in (dur, mel_lens, rw):
-                if t is None:
-                    self.bufs.append(None)
-                    continue
-                h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-                h.copy_(t, non_blocking=True)
-                self.bufs.append(h)
+            if one:
+                h = torch.empty(base.shape, dtype=base.dtype, pin_memory=True)
+                h.copy_(base, non_blocking=True)
+                p0 = base.data_ptr()
+                self.bufs = [None if t is None else
+                             h[(t.data_ptr() - p0) // 4:(t.data_ptr() - p0) // 4 + t.numel()].view(t.shape) for t in ts]
+            else:
+                self.bufs = []
+                for t in ts:
+                    if t is None:
+                        self.bufs.append(None)
+                        continue
+                    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                    h.copy_(t, non_blocking=True)
+                    self.bufs.append(h)
             self.ev = torch.cuda.Event()
             self.ev.record(s)
 

@@ -169,3 +169,31 @@ def test_device_bytes_cover_weights_and_workspace():
     assert b1 - b0 >= wbytes + work
     eng.close()
     assert device_bytes(0) == b0
+
+
+def test_packed_upload_and_host_read(model32):
+    """The request's integer inputs go up as one pinned block (model._upload_i32) and the
+    acoustic pass's durations / frame counts / range word come back with one copy
+    (model._HostRead over GonovaEngine.acoustic's views): the values equal per-array transfers."""
+    from gonova_tts_amd import model as M
+    rng = np.random.default_rng(3)
+    tok = rng.integers(1, 70, size=(3, 17)).astype(np.int32)
+    lens = np.array([17, 9, 1], np.int32)
+    dur = rng.integers(0, 5, size=(3, 17)).astype(np.int64)
+    empty = np.zeros((2, 0), np.int32)
+    t_d, l_d, none_d, d_d, e_d = M._upload_i32((tok, lens, None, dur, empty), "cuda:0")
+    assert none_d is None and e_d.shape == (2, 0)
+    for a, d in ((tok, t_d), (lens, l_d), (dur, d_d)):
+        assert d.dtype == torch.int32 and d.is_contiguous() and tuple(d.shape) == a.shape
+        np.testing.assert_array_equal(d.cpu().numpy(), a.astype(np.int32))
+    assert t_d.data_ptr() % 64 == 0 and l_d.data_ptr() % 64 == 0 and d_d.data_ptr() % 64 == 0
+    eng = model32.engine
+    mel, mel_lens, dd, rw = eng.acoustic(t_d, l_d, 12 * 17, return_durations=True, return_range=True)
+    one = M._HostRead(dd, mel_lens, rw)
+    sep = M._HostRead(dd.clone(), mel_lens.clone(), None if rw is None else rw.clone())
+    need1, lens1, tr1 = one.result()
+    need2, lens2, tr2 = sep.result()
+    assert need1 == need2 and tr1 == tr2
+    np.testing.assert_array_equal(lens1, lens2)
+    np.testing.assert_array_equal(lens1, mel_lens.cpu().numpy())
+    np.testing.assert_array_equal(one.bufs[0].numpy(), dd.cpu().numpy())

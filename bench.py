@@ -288,11 +288,17 @@ class Ctx:
 
 
 def pmc_traffic(kernel, kind="c2"):
-    """HBM bytes per launch of one kernel family from the newest committed PMC summary
-    (tools/pmc_traffic.py, profiles/*_pmc_traffic_<kind>.json: "c2" the headline step, "c3voc_bf16"
-    the C3 vocoder in bf16 at 864 frames), if it covers that family."""
+    """HBM bytes per launch of one kernel family from a committed PMC summary (tools/pmc_traffic.py,
+    profiles/*_pmc_traffic_<kind>.json: "c2" the headline step, "c3voc_bf16" the C3 vocoder in bf16
+    at 864 frames), if it covers that family: the file profiles/pmc_current.json names for `kind`
+    (the run on the current kernels), else the last by name."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_traffic_{kind}.json")))
+    cur = os.path.join(ROOT, "profiles", "pmc_current.json")
+    if os.path.exists(cur):
+        name = json.load(open(cur)).get(kind)
+        if name and os.path.exists(os.path.join(ROOT, "profiles", name)):
+            files = [os.path.join(ROOT, "profiles", name)]
     if not files:
         return None
     d = json.load(open(files[-1]))

@@ -2,7 +2,8 @@
 # usage (on the GPU box): bash tools/evidence.sh <tag>
 # Round evidence in one call, everything under gpurun_out/<tag>/:
 #   1. PMC traffic of the default C2 step (separate FETCH_SIZE / WRITE_SIZE passes) ->
-#      profiles/<tag>_pmc_traffic_c2.json (read by bench.py for roofline.traffic), and of the
+#      profiles/<tag>_pmc_traffic_c2.json (bench.py reads the file profiles/pmc_current.json names
+#      for roofline.traffic: point it at the new tag), and of the
 #      C3 vocoder (bf16, 864 frames) -> profiles/<tag>_pmc_traffic_c3voc_bf16.json
 #      (full_pipeline.roofline.traffic);
 #   2. the default bench line (bench.json);

@@ -1,4 +1,4 @@
-"""Multi-process CPU tests (gloo, world size 2 and 3) of the utterance-sharding
+"""Multi-process CPU tests (gloo, world size 2, 3, 4 and 8) of the utterance-sharding
 bookkeeping: plan, token broadcast, packed P2P gather, original order restored."""
 import os
 import socket
@@ -68,7 +68,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,empties", [(2, False), (3, False), (2, True)])
+@pytest.mark.parametrize("world,empties", [(2, False), (3, False), (2, True), (8, False)])  # 8: the driver's N=8 layout
 def test_sharded_gather_restores_order(world, empties):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -58,3 +58,22 @@ def test_failed_rank_ends_the_run_within_seconds():
     assert "rank 1 exited with status 7" in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert took < 60, took
+
+
+def test_driver_torchrun_form_8_ranks():
+    """The driver's N=8 launch, verbatim (torch.distributed.run, one node, 8 processes, master on
+    127.0.0.1), on the gloo selftest: one JSON line from rank 0 with every rank in the all-reduce."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "8",
+                        "--workload", "selftest"], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["rank_sum"] == 28.0 and out["config"]["parallelism"] == "dp8"

@@ -502,6 +502,8 @@ struct AcousticModel::Impl {
     split_ws_bytes = wsb;
     // fp32 models: the key-chunk partials of the fp32 attention (attention.hip), both stacks
     attn_ws_bytes = dt == DT_F32 ? rel_attn_f32_ws_bytes(B, Tm, Tp, D, H) : 0;
+    // the split-precision attention of an fp32 encoder side (key chunks in TTS_ATTN_SPLIT_KC builds)
+    if (dte == DT_F32) attn_ws_bytes = std::max(attn_ws_bytes, rel_attn_split_ws_bytes(B, N, enc_rows(N), D, H));
     attn_ws = attn_ws_bytes ? (float*)alloc_ws((size_t)attn_ws_bytes, 1) : nullptr;
     cap_B = B; cap_N = N; cap_T = T;
   }

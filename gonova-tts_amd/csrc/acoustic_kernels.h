@@ -52,5 +52,6 @@ hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* 
                            long long ws_bytes = 0);
 int rel_attn_f32_kc();  // keys per chunk of the fp32 form (0: no chunks)
 long long rel_attn_f32_ws_bytes(int B, int Tm, int Tp, int D, int H);
+long long rel_attn_split_ws_bytes(int B, int Tm, int Tp, int D, int H);  // split form's key-chunk partials (0: none)
 
 }  // namespace tts

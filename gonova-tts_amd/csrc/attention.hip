@@ -93,6 +93,12 @@ constexpr int AT_RW = AT_BQ + AT_BK;  // R window rows per block (95 used)
 // fp32 attention key chunk (keys per block; rel_attn_f32_kernel), TTS_ATTN_F32_KC (0: off).
 // C1 (same box, profiles/r06ab/): 64 beat 128 by 40-75 us per sentence and 256 by ~170; 32 ties 64
 constexpr int AT_F32_KC = 64;
+// Key chunk of the split-precision form (the exact encoder), a multiple of AT_BK; 0: one pass.
+// A build-time choice (A/B variant builds): see DESIGN §11 for the batch-8 / batch-32 trade.
+#ifndef TTS_ATTN_SPLIT_KC
+#define TTS_ATTN_SPLIT_KC 0
+#endif
+static_assert(TTS_ATTN_SPLIT_KC % AT_BK == 0, "split key chunk: whole key steps");
 // Lazy online-softmax rescale (16-bit kernel): a row's reference max moves only when a step's
 // max exceeds it by more than AT_LAZY (log2 units), so P = 2^(s - m) stays <= 2^AT_LAZY (f16 /
 // bf16 hold it exactly as well as any P <= 1: same relative precision) and the O^T rescale of
@@ -669,7 +675,8 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
                                                                const float* __restrict__ ptab, const int* __restrict__ lens,
                                                                int Tp, int D, int H, int rmax, float scale,
                                                                float* __restrict__ out, int nqb, int nbatch,
-                                                               int* __restrict__ range_flag) {
+                                                               int* __restrict__ range_flag, int kc, int nks,
+                                                               float* __restrict__ po, float* __restrict__ pml) {
   using MF = Mfma16<half_t>;
   typedef half8 Frag;
   constexpr int KS = DK / 32;         // k-steps over dk
@@ -682,12 +689,16 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
   char* Rs = Vs + 2 * KPL;                                // 2 x [96 slots][DK]
   float* Gs = reinterpret_cast<float*>(Rs + 2 * RPL);     // [4 waves][48 slots][16 q]
 
-  int bh, qb;
-  if (!xcd_tile(nqb, H * nbatch, bh, qb)) return;
+  int bh, qt;
+  if (!xcd_tile(nqb * nks, H * nbatch, bh, qt)) return;
+  const int kcn = qt / nqb, qb = qt - kcn * nqb;  // key chunk, query tile (rel_attn_f32_kernel's map)
   const int b = bh / H, h = bh - b * H;
   const int i0 = qb * AT_BQ;
   const int len = lens[b];
   if (i0 >= len) return;
+  const int kbeg = kcn * kc;  // (kc = 0: one chunk, all keys; kc a multiple of AT_BK)
+  if (kbeg >= len) return;
+  const int kend = kc > 0 ? min(len, kbeg + kc) : len;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane & 15, g = lane >> 4;
@@ -746,7 +757,7 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
     kofs[i] = r * rowB + c * 16;                         // K and V rows
     kdst[i] = r * KR + c * 8;
     rofs[i] = r * D * 4 + c * 16;                        // table row row0 + r <-> m = i0 - j0 - r
-    rdst[i] = rslot(i0 - AT_BK - r) * KR + c * 8;        // slot for the first prefetch (j0 = 32)
+    rdst[i] = rslot(i0 - kbeg - AT_BK - r) * KR + c * 8;  // slot for the first prefetch (j0 = kbeg + 32)
   }
   f32x4 pkv[KP], pvt[KP], prr[KP];
   auto load_kv = [&](int j0) __attribute__((always_inline)) {
@@ -783,17 +794,18 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
   };
   for (int p = tid; p < AT_RW * (DK / 4); p += 256) {
     const int sb = p / (DK / 4), c = p - sb * (DK / 4);
-    const int m = i0 - (AT_BK - 1) + sb;
+    const int m = i0 - kbeg - (AT_BK - 1) + sb;
     put(Rs, RPL, rslot(m) * KR + c * 8, *reinterpret_cast<const f32x4*>(ptab + (long long)rrow(m) * rowD + h * DK + c * 4));
   }
-  load_kv(0);
+  load_kv(kbeg);
   write_kv();
   __syncthreads();
-  unsigned ra = rslot(i0w - (AT_BK - 1) + q) * KR + 16 * g;  // this lane's R rows (slot of m + 16 t) and column
+  unsigned ra = rslot(i0w - kbeg - (AT_BK - 1) + q) * KR + 16 * g;  // this lane's R rows (slot of m + 16 t) and column
   const int vta = at_tr_addr(KR, g, q);  // this lane's transposed-read address in the V planes (tile 0)
 
-  // (the last-step peel of rel_attn_kernel pushed this kernel past 256 VGPRs: kept as one loop)
-  for (int j0 = 0; j0 < len; j0 += AT_BK) {
+  // (the last-step peel of rel_attn_kernel pushed this kernel past 256 VGPRs: kept as one loop).
+  // Only the last chunk's last step has keys past len (kc is a multiple of AT_BK): the mask below.
+  for (int j0 = kbeg; j0 < kend; j0 += AT_BK) {
     load_kv(j0 + AT_BK);
     load_r(j0 + AT_BK);
     __builtin_amdgcn_sched_barrier(0);
@@ -902,11 +914,20 @@ __global__ __launch_bounds__(256, 1) void rel_attn_split_kernel(const float* __r
   }
   const int i = i0w + q;
   if (i < len) {
-    const float inv = 1.f / l_run;
-    float* orow = out + ((long long)b * Tp + i) * rowD + h * DK;
+    if (po != nullptr) {  // key chunk: unnormalised rows and the row's (reference max, sum), merged
+                          // by rel_attn_merge_kernel (the lazy reference max is a valid one)
+      const long long prow = ((long long)(kcn * nbatch + b) * H + h) * Tp + i;
+      float* orow = po + prow * DK;
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
-      *reinterpret_cast<f32x4*>(orow + 16 * t + 4 * g) = (oacc[t] + oaccx[t] * (1.f / AT_SPLIT)) * inv;
+      for (int t = 0; t < DT; ++t) *reinterpret_cast<f32x4*>(orow + 16 * t + 4 * g) = oacc[t] + oaccx[t] * (1.f / AT_SPLIT);
+      if (g == 0) *reinterpret_cast<float2*>(pml + 2 * prow) = float2{m_run, l_run};
+    } else {
+      const float inv = 1.f / l_run;
+      float* orow = out + ((long long)b * Tp + i) * rowD + h * DK;
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+        *reinterpret_cast<f32x4*>(orow + 16 * t + 4 * g) = (oacc[t] + oaccx[t] * (1.f / AT_SPLIT)) * inv;
+    }
   }
   range_report(range_flag, rng);
 }
@@ -940,6 +961,13 @@ int rel_attn_f32_kc() {
   return v == 0 ? 0 : std::max(AT_BK, v / AT_BK * AT_BK);
 }
 
+long long rel_attn_split_ws_bytes(int B, int Tm, int Tp, int D, int H) {
+  const int kc = TTS_ATTN_SPLIT_KC;
+  if (kc == 0 || Tm <= kc) return 0;
+  const long long nks = (Tm + kc - 1) / kc;
+  return nks * B * Tp * ((long long)D + 2 * H) * 4;
+}
+
 long long rel_attn_f32_ws_bytes(int B, int Tm, int Tp, int D, int H) {
   const int kc = rel_attn_f32_kc();
   if (kc == 0 || Tm <= kc) return 0;
@@ -954,9 +982,25 @@ hipError_t launch_rel_attn(int dt, bool split, const float* pos_u, const float* 
   const int nqb = (Tm + AT_BQ - 1) / AT_BQ;
   dim3 grid(xcd_grid(nqb, H * B));
   if (dt == DT_F32 && split) {
+    // key chunks of TTS_ATTN_SPLIT_KC keys when the workspace holds them (as the fp32 form below)
+    const int kc = TTS_ATTN_SPLIT_KC;
+    const long long need = rel_attn_split_ws_bytes(B, Tm, Tp, D, H);
+    if (need > 0 && ws != nullptr && need <= ws_bytes) {
+      const int nks = (Tm + kc - 1) / kc;
+      float* po = ws;
+      float* pml = ws + (long long)nks * B * Tp * D;
+      hipLaunchKernelGGL((rel_attn_split_kernel<192>), dim3(xcd_grid(nqb * nks, H * B)), dim3(256), rel_attn_split_lds<192>(), s,
+                         pos_u, pos_v, (const float*)qkv, (const float*)ptab, lens, Tp, D, H, rmax, scale,
+                         (float*)out, nqb, B, range_flag, kc, nks, po, pml);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL((rel_attn_merge_kernel<192>), dim3((B * Tp + 1) / 2), dim3(192), 0, s, po, pml, lens, Tp, D, H,
+                         kc, B, (float*)out);
+      return hipGetLastError();
+    }
     hipLaunchKernelGGL((rel_attn_split_kernel<192>), grid, dim3(256), rel_attn_split_lds<192>(), s, pos_u, pos_v,
                        (const float*)qkv, (const float*)ptab, lens, Tp, D, H, rmax, scale,
-                       (float*)out, nqb, B, range_flag);
+                       (float*)out, nqb, B, range_flag, 0, 1, nullptr, nullptr);
     return hipGetLastError();
   }
   if (dt == DT_F32) {

@@ -5,6 +5,8 @@ latency-bound acoustic pass overlaps the other half's MFMA-bound vocoder:
   conc     two engines, B = 16 each, both halves started together every step
   stagger  two engines, B = 16 each; the second half's stream starts after the first half's
            acoustic pass (one event), so its acoustic pass runs beside the first half's vocoder
+  concK    K engines (PROBE_K, default "3,4"), the batch split in K near-equal parts, all started
+           together every step, a stream each
 Prints ms per 32-utterance step (device-resident inputs, 10 timed steps after 3 warmups).
 
 usage (GPU box): python3 tools/c3_overlap_probe.py
@@ -77,6 +79,33 @@ def main():
     print(f"C3 ms per 32-utterance step: seq {t_seq:.3f} / {t_seq2:.3f}, conc {t_conc:.3f}, stagger {t_stag:.3f}")
     e1.close()
     e2.close()
+    for k in [int(x) for x in os.environ.get("PROBE_K", "3,4").split(",") if x]:
+        cuts = [B * i // k for i in range(k + 1)]
+        parts = [slice(cuts[i], cuts[i + 1]) for i in range(k)]
+        engs = []
+        for sl in parts:
+            e = HipEngine("cuda:0", vocoder_dtype="bf16", acoustic_dtype="bf16", max_batch=sl.stop - sl.start,
+                          max_frames=T, max_tokens=N)
+            e.load_weights(vocoder=vw, acoustic=aw)
+            engs.append(e)
+        sts = [torch.cuda.Stream() for _ in range(k)]
+
+        def conc_k():
+            cur = torch.cuda.current_stream()
+            for st in sts:
+                st.wait_stream(cur)
+            for e, st, sl in zip(engs, sts, parts):
+                with torch.cuda.stream(st):
+                    mel, ml = e.acoustic(tok[sl], tl[sl], T, stream=st)
+                    e.vocoder(mel, ml, out=wav[sl], stream=st)
+            for st in sts:
+                cur.wait_stream(st)
+
+        t_k = timed(conc_k)
+        t_k2 = timed(conc_k)
+        print(f"C3 ms per 32-utterance step: conc{k} {t_k:.3f} / {t_k2:.3f} ({[sl.stop - sl.start for sl in parts]})")
+        for e in engs:
+            e.close()
 
 
 if __name__ == "__main__":

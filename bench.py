@@ -439,7 +439,44 @@ def bench_full(ctx, args, steps, warmup):
         torch.cuda.synchronize()
         assert int(lens2.min()) == T
         eng2.close()
-    el = min(el1, el2) if el2 is not None else el1
+    # Pipelined across batches, the service's steady state under load (a stream of requests): every
+    # timed step runs one whole 32-utterance acoustic pass (engine A, stream a) beside the vocoder
+    # pass of the batch before it (engine B, stream b), both streams joined at the end of the step.
+    # K timed steps therefore do K acoustic and K vocoder passes of 32 utterances each; the first
+    # timed vocoder consumes the mel of the last warmup step.  The waveform is checked bit for bit
+    # against the one-stream step's (tools/c3_overlap_probe.py, round 6: 21.0 vs 21.4 ms two halves).
+    step()
+    torch.cuda.synchronize()
+    ref = wav.clone()  # the one-stream step's waveform
+    engp = HipEngine(ctx.local, vocoder_dtype="bf16", acoustic_dtype="bf16", max_batch=B, max_frames=T, max_tokens=N)
+    engp.load_weights(vocoder=make_vocoder_weights(seed=0), acoustic=make_acoustic_weights(seed=0, fixed_duration=dur))
+    # the two-engine form's streams when it ran: HIP maps streams onto a few hardware queues in
+    # creation order, and two more new streams can share one queue (no overlap at all)
+    spa, spb = (sa, sb) if h > 0 else (torch.cuda.Stream(device=ctx.dev), torch.cuda.Stream(device=ctx.dev))
+    prev = {}
+
+    def step3():
+        cur = torch.cuda.current_stream()
+        spa.wait_stream(cur)
+        spb.wait_stream(cur)
+        with torch.cuda.stream(spa):
+            m_, l_ = eng.acoustic(tok, tl, T, stream=spa)
+        if prev:
+            with torch.cuda.stream(spb):
+                engp.vocoder(prev["mel"], prev["lens"], out=wav, stream=spb)
+        cur.wait_stream(spa)
+        cur.wait_stream(spb)
+        prev.update(mel=m_, lens=l_)
+
+    el3, _ = ctx.timed(step3, steps, max(warmup, 1))
+    torch.cuda.synchronize()
+    assert torch.equal(wav, ref), "pipelined C3 waveform differs from the one-stream step's"
+    engp.close()
+    forms = {"one engine, one stream": el1, "pipelined: batch k's acoustic pass beside batch k-1's vocoder (two engines, two streams)": el3}
+    if el2 is not None:
+        forms["two engines on two streams, 16 utterances each"] = el2
+    form = min(forms, key=forms.get)
+    el = forms[form]
     value = samples / el
     ac_ms = None
     # acoustic-only timing (same inputs) to split the step; the live per-family timing of its
@@ -468,10 +505,10 @@ def bench_full(ctx, args, steps, warmup):
     el_f, _ = ctx.timed(lambda: engf.acoustic(tok, tl, T), steps, 1)
     engf.close()
     return {"value": round(value, 1), "unit": "samples/s", "ms_per_step": round(el * 1e3 / steps, 3),
-            "form": "two engines on two streams, 16 utterances each" if el2 is not None and el2 < el1
-                    else "one engine, one stream",
+            "form": form,
             "one_stream_ms_per_step": round(el1 * 1e3 / steps, 3),
             "two_engine_ms_per_step": round(el2 * 1e3 / steps, 3) if el2 is not None else None,
+            "pipelined_ms_per_step": round(el3 * 1e3 / steps, 3),
             "acoustic_ms_per_step": round(ac_ms, 3),
             "acoustic_roofline": ac_roof,
             "acoustic_ms_per_step_fast_encoder": round(el_f * 1e3 / steps, 3),

@@ -7,6 +7,8 @@ latency-bound acoustic pass overlaps the other half's MFMA-bound vocoder:
            acoustic pass (one event), so its acoustic pass runs beside the first half's vocoder
   concK    K engines (PROBE_K, default "3,4"), the batch split in K near-equal parts, all started
            together every step, a stream each
+  pipe     two engines, whole batches: step i runs batch i's acoustic pass (engine A, stream a)
+           beside batch i-1's vocoder (engine B, stream b); both streams joined every step
 Prints ms per 32-utterance step (device-resident inputs, 10 timed steps after 3 warmups).
 
 usage (GPU box): python3 tools/c3_overlap_probe.py
@@ -77,8 +79,34 @@ def main():
     t_stag = timed(lambda: halves(True))
     t_seq2 = timed(seq)
     print(f"C3 ms per 32-utterance step: seq {t_seq:.3f} / {t_seq2:.3f}, conc {t_conc:.3f}, stagger {t_stag:.3f}")
-    e1.close()
     e2.close()
+    ea = HipEngine("cuda:0", vocoder_dtype="bf16", acoustic_dtype="bf16", max_batch=B, max_frames=T, max_tokens=N)
+    ea.load_weights(vocoder=vw, acoustic=aw)
+    eb = HipEngine("cuda:0", vocoder_dtype="bf16", acoustic_dtype="bf16", max_batch=B, max_frames=T, max_tokens=N)
+    eb.load_weights(vocoder=vw, acoustic=aw)
+    prev = {}
+
+    def pipe():
+        cur = torch.cuda.current_stream()
+        sa.wait_stream(cur)
+        sb.wait_stream(cur)
+        with torch.cuda.stream(sa):
+            mel, ml = ea.acoustic(tok, tl, T, stream=sa)
+        if prev:
+            with torch.cuda.stream(sb):
+                eb.vocoder(prev["mel"], prev["ml"], out=wav, stream=sb)
+        cur.wait_stream(sa)
+        cur.wait_stream(sb)
+        prev.update(mel=mel, ml=ml)
+
+    t_p = timed(pipe)
+    t_p2 = timed(pipe)
+    ref = wav.clone()
+    seq()
+    torch.cuda.synchronize()
+    print(f"C3 ms per 32-utterance step: pipe {t_p:.3f} / {t_p2:.3f} (same waveform as seq: {bool(torch.equal(ref, wav))})")
+    ea.close()
+    eb.close()
     for k in [int(x) for x in os.environ.get("PROBE_K", "3,4").split(",") if x]:
         cuts = [B * i // k for i in range(k + 1)]
         parts = [slice(cuts[i], cuts[i + 1]) for i in range(k)]
@@ -106,6 +134,7 @@ def main():
         print(f"C3 ms per 32-utterance step: conc{k} {t_k:.3f} / {t_k2:.3f} ({[sl.stop - sl.start for sl in parts]})")
         for e in engs:
             e.close()
+    e1.close()
 
 
 if __name__ == "__main__":

@@ -204,3 +204,47 @@ def test_c4_sharded_batch256_matches_solo_and_oracle():
         check(f"C4.wav[u={u}, N={L}] bf16 frames {w0}-{w1}", out[u][w0 * HOP:w1 * HOP],
               oracle_window(ref["mel"], w0, w1, vw), kind="e2e_bf16")
     m.engine.close()
+
+
+def test_c3_pipelined_form_matches_one_stream():
+    """bench.py's pipelined C3 form -- each step runs batch k's acoustic pass (engine A, stream a)
+    beside batch k-1's vocoder (engine B, stream b) -- writes the same waveform bits as the
+    one-stream step, for batches that differ from step to step."""
+    B, N, dur = 4, 32, 6
+    T = N * dur
+    aw, vw = make_acoustic_weights(seed=0, fixed_duration=dur), make_vocoder_weights(seed=0)
+    engs = []
+    for _ in range(2):
+        e = HipEngine(DEV, vocoder_dtype="bf16", acoustic_dtype="bf16", max_batch=B, max_frames=T, max_tokens=N)
+        e.load_weights(vocoder=vw, acoustic=aw)
+        engs.append(e)
+    ea, eb = engs
+    g = torch.Generator(device="cpu").manual_seed(11)
+    toks = [torch.randint(1, 78, (B, N), generator=g, dtype=torch.int32).to(DEV) for _ in range(3)]
+    tl = torch.full((B,), N, dtype=torch.int32, device=DEV)
+    ref = []
+    for tok in toks:
+        mel, ml = ea.acoustic(tok, tl, T)
+        ref.append(ea.vocoder(mel, ml).clone())
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    outs, prev = [], None
+    for tok in toks + [None]:
+        cur = torch.cuda.current_stream()
+        sa.wait_stream(cur)
+        sb.wait_stream(cur)
+        nxt = None
+        if tok is not None:
+            with torch.cuda.stream(sa):
+                nxt = ea.acoustic(tok, tl, T, stream=sa)
+        if prev is not None:
+            with torch.cuda.stream(sb):
+                outs.append(eb.vocoder(prev[0], prev[1], stream=sb))
+        cur.wait_stream(sa)
+        cur.wait_stream(sb)
+        prev = nxt
+    torch.cuda.synchronize()
+    for e in engs:
+        e.close()
+    assert len(outs) == len(ref)
+    for o, r in zip(outs, ref):
+        assert torch.equal(o, r)
